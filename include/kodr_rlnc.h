@@ -1,0 +1,205 @@
+/*
+ * kodr_rlnc.h -- C ABI of the MI355X-native RLNC engine (libkodr_rlnc.so).
+ *
+ * This is the drop-in boundary for kodr's full/ and systematic/ packages
+ * (reference: itzmeanjan/kodr, paths relative to its checkout).  kodr is pure
+ * Go with no FFI layer of its own; each entry point below is what a cgo
+ * binding of that package would call in place of the Go method body named
+ * next to it (INTEGRATION.md shows the Go side).  All arithmetic is GF(2^8)
+ * with kodr's field (poly 0x11D, generator 2; gf256.go:15-44) and every result
+ * is bit-identical to kodr's on the same input bytes and coding vectors.
+ *
+ * Conventions
+ *  - Return value: 0 = OK; 1..12 = kodr's sentinel errors in the order of
+ *    errors.go:6-17 (RLNC_ERR_*); negative = engine/HIP failures.
+ *  - Host pointers are borrowed for the duration of the call only; the engine
+ *    copies what it keeps (cgo pointer rule).  Nothing is aliased, unlike
+ *    kodr's encoder (data.go:121-128) and decoder (decoder_state.go:205-208).
+ *  - "*_device" entry points take device pointers, enqueue on the context's
+ *    stream and return without synchronising.  All others are synchronous.
+ *  - A handle is not thread-safe (kodr's types are not goroutine-safe either):
+ *    one handle per thread.
+ *  - Coding vectors are supplied by the caller (kodr draws them from
+ *    crypto/rand, data.go:90-95); rlnc_random_bytes() is provided for callers
+ *    without an RNG.  The wire layout of a coded piece is vector ++ piece
+ *    (CodedPiece.Flatten, data.go:52-57).
+ */
+#ifndef KODR_RLNC_H
+#define KODR_RLNC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: errors.go:6-17, same order ------------------------- */
+#define RLNC_OK                                   0
+#define RLNC_ERR_CANNOT_INVERT_GF256_ADD_IDENTITY 1  /* errors.go:6  */
+#define RLNC_ERR_MATRIX_DIMENSION_MISMATCH        2  /* errors.go:7  */
+#define RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED       3  /* errors.go:8  */
+#define RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED      4  /* errors.go:9  */
+#define RLNC_ERR_COPY_FAILED_DURING_PIECE_CONSTRUCTION 5 /* errors.go:10 */
+#define RLNC_ERR_PIECE_COUNT_MORE_THAN_TOTAL_BYTES 6 /* errors.go:11 */
+#define RLNC_ERR_ZERO_PIECE_SIZE                  7  /* errors.go:12 */
+#define RLNC_ERR_BAD_PIECE_COUNT                  8  /* errors.go:13 */
+#define RLNC_ERR_CODED_DATA_LENGTH_MISMATCH       9  /* errors.go:14 */
+#define RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH    10 /* errors.go:15 */
+#define RLNC_ERR_PIECE_NOT_DECODED_YET            11 /* errors.go:16 */
+#define RLNC_ERR_PIECE_OUT_OF_BOUND               12 /* errors.go:17 */
+/* engine errors (no kodr counterpart) */
+#define RLNC_ERR_INVALID_ARGUMENT                 -1
+#define RLNC_ERR_OUT_OF_MEMORY                    -2
+#define RLNC_ERR_HIP                              -3
+#define RLNC_ERR_NO_DEVICE                        -4
+
+typedef struct rlnc_ctx rlnc_ctx;
+typedef struct rlnc_encoder rlnc_encoder;
+typedef struct rlnc_recoder rlnc_recoder;
+typedef struct rlnc_decoder rlnc_decoder;
+
+/* ---- library / context ------------------------------------------------ */
+const char* rlnc_version(void);
+const char* rlnc_status_string(int status);      /* kodr's error text for 1..12 */
+const char* rlnc_last_hip_error(void);           /* detail for RLNC_ERR_HIP (thread-local) */
+int rlnc_device_count(int* count);
+/* stream: a hipStream_t to enqueue on, or NULL for a stream owned by the ctx */
+int rlnc_ctx_create(int device, void* stream, rlnc_ctx** out);
+int rlnc_ctx_destroy(rlnc_ctx* ctx);
+int rlnc_ctx_synchronize(rlnc_ctx* ctx);
+void* rlnc_ctx_stream(rlnc_ctx* ctx);            /* the hipStream_t in use */
+int rlnc_random_bytes(uint8_t* out, size_t n);   /* getrandom(2): crypto/rand stand-in */
+
+/* device memory helpers (plumbing for device-resident callers and benches) */
+int rlnc_dev_alloc(rlnc_ctx* ctx, size_t bytes, void** dptr);
+int rlnc_dev_free(rlnc_ctx* ctx, void* dptr);
+int rlnc_memcpy_h2d(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
+int rlnc_memcpy_d2h(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
+int rlnc_memcpy_d2d_async(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* stream-ordered timing: record a named mark, read elapsed ms between two */
+int rlnc_event_create(rlnc_ctx* ctx, void** ev);
+int rlnc_event_record(rlnc_ctx* ctx, void* ev);
+int rlnc_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);   /* syncs ev_end */
+int rlnc_event_destroy(void* ev);
+
+/* ---- piece splitting: data.go:103-166 (host only) ---------------------- */
+/* OriginalPiecesFromDataAndPieceCount (data.go:137-166) */
+int rlnc_split_by_piece_count(size_t data_len, size_t piece_count,
+                              size_t* piece_size, size_t* padding);
+/* OriginalPiecesFromDataAndPieceSize (data.go:103-132) */
+int rlnc_split_by_piece_size(size_t data_len, size_t piece_size,
+                             size_t* piece_count, size_t* padding);
+/* CodedPiecesForRecoding validation (data.go:173-193) */
+int rlnc_coded_pieces_for_recoding(size_t data_len, size_t piece_count,
+                                   size_t pieces_coded_together, size_t* coded_piece_len);
+/* CodedPiece.IsSystematic (data.go:64-84) */
+int rlnc_is_systematic(const uint8_t* vector, size_t n);
+
+/* ---- encoders: full/encoder.go, systematic/encoder.go ------------------ */
+#define RLNC_FULL        0
+#define RLNC_SYSTEMATIC  1
+/* NewFullRLNCEncoderWithPieceCount (full/encoder.go:84-93) /
+ * NewSystematicRLNCEncoderWithPieceCount (systematic/encoder.go:123-132) */
+int rlnc_encoder_create_with_piece_count(rlnc_ctx* ctx, int kind, const uint8_t* data,
+                                         size_t data_len, size_t piece_count, rlnc_encoder** out);
+/* NewFullRLNCEncoderWithPieceSize (full/encoder.go:98-107) /
+ * NewSystematicRLNCEncoderWithPieceSize (systematic/encoder.go:137-146) */
+int rlnc_encoder_create_with_piece_size(rlnc_ctx* ctx, int kind, const uint8_t* data,
+                                        size_t data_len, size_t piece_size, rlnc_encoder** out);
+/* NewFullRLNCEncoder(pieces) (full/encoder.go:76-78) / NewSystematicRLNCEncoder
+ * (systematic/encoder.go:115-117): k pieces of L bytes, row-major contiguous */
+int rlnc_encoder_create(rlnc_ctx* ctx, int kind, const uint8_t* pieces, size_t piece_count,
+                        size_t piece_size, rlnc_encoder** out);
+/* the same from a device buffer (k rows, row pitch `pitch` bytes), copied D2D */
+int rlnc_encoder_create_device(rlnc_ctx* ctx, int kind, const uint8_t* d_pieces, size_t piece_count,
+                               size_t piece_size, size_t pitch, rlnc_encoder** out);
+int rlnc_encoder_destroy(rlnc_encoder* enc);
+/* accessors: PieceCount/PieceSize/DecodableLen/CodedPieceLen/Padding (full/encoder.go:15-55) */
+size_t rlnc_encoder_piece_count(const rlnc_encoder* enc);
+size_t rlnc_encoder_piece_size(const rlnc_encoder* enc);
+size_t rlnc_encoder_decodable_len(const rlnc_encoder* enc);
+size_t rlnc_encoder_coded_piece_len(const rlnc_encoder* enc);
+size_t rlnc_encoder_padding(const rlnc_encoder* enc);
+/* device pointer of the resident generation (k rows of `pitch` bytes) */
+const uint8_t* rlnc_encoder_device_pieces(const rlnc_encoder* enc, size_t* pitch);
+/* count calls after which a systematic encoder emits coded pieces (0 for full) */
+size_t rlnc_encoder_systematic_remaining(const rlnc_encoder* enc);
+/* `count` consecutive CodedPiece() calls (full/encoder.go:61-71,
+ * systematic/encoder.go:82-109).  vectors: count x k caller-drawn bytes; a
+ * systematic encoder ignores (and overwrites with e_i) the rows it emits
+ * systematically.  out: count x (k+L) bytes in wire layout (vector ++ piece). */
+int rlnc_encoder_coded_pieces(rlnc_encoder* enc, uint8_t* vectors, size_t count, uint8_t* out);
+/* device-resident batch: d_vectors count x k (device), d_out count rows of L
+ * bytes at row pitch out_pitch (pieces only; the vectors are the caller's).
+ * Full-RLNC semantics (no systematic phase).  Async on the ctx stream. */
+int rlnc_encoder_coded_pieces_device(rlnc_encoder* enc, const uint8_t* d_vectors, size_t count,
+                                     uint8_t* d_out, size_t out_pitch);
+
+/* ---- recoder: full/recoder.go ------------------------------------------ */
+/* NewFullRLNCRecoderWithFlattenData (full/recoder.go:63-70): flat holds
+ * piece_count coded pieces (wire layout), each pieces_coded_together + L bytes */
+int rlnc_recoder_create(rlnc_ctx* ctx, const uint8_t* flat, size_t flat_len, size_t piece_count,
+                        size_t pieces_coded_together, rlnc_recoder** out);
+/* the same from a device buffer of n wire rows at row pitch `pitch` */
+int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t piece_count,
+                               size_t coded_piece_len, size_t pitch, size_t pieces_coded_together,
+                               rlnc_recoder** out);
+int rlnc_recoder_destroy(rlnc_recoder* rec);
+size_t rlnc_recoder_piece_count(const rlnc_recoder* rec);        /* n held coded pieces */
+size_t rlnc_recoder_coded_piece_len(const rlnc_recoder* rec);    /* k + L */
+/* `count` CodedPiece() calls (full/recoder.go:27-46): r = count x n caller
+ * bytes; out = count x (k+L) wire rows [r x C | sum r_i P_i] */
+int rlnc_recoder_coded_pieces(rlnc_recoder* rec, const uint8_t* r, size_t count, uint8_t* out);
+/* device-resident: d_r count x n (device), d_out count wire rows at out_pitch */
+int rlnc_recoder_coded_pieces_device(rlnc_recoder* rec, const uint8_t* d_r, size_t count,
+                                     uint8_t* d_out, size_t out_pitch);
+
+/* ---- decoder: full/decoder.go, systematic/decoder.go, decoder_state.go -- */
+/* NewFullRLNCDecoder (full/decoder.go:109-112) == NewSystematicRLNCDecoder
+ * (systematic/decoder.go:105-108).  ctx may be NULL: coefficient-side only
+ * (counters, rank, transform; no piece data), used by host-logic tests. */
+int rlnc_decoder_create(rlnc_ctx* ctx, size_t piece_count, rlnc_decoder** out);
+int rlnc_decoder_destroy(rlnc_decoder* dec);
+/* AddPiece (full/decoder.go:50-66): returns RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED
+ * once decoded.  vector: piece_count bytes; piece: L bytes (L fixed by the
+ * first piece; a different length is RLNC_ERR_INVALID_ARGUMENT). */
+int rlnc_decoder_add_piece(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
+                           const uint8_t* piece, size_t piece_len);
+/* same, with the piece bytes already on the device (copied D2D, async) */
+int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
+                                  const uint8_t* d_piece, size_t piece_len);
+/* batch of `count` wire rows (vector ++ piece) at row pitch `pitch`, host or
+ * device (is_device).  Processes pieces in order, stops at the first error;
+ * *consumed = pieces accepted (OK).  Returns the first non-OK status or OK. */
+int rlnc_decoder_add_pieces(rlnc_decoder* dec, const uint8_t* rows, size_t count, size_t pitch,
+                            int is_device, size_t* consumed);
+int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */
+size_t rlnc_decoder_required(const rlnc_decoder* dec);       /* Required  :38-40 */
+size_t rlnc_decoder_useful(const rlnc_decoder* dec);         /* rank */
+size_t rlnc_decoder_received(const rlnc_decoder* dec);
+size_t rlnc_decoder_piece_length(const rlnc_decoder* dec);   /* PieceLength :18-25 */
+size_t rlnc_decoder_piece_count(const rlnc_decoder* dec);
+/* GetPiece (full/decoder.go:77-79 -> decoder_state.go:221-261) into out (L bytes) */
+int rlnc_decoder_get_piece(rlnc_decoder* dec, size_t index, uint8_t* out);
+/* GetPieces (full/decoder.go:83-99): out = useful x L bytes */
+int rlnc_decoder_get_pieces(rlnc_decoder* dec, uint8_t* out);
+/* GetPieces into device memory: useful rows of L bytes at out_pitch (async) */
+int rlnc_decoder_get_pieces_device(rlnc_decoder* dec, uint8_t* d_out, size_t out_pitch);
+/* introspection of the mirrored decoder state (decoder_state.go:192-200):
+ * coefficient matrix (useful x piece_count) and the transform T
+ * (useful x received) with coded rows == T x received pieces */
+int rlnc_decoder_coefficients(const rlnc_decoder* dec, uint8_t* out);
+int rlnc_decoder_transform(const rlnc_decoder* dec, uint8_t* out);
+
+/* ---- raw kernel entry: Y = A (x) X over GF(2^8) ------------------------ */
+/* Y[m][j] = XOR_k mul(A[m][k], X[k][j]) for m<M, j<ncols.  A is M x K host
+ * bytes (row stride lda); X and Y are device rows at pitches ldx/ldy (multiples
+ * of 16, >= ncols).  Async on the ctx stream. */
+int rlnc_gf_matmul_device(rlnc_ctx* ctx, const uint8_t* d_A, size_t lda, size_t M, size_t K,
+                          const uint8_t* d_X, size_t ldx, uint8_t* d_Y, size_t ldy, size_t ncols);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KODR_RLNC_H */

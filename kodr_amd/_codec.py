@@ -1,0 +1,195 @@
+"""Shared encoder / recoder / decoder machinery behind full.py and systematic.py.
+
+Each object owns one C-ABI handle on a device Context.  Encoders and recoders
+draw coding vectors on the host (crypto/rand analogue, injectable) and fetch
+coded pieces from the device in batches of ``batch`` consecutive
+CodedPiece() calls; the returned sequence is exactly what one-at-a-time calls
+would return, since every piece carries its own vector.
+"""
+import ctypes
+from collections import deque
+
+import numpy as np
+
+from . import errors
+from ._lib import lib, u8
+from .device import default_context
+from .kodr_internals import CodedPiece, GenerateCodingVector
+
+FULL, SYSTEMATIC = 0, 1
+
+
+def _u8arr(b):
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+class _Encoder:
+    def __init__(self, handle, ctx, rng=None, batch=16):
+        self._h = handle
+        self._ctx = ctx
+        self._rng = rng
+        self._batch = max(1, int(batch))
+        self._queue = deque()
+
+    @classmethod
+    def _create(cls, fn, ctx, kind, buf, a, b, **kw):
+        ctx = ctx or default_context()
+        h = ctypes.c_void_p()
+        arr, p = u8(buf)
+        errors.check(fn(ctx.handle, kind, p, a, b, ctypes.byref(h)))
+        return cls(h, ctx, **kw)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rlnc_encoder_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # accessors: full/encoder.go:15-55, systematic/encoder.go:16-56
+    def PieceCount(self):
+        return lib().rlnc_encoder_piece_count(self._h)
+
+    def PieceSize(self):
+        return lib().rlnc_encoder_piece_size(self._h)
+
+    def DecodableLen(self):
+        return lib().rlnc_encoder_decodable_len(self._h)
+
+    def CodedPieceLen(self):
+        return lib().rlnc_encoder_coded_piece_len(self._h)
+
+    def Padding(self):
+        return lib().rlnc_encoder_padding(self._h)
+
+    def device_pieces(self):
+        pitch = ctypes.c_size_t()
+        ptr = lib().rlnc_encoder_device_pieces(self._h, ctypes.byref(pitch))
+        return ptr, pitch.value
+
+    def coded_pieces(self, vectors):
+        """Run len(vectors)//k consecutive CodedPiece() calls with the given
+        vectors (bytes, count*k).  Returns (vectors_used, wire_rows) as numpy
+        arrays; systematic encoders overwrite the vectors they emit as e_i."""
+        k, clen = self.PieceCount(), self.CodedPieceLen()
+        vec = np.array(_u8arr(vectors), dtype=np.uint8)
+        count = vec.size // k
+        out = np.empty(count * clen, dtype=np.uint8)
+        if count:
+            errors.check(lib().rlnc_encoder_coded_pieces(
+                self._h, vec.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), count,
+                out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return vec.reshape(count, k), out.reshape(count, clen)
+
+    def CodedPiece(self):
+        """full/encoder.go:61-71 / systematic/encoder.go:82-109."""
+        if not self._queue:
+            k = self.PieceCount()
+            vec = b"".join(GenerateCodingVector(k, self._rng) for _ in range(self._batch))
+            vecs, rows = self.coded_pieces(vec)
+            for v, r in zip(vecs, rows):
+                self._queue.append(CodedPiece(v.tobytes(), r[k:].tobytes()))
+        return self._queue.popleft()
+
+
+class _Recoder:
+    """full/recoder.go."""
+
+    def __init__(self, handle, ctx, rng=None, batch=16):
+        self._h = handle
+        self._ctx = ctx
+        self._rng = rng
+        self._batch = max(1, int(batch))
+        self._queue = deque()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rlnc_recoder_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def PieceCount(self):
+        return lib().rlnc_recoder_piece_count(self._h)
+
+    def CodedPieceLen(self):
+        return lib().rlnc_recoder_coded_piece_len(self._h)
+
+    def recode(self, r):
+        """count consecutive CodedPiece() calls with caller-supplied recoding
+        vectors r (count*n bytes) -> wire rows (count, k+L)."""
+        n, clen = self.PieceCount(), self.CodedPieceLen()
+        rv = np.array(_u8arr(r), dtype=np.uint8)
+        count = rv.size // n
+        out = np.empty(count * clen, dtype=np.uint8)
+        if count:
+            errors.check(lib().rlnc_recoder_coded_pieces(
+                self._h, rv.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), count,
+                out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out.reshape(count, clen)
+
+    def CodedPiece(self, k=None):
+        """full/recoder.go:27-46 -> CodedPiece(Vector = r x C, Piece = sum r_i P_i)."""
+        if not self._queue:
+            n = self.PieceCount()
+            r = b"".join(GenerateCodingVector(n, self._rng) for _ in range(self._batch))
+            rows = self.recode(r)
+            kk = self._k
+            for row in rows:
+                self._queue.append(CodedPiece(row[:kk].tobytes(), row[kk:].tobytes()))
+        return self._queue.popleft()
+
+
+class _Decoder:
+    """full/decoder.go (== systematic/decoder.go)."""
+
+    def __init__(self, pieceCount, ctx=None):
+        self._ctx = ctx or default_context()
+        h = ctypes.c_void_p()
+        errors.check(lib().rlnc_decoder_create(self._ctx.handle, pieceCount, ctypes.byref(h)))
+        self._h = h
+        self._k = pieceCount
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rlnc_decoder_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def PieceLength(self):  # full/decoder.go:18-25
+        return lib().rlnc_decoder_piece_length(self._h)
+
+    def IsDecoded(self):  # :32-34
+        return bool(lib().rlnc_decoder_is_decoded(self._h))
+
+    def Required(self):  # :38-40
+        return lib().rlnc_decoder_required(self._h)
+
+    def useful(self):
+        return lib().rlnc_decoder_useful(self._h)
+
+    def received(self):
+        return lib().rlnc_decoder_received(self._h)
+
+    def AddPiece(self, piece):  # :50-66
+        va, vp = u8(piece.Vector)
+        pa, pp = u8(piece.Piece)
+        errors.check(lib().rlnc_decoder_add_piece(self._h, vp, len(piece.Vector), pp, len(piece.Piece)))
+
+    def GetPiece(self, i):  # :77-79
+        L = self.PieceLength()
+        out = np.empty(max(L, 1), dtype=np.uint8)
+        errors.check(lib().rlnc_decoder_get_piece(self._h, i, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return out[:L].tobytes()
+
+    def GetPieces(self):  # :83-99
+        if not self.IsDecoded():
+            raise errors.ErrMoreUsefulPiecesRequired("not enough pieces received yet to decode")
+        L, n = self.PieceLength(), self.useful()
+        out = np.empty(max(L * n, 1), dtype=np.uint8)
+        errors.check(lib().rlnc_decoder_get_pieces(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
+        return [out[i * L:(i + 1) * L].tobytes() for i in range(n)]

@@ -1,0 +1,118 @@
+"""ctypes binding of libkodr_rlnc.so (include/kodr_rlnc.h).
+
+The shared library is built in-tree by kodr_amd/build.sh (or
+``__graft_entry__.build()``).  There is no pure-Python fallback: if the library
+is missing or no HIP device is usable, data-plane calls raise.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("KODR_RLNC_LIB", os.path.join(_HERE, "libkodr_rlnc.so"))
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_sz = ctypes.c_size_t
+_szp = ctypes.POINTER(ctypes.c_size_t)
+_vp = ctypes.c_void_p
+_vpp = ctypes.POINTER(ctypes.c_void_p)
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); mirrors include/kodr_rlnc.h one to one
+SIGNATURES = {
+    "rlnc_version": (ctypes.c_char_p, []),
+    "rlnc_status_string": (ctypes.c_char_p, [_int]),
+    "rlnc_last_hip_error": (ctypes.c_char_p, []),
+    "rlnc_device_count": (_int, [ctypes.POINTER(_int)]),
+    "rlnc_ctx_create": (_int, [_int, _vp, _vpp]),
+    "rlnc_ctx_destroy": (_int, [_vp]),
+    "rlnc_ctx_synchronize": (_int, [_vp]),
+    "rlnc_ctx_stream": (_vp, [_vp]),
+    "rlnc_random_bytes": (_int, [_u8p, _sz]),
+    "rlnc_dev_alloc": (_int, [_vp, _sz, _vpp]),
+    "rlnc_dev_free": (_int, [_vp, _vp]),
+    "rlnc_memcpy_h2d": (_int, [_vp, _vp, _vp, _sz]),
+    "rlnc_memcpy_d2h": (_int, [_vp, _vp, _vp, _sz]),
+    "rlnc_memcpy_d2d_async": (_int, [_vp, _vp, _vp, _sz]),
+    "rlnc_event_create": (_int, [_vp, _vpp]),
+    "rlnc_event_record": (_int, [_vp, _vp]),
+    "rlnc_event_elapsed_ms": (_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
+    "rlnc_event_destroy": (_int, [_vp]),
+    "rlnc_split_by_piece_count": (_int, [_sz, _sz, _szp, _szp]),
+    "rlnc_split_by_piece_size": (_int, [_sz, _sz, _szp, _szp]),
+    "rlnc_coded_pieces_for_recoding": (_int, [_sz, _sz, _sz, _szp]),
+    "rlnc_is_systematic": (_int, [_u8p, _sz]),
+    "rlnc_encoder_create_with_piece_count": (_int, [_vp, _int, _u8p, _sz, _sz, _vpp]),
+    "rlnc_encoder_create_with_piece_size": (_int, [_vp, _int, _u8p, _sz, _sz, _vpp]),
+    "rlnc_encoder_create": (_int, [_vp, _int, _u8p, _sz, _sz, _vpp]),
+    "rlnc_encoder_create_device": (_int, [_vp, _int, _vp, _sz, _sz, _sz, _vpp]),
+    "rlnc_encoder_destroy": (_int, [_vp]),
+    "rlnc_encoder_piece_count": (_sz, [_vp]),
+    "rlnc_encoder_piece_size": (_sz, [_vp]),
+    "rlnc_encoder_decodable_len": (_sz, [_vp]),
+    "rlnc_encoder_coded_piece_len": (_sz, [_vp]),
+    "rlnc_encoder_padding": (_sz, [_vp]),
+    "rlnc_encoder_device_pieces": (_vp, [_vp, _szp]),
+    "rlnc_encoder_systematic_remaining": (_sz, [_vp]),
+    "rlnc_encoder_coded_pieces": (_int, [_vp, _u8p, _sz, _u8p]),
+    "rlnc_encoder_coded_pieces_device": (_int, [_vp, _vp, _sz, _vp, _sz]),
+    "rlnc_recoder_create": (_int, [_vp, _u8p, _sz, _sz, _sz, _vpp]),
+    "rlnc_recoder_create_device": (_int, [_vp, _vp, _sz, _sz, _sz, _sz, _vpp]),
+    "rlnc_recoder_destroy": (_int, [_vp]),
+    "rlnc_recoder_piece_count": (_sz, [_vp]),
+    "rlnc_recoder_coded_piece_len": (_sz, [_vp]),
+    "rlnc_recoder_coded_pieces": (_int, [_vp, _u8p, _sz, _u8p]),
+    "rlnc_recoder_coded_pieces_device": (_int, [_vp, _vp, _sz, _vp, _sz]),
+    "rlnc_decoder_create": (_int, [_vp, _sz, _vpp]),
+    "rlnc_decoder_destroy": (_int, [_vp]),
+    "rlnc_decoder_add_piece": (_int, [_vp, _u8p, _sz, _u8p, _sz]),
+    "rlnc_decoder_add_piece_device": (_int, [_vp, _u8p, _sz, _vp, _sz]),
+    "rlnc_decoder_add_pieces": (_int, [_vp, _vp, _sz, _sz, _int, _szp]),
+    "rlnc_decoder_is_decoded": (_int, [_vp]),
+    "rlnc_decoder_required": (_sz, [_vp]),
+    "rlnc_decoder_useful": (_sz, [_vp]),
+    "rlnc_decoder_received": (_sz, [_vp]),
+    "rlnc_decoder_piece_length": (_sz, [_vp]),
+    "rlnc_decoder_piece_count": (_sz, [_vp]),
+    "rlnc_decoder_get_piece": (_int, [_vp, _sz, _u8p]),
+    "rlnc_decoder_get_pieces": (_int, [_vp, _u8p]),
+    "rlnc_decoder_get_pieces_device": (_int, [_vp, _vp, _sz]),
+    "rlnc_decoder_coefficients": (_int, [_vp, _u8p]),
+    "rlnc_decoder_transform": (_int, [_vp, _u8p]),
+    "rlnc_gf_matmul_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle of libkodr_rlnc.so."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise LibraryMissing(
+                    f"{LIB_PATH} not built: run kodr_amd/build.sh (or __graft_entry__.build())")
+            h = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = h
+    return _lib
+
+
+def u8(buf):
+    """Borrow a pointer to a bytes-like / numpy uint8 buffer (no copy when writable)."""
+    import numpy as np
+    arr = buf if isinstance(buf, np.ndarray) else np.frombuffer(bytes(buf), dtype=np.uint8)
+    if arr.dtype != np.uint8 or not arr.flags["C_CONTIGUOUS"]:
+        arr = np.ascontiguousarray(arr, dtype=np.uint8)
+    return arr, arr.ctypes.data_as(_u8p)

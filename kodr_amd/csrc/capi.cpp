@@ -1,0 +1,806 @@
+// capi.cpp -- implementation of include/kodr_rlnc.h.
+//
+// Host-side mirror of kodr's codec API (full/, systematic/, kodr_internals/)
+// over device-resident generations.  Every data-plane byte is produced by the
+// HIP kernel in gf_kernels.hip; the host only validates arguments, mirrors
+// kodr's counters / pivot decisions (decoder_core.cpp) and moves bytes.  There
+// is no CPU compute fallback: without a usable HIP device every data call
+// fails with RLNC_ERR_NO_DEVICE / RLNC_ERR_HIP.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/kodr_rlnc.h"
+#include "decoder_core.hpp"
+#include "gf_kernels.hpp"
+
+using kodr_amd::DecoderCore;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+  g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+  return (e == hipErrorNoDevice || e == hipErrorInvalidDevice) ? RLNC_ERR_NO_DEVICE : RLNC_ERR_HIP;
+}
+
+#define HIPC(expr)                                 \
+  do {                                             \
+    hipError_t _e = (expr);                        \
+    if (_e != hipSuccess) return hip_fail(_e, #expr); \
+  } while (0)
+
+constexpr size_t kPitchAlign = 256;
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+constexpr size_t kMaxDescBytes = (size_t)1 << 31;  // 32-bit buffer offsets in gf_gemm
+
+// Device buffer that only grows.
+struct DevBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return RLNC_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    HIPC(hipMalloc((void**)&p, bytes));
+    cap = bytes;
+    return RLNC_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+const char* kErrText[] = {
+    "",
+    "additive identity of Gf(2^8) i.e. 0, doesn't have a multiplicative inverse",
+    "can't perform matrix multiplication",
+    "no more pieces required for decoding",
+    "not enough pieces received yet to decode",
+    "failed to copy whole data before splitting into pieces",
+    "requested piece count > total bytes of original data",
+    "pieces can't be sized as zero byte",
+    "minimum 2 pieces required for RLNC",
+    "coded data length != coded piece count x coded piece length",
+    "coding vector length > coded piece length ( in total )",
+    "piece not decoded yet, more pieces required",
+    "requested piece index >= pieceCount ( pieces coded together )",
+};
+
+}  // namespace
+
+struct rlnc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+};
+
+struct rlnc_encoder {
+  rlnc_ctx* ctx = nullptr;
+  int kind = RLNC_FULL;
+  size_t k = 0, L = 0, pitch = 0, padding = 0;
+  size_t sys_next = 0;       // systematic/encoder.go:8 currentPieceId
+  DevBuf pieces;             // k x pitch, zero padded
+  DevBuf vecs, out;          // staging for host-pointer calls
+};
+
+struct rlnc_recoder {
+  rlnc_ctx* ctx = nullptr;
+  size_t n = 0, k = 0, clen = 0, pitch = 0;
+  DevBuf flat;               // n x pitch wire rows
+  DevBuf r, out;
+};
+
+struct rlnc_decoder {
+  rlnc_ctx* ctx = nullptr;   // may be null: coefficient side only
+  DecoderCore core;
+  size_t L = 0, pitch = 0;
+  bool have_len = false;
+  DevBuf recv;               // received pieces, row i = piece i, pitch
+  size_t recv_rows = 0;
+  DevBuf tmat;               // transform upload
+  DevBuf decoded;            // useful x pitch, valid when decoded_ready
+  DevBuf rowbuf;             // one row for partial GetPiece
+  bool decoded_ready = false;
+  std::vector<uint8_t> hT;
+  explicit rlnc_decoder(size_t k) : core(k) {}
+};
+
+namespace {
+
+int set_dev(const rlnc_ctx* ctx) {
+  if (!ctx) return RLNC_ERR_NO_DEVICE;
+  HIPC(hipSetDevice(ctx->device));
+  return RLNC_OK;
+}
+
+#define TRY(expr)              \
+  do {                         \
+    int _s = (expr);           \
+    if (_s != RLNC_OK) return _s; \
+  } while (0)
+
+// split rules of data.go:103-166
+int split_count(size_t len, size_t count, size_t* size, size_t* pad) {
+  if (count < 2) return RLNC_ERR_BAD_PIECE_COUNT;
+  if (count > len) return RLNC_ERR_PIECE_COUNT_MORE_THAN_TOTAL_BYTES;
+  const size_t ps = (len + count - 1) / count;
+  if (ps >= ps * count) return RLNC_ERR_BAD_PIECE_COUNT;
+  *size = ps;
+  *pad = count * ps - len;
+  return RLNC_OK;
+}
+
+int split_size(size_t len, size_t size, size_t* count, size_t* pad) {
+  if (size == 0) return RLNC_ERR_ZERO_PIECE_SIZE;
+  if (size >= len) return RLNC_ERR_BAD_PIECE_COUNT;
+  const size_t pc = (len + size - 1) / size;
+  *count = pc;
+  *pad = pc * size - len;
+  return RLNC_OK;
+}
+
+int gemm(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
+         size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (K * ldx >= kMaxDescBytes || (ldx % 16) || (ldy % 16) || ldx < ncols || ldy < ncols) {
+    g_last_error = "gf_gemm: unsupported layout (pitch must be a multiple of 16, K*pitch < 2^31)";
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  HIPC(kodr_amd::gf_gemm(dA, lda, M, K, dX, ldx, dY, ldy, ncols, ctx->stream));
+  return RLNC_OK;
+}
+
+int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** out) {
+  if (!ctx || !out || (kind != RLNC_FULL && kind != RLNC_SYSTEMATIC) || k == 0 || L == 0)
+    return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  rlnc_encoder* e = new (std::nothrow) rlnc_encoder;
+  if (!e) return RLNC_ERR_OUT_OF_MEMORY;
+  e->ctx = ctx;
+  e->kind = kind;
+  e->k = k;
+  e->L = L;
+  e->pitch = round_up(L, kPitchAlign);
+  if (k * e->pitch >= kMaxDescBytes) {
+    delete e;
+    g_last_error = "generation larger than 2 GiB";
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  int s = e->pieces.reserve(k * e->pitch);
+  if (s == RLNC_OK) {
+    hipError_t he = hipMemsetAsync(e->pieces.p, 0, k * e->pitch, ctx->stream);
+    if (he != hipSuccess) s = hip_fail(he, "hipMemsetAsync");
+  }
+  if (s != RLNC_OK) {
+    e->pieces.release();
+    delete e;
+    return s;
+  }
+  *out = e;
+  return RLNC_OK;
+}
+
+// upload `len` bytes of data as k rows of L bytes (last row zero padded)
+int upload_generation(rlnc_encoder* e, const uint8_t* data, size_t len) {
+  const size_t full_rows = len / e->L, tail = len - full_rows * e->L;
+  if (full_rows)
+    HIPC(hipMemcpy2DAsync(e->pieces.p, e->pitch, data, e->L, e->L, full_rows, hipMemcpyHostToDevice,
+                          e->ctx->stream));
+  if (tail)
+    HIPC(hipMemcpyAsync(e->pieces.p + full_rows * e->pitch, data + full_rows * e->L, tail,
+                        hipMemcpyHostToDevice, e->ctx->stream));
+  HIPC(hipStreamSynchronize(e->ctx->stream));
+  return RLNC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rlnc_version(void) { return "kodr_amd 0.1.0 (gfx950)"; }
+
+const char* rlnc_status_string(int s) {
+  if (s >= 0 && s <= 12) return s == 0 ? "ok" : kErrText[s];
+  switch (s) {
+    case RLNC_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case RLNC_ERR_OUT_OF_MEMORY: return "out of memory";
+    case RLNC_ERR_HIP: return "HIP runtime error";
+    case RLNC_ERR_NO_DEVICE: return "no usable HIP device";
+    default: return "unknown status";
+  }
+}
+
+const char* rlnc_last_hip_error(void) { return g_last_error.c_str(); }
+
+int rlnc_device_count(int* count) {
+  if (!count) return RLNC_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return RLNC_OK;
+}
+
+int rlnc_ctx_create(int device, void* stream, rlnc_ctx** out) {
+  if (!out) return RLNC_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  TRY(rlnc_device_count(&n));
+  if (device < 0 || device >= n) {
+    g_last_error = "device index out of range";
+    return RLNC_ERR_NO_DEVICE;
+  }
+  HIPC(hipSetDevice(device));
+  rlnc_ctx* c = new (std::nothrow) rlnc_ctx;
+  if (!c) return RLNC_ERR_OUT_OF_MEMORY;
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return hip_fail(e, "hipStreamCreate");
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return RLNC_OK;
+}
+
+int rlnc_ctx_destroy(rlnc_ctx* ctx) {
+  if (!ctx) return RLNC_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+  }
+  delete ctx;
+  return RLNC_OK;
+}
+
+int rlnc_ctx_synchronize(rlnc_ctx* ctx) {
+  TRY(set_dev(ctx));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return RLNC_OK;
+}
+
+void* rlnc_ctx_stream(rlnc_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int rlnc_random_bytes(uint8_t* out, size_t n) {
+  size_t got = 0;
+  while (got < n) {
+    ssize_t r = getrandom(out + got, n - got, 0);
+    if (r < 0) return RLNC_ERR_INVALID_ARGUMENT;
+    got += (size_t)r;
+  }
+  return RLNC_OK;
+}
+
+int rlnc_dev_alloc(rlnc_ctx* ctx, size_t bytes, void** dptr) {
+  if (!dptr) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(hipMalloc(dptr, bytes ? bytes : 1));
+  return RLNC_OK;
+}
+int rlnc_dev_free(rlnc_ctx* ctx, void* dptr) {
+  TRY(set_dev(ctx));
+  HIPC(hipFree(dptr));
+  return RLNC_OK;
+}
+int rlnc_memcpy_h2d(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  TRY(set_dev(ctx));
+  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_memcpy_d2h(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  TRY(set_dev(ctx));
+  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_memcpy_d2d_async(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  TRY(set_dev(ctx));
+  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_event_create(rlnc_ctx* ctx, void** ev) {
+  if (!ev) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(hipEventCreate((hipEvent_t*)ev));
+  return RLNC_OK;
+}
+int rlnc_event_record(rlnc_ctx* ctx, void* ev) {
+  TRY(set_dev(ctx));
+  HIPC(hipEventRecord((hipEvent_t)ev, ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_event_elapsed_ms(void* a, void* b, float* ms) {
+  if (!ms) return RLNC_ERR_INVALID_ARGUMENT;
+  HIPC(hipEventSynchronize((hipEvent_t)b));
+  HIPC(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+  return RLNC_OK;
+}
+int rlnc_event_destroy(void* ev) {
+  HIPC(hipEventDestroy((hipEvent_t)ev));
+  return RLNC_OK;
+}
+
+/* ---- splitting ---------------------------------------------------------- */
+int rlnc_split_by_piece_count(size_t len, size_t count, size_t* size, size_t* pad) {
+  if (!size || !pad) return RLNC_ERR_INVALID_ARGUMENT;
+  return split_count(len, count, size, pad);
+}
+int rlnc_split_by_piece_size(size_t len, size_t size, size_t* count, size_t* pad) {
+  if (!count || !pad) return RLNC_ERR_INVALID_ARGUMENT;
+  return split_size(len, size, count, pad);
+}
+int rlnc_coded_pieces_for_recoding(size_t len, size_t count, size_t together, size_t* cpl) {
+  if (!cpl) return RLNC_ERR_INVALID_ARGUMENT;
+  if (count == 0) return RLNC_ERR_CODED_DATA_LENGTH_MISMATCH;
+  const size_t l = len / count;                                   // data.go:174
+  if (l * count != len) return RLNC_ERR_CODED_DATA_LENGTH_MISMATCH;  // :175-177
+  if (!(together < l)) return RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH;  // :179-181
+  *cpl = l;
+  return RLNC_OK;
+}
+int rlnc_is_systematic(const uint8_t* v, size_t n) {              // data.go:64-84
+  long pos = -1;
+  for (size_t i = 0; i < n; i++) {
+    if (v[i] == 0) continue;
+    if (v[i] != 1 || pos != -1) return 0;
+    pos = (long)i;
+  }
+  return pos >= 0;
+}
+
+/* ---- encoder ------------------------------------------------------------ */
+int rlnc_encoder_create_with_piece_count(rlnc_ctx* ctx, int kind, const uint8_t* data, size_t len,
+                                         size_t count, rlnc_encoder** out) {
+  size_t size = 0, pad = 0;
+  TRY(split_count(len, count, &size, &pad));
+  if (!data) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_encoder* e = nullptr;
+  TRY(encoder_alloc(ctx, kind, count, size, &e));
+  e->padding = pad;
+  int s = upload_generation(e, data, len);
+  if (s != RLNC_OK) {
+    rlnc_encoder_destroy(e);
+    return s;
+  }
+  *out = e;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_create_with_piece_size(rlnc_ctx* ctx, int kind, const uint8_t* data, size_t len,
+                                        size_t size, rlnc_encoder** out) {
+  size_t count = 0, pad = 0;
+  TRY(split_size(len, size, &count, &pad));
+  if (!data) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_encoder* e = nullptr;
+  TRY(encoder_alloc(ctx, kind, count, size, &e));
+  e->padding = pad;
+  int s = upload_generation(e, data, len);
+  if (s != RLNC_OK) {
+    rlnc_encoder_destroy(e);
+    return s;
+  }
+  *out = e;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_create(rlnc_ctx* ctx, int kind, const uint8_t* pieces, size_t k, size_t L,
+                        rlnc_encoder** out) {
+  if (!pieces) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_encoder* e = nullptr;
+  TRY(encoder_alloc(ctx, kind, k, L, &e));
+  int s = upload_generation(e, pieces, k * L);
+  if (s != RLNC_OK) {
+    rlnc_encoder_destroy(e);
+    return s;
+  }
+  *out = e;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_create_device(rlnc_ctx* ctx, int kind, const uint8_t* d_pieces, size_t k, size_t L,
+                               size_t pitch, rlnc_encoder** out) {
+  if (!d_pieces || pitch < L) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_encoder* e = nullptr;
+  TRY(encoder_alloc(ctx, kind, k, L, &e));
+  hipError_t he = hipMemcpy2DAsync(e->pieces.p, e->pitch, d_pieces, pitch, L, k,
+                                   hipMemcpyDeviceToDevice, ctx->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+  if (he != hipSuccess) {
+    rlnc_encoder_destroy(e);
+    return hip_fail(he, "hipMemcpy2DAsync");
+  }
+  *out = e;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_destroy(rlnc_encoder* e) {
+  if (!e) return RLNC_OK;
+  (void)hipSetDevice(e->ctx->device);
+  (void)hipStreamSynchronize(e->ctx->stream);
+  e->pieces.release();
+  e->vecs.release();
+  e->out.release();
+  delete e;
+  return RLNC_OK;
+}
+
+size_t rlnc_encoder_piece_count(const rlnc_encoder* e) { return e ? e->k : 0; }
+size_t rlnc_encoder_piece_size(const rlnc_encoder* e) { return e ? e->L : 0; }
+size_t rlnc_encoder_decodable_len(const rlnc_encoder* e) { return e ? e->k * (e->k + e->L) : 0; }
+size_t rlnc_encoder_coded_piece_len(const rlnc_encoder* e) { return e ? e->k + e->L : 0; }
+size_t rlnc_encoder_padding(const rlnc_encoder* e) { return e ? e->padding : 0; }
+const uint8_t* rlnc_encoder_device_pieces(const rlnc_encoder* e, size_t* pitch) {
+  if (!e) return nullptr;
+  if (pitch) *pitch = e->pitch;
+  return e->pieces.p;
+}
+size_t rlnc_encoder_systematic_remaining(const rlnc_encoder* e) {
+  if (!e || e->kind != RLNC_SYSTEMATIC) return 0;
+  return e->k - std::min(e->sys_next, e->k);
+}
+
+int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, uint8_t* out) {
+  if (!e || (count && (!vectors || !out))) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(e->ctx));
+  const size_t k = e->k, L = e->L, clen = k + L;
+  hipStream_t st = e->ctx->stream;
+  size_t i = 0;
+  // systematic/encoder.go:83-96: the first k calls return e_id ++ copy(P_id)
+  while (i < count && e->kind == RLNC_SYSTEMATIC && e->sys_next < k) {
+    const size_t id = e->sys_next++;
+    memset(vectors + i * k, 0, k);
+    vectors[i * k + id] = 1;
+    memcpy(out + i * clen, vectors + i * k, k);
+    HIPC(hipMemcpyAsync(out + i * clen + k, e->pieces.p + id * e->pitch, L, hipMemcpyDeviceToHost, st));
+    i++;
+  }
+  // full/encoder.go:61-71 (and systematic/encoder.go:98-108) in batches
+  const size_t kBatch = 256;
+  while (i < count) {
+    const size_t B = std::min(kBatch, count - i);
+    TRY(e->vecs.reserve(B * k));
+    TRY(e->out.reserve(B * e->pitch));
+    HIPC(hipMemcpyAsync(e->vecs.p, vectors + i * k, B * k, hipMemcpyHostToDevice, st));
+    TRY(gemm(e->ctx, e->vecs.p, k, B, k, e->pieces.p, e->pitch, e->out.p, e->pitch, L));
+    HIPC(hipMemcpy2DAsync(out + i * clen + k, clen, e->out.p, e->pitch, L, B, hipMemcpyDeviceToHost, st));
+    for (size_t b = 0; b < B; b++) memcpy(out + (i + b) * clen, vectors + (i + b) * k, k);
+    HIPC(hipStreamSynchronize(st));
+    i += B;
+  }
+  HIPC(hipStreamSynchronize(st));
+  return RLNC_OK;
+}
+
+int rlnc_encoder_coded_pieces_device(rlnc_encoder* e, const uint8_t* d_vectors, size_t count,
+                                     uint8_t* d_out, size_t out_pitch) {
+  if (!e || (count && (!d_vectors || !d_out)) || out_pitch < e->L) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(e->ctx));
+  return gemm(e->ctx, d_vectors, e->k, count, e->k, e->pieces.p, e->pitch, d_out, out_pitch, e->L);
+}
+
+/* ---- recoder ------------------------------------------------------------ */
+static int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_recoder** out) {
+  if (!ctx || !out || n == 0) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  rlnc_recoder* r = new (std::nothrow) rlnc_recoder;
+  if (!r) return RLNC_ERR_OUT_OF_MEMORY;
+  r->ctx = ctx;
+  r->n = n;
+  r->k = k;
+  r->clen = clen;
+  r->pitch = round_up(clen, kPitchAlign);
+  if (n * r->pitch >= kMaxDescBytes) {
+    delete r;
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  int s = r->flat.reserve(n * r->pitch);
+  if (s == RLNC_OK) {
+    hipError_t he = hipMemsetAsync(r->flat.p, 0, n * r->pitch, ctx->stream);
+    if (he != hipSuccess) s = hip_fail(he, "hipMemsetAsync");
+  }
+  if (s != RLNC_OK) {
+    r->flat.release();
+    delete r;
+    return s;
+  }
+  *out = r;
+  return RLNC_OK;
+}
+
+int rlnc_recoder_create(rlnc_ctx* ctx, const uint8_t* flat, size_t len, size_t n, size_t together,
+                        rlnc_recoder** out) {
+  size_t clen = 0;
+  TRY(rlnc_coded_pieces_for_recoding(len, n, together, &clen));  // full/recoder.go:64-67
+  if (!flat) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_recoder* r = nullptr;
+  TRY(recoder_alloc(ctx, n, clen, together, &r));
+  hipError_t he = hipMemcpy2DAsync(r->flat.p, r->pitch, flat, clen, clen, n, hipMemcpyHostToDevice,
+                                   ctx->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+  if (he != hipSuccess) {
+    rlnc_recoder_destroy(r);
+    return hip_fail(he, "hipMemcpy2DAsync");
+  }
+  *out = r;
+  return RLNC_OK;
+}
+
+int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t n, size_t clen,
+                               size_t pitch, size_t together, rlnc_recoder** out) {
+  if (!d_flat || pitch < clen) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!(together < clen)) return RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH;
+  rlnc_recoder* r = nullptr;
+  TRY(recoder_alloc(ctx, n, clen, together, &r));
+  hipError_t he = hipMemcpy2DAsync(r->flat.p, r->pitch, d_flat, pitch, clen, n,
+                                   hipMemcpyDeviceToDevice, ctx->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+  if (he != hipSuccess) {
+    rlnc_recoder_destroy(r);
+    return hip_fail(he, "hipMemcpy2DAsync");
+  }
+  *out = r;
+  return RLNC_OK;
+}
+
+int rlnc_recoder_destroy(rlnc_recoder* r) {
+  if (!r) return RLNC_OK;
+  (void)hipSetDevice(r->ctx->device);
+  (void)hipStreamSynchronize(r->ctx->stream);
+  r->flat.release();
+  r->r.release();
+  r->out.release();
+  delete r;
+  return RLNC_OK;
+}
+
+size_t rlnc_recoder_piece_count(const rlnc_recoder* r) { return r ? r->n : 0; }
+size_t rlnc_recoder_coded_piece_len(const rlnc_recoder* r) { return r ? r->clen : 0; }
+
+int rlnc_recoder_coded_pieces(rlnc_recoder* r, const uint8_t* rv, size_t count, uint8_t* out) {
+  if (!r || (count && (!rv || !out))) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(r->ctx));
+  hipStream_t st = r->ctx->stream;
+  const size_t kBatch = 256;
+  for (size_t i = 0; i < count;) {
+    const size_t B = std::min(kBatch, count - i);
+    TRY(r->r.reserve(B * r->n));
+    TRY(r->out.reserve(B * r->pitch));
+    HIPC(hipMemcpyAsync(r->r.p, rv + i * r->n, B * r->n, hipMemcpyHostToDevice, st));
+    // wire rows in, wire rows out: [r x C | sum r_i P_i] (full/recoder.go:32-40)
+    TRY(gemm(r->ctx, r->r.p, r->n, B, r->n, r->flat.p, r->pitch, r->out.p, r->pitch, r->clen));
+    HIPC(hipMemcpy2DAsync(out + i * r->clen, r->clen, r->out.p, r->pitch, r->clen, B,
+                          hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    i += B;
+  }
+  return RLNC_OK;
+}
+
+int rlnc_recoder_coded_pieces_device(rlnc_recoder* r, const uint8_t* d_r, size_t count,
+                                     uint8_t* d_out, size_t out_pitch) {
+  if (!r || (count && (!d_r || !d_out)) || out_pitch < r->clen) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(r->ctx));
+  return gemm(r->ctx, d_r, r->n, count, r->n, r->flat.p, r->pitch, d_out, out_pitch, r->clen);
+}
+
+/* ---- decoder ------------------------------------------------------------ */
+int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
+  if (!out) return RLNC_ERR_INVALID_ARGUMENT;
+  if (ctx) TRY(set_dev(ctx));
+  rlnc_decoder* d = new (std::nothrow) rlnc_decoder(k);
+  if (!d) return RLNC_ERR_OUT_OF_MEMORY;
+  d->ctx = ctx;
+  *out = d;
+  return RLNC_OK;
+}
+
+int rlnc_decoder_destroy(rlnc_decoder* d) {
+  if (!d) return RLNC_OK;
+  if (d->ctx) {
+    (void)hipSetDevice(d->ctx->device);
+    (void)hipStreamSynchronize(d->ctx->stream);
+  }
+  d->recv.release();
+  d->tmat.release();
+  d->decoded.release();
+  d->rowbuf.release();
+  delete d;
+  return RLNC_OK;
+}
+
+namespace {
+
+int dec_store_piece(rlnc_decoder* d, const uint8_t* piece, bool dev) {
+  if (!d->ctx) return RLNC_OK;
+  const size_t row = d->core.received() - 1;
+  if (row + 1 > d->recv_rows) {
+    // grow: keep received rows, double capacity
+    size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, row + 1);
+    if (nrows * d->pitch >= kMaxDescBytes) nrows = std::max(row + 1, kMaxDescBytes / d->pitch - 1);
+    uint8_t* np = nullptr;
+    HIPC(hipMalloc((void**)&np, nrows * d->pitch));
+    HIPC(hipMemsetAsync(np, 0, nrows * d->pitch, d->ctx->stream));
+    if (d->recv.p && row)
+      HIPC(hipMemcpyAsync(np, d->recv.p, row * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
+    HIPC(hipStreamSynchronize(d->ctx->stream));
+    d->recv.release();
+    d->recv.p = np;
+    d->recv.cap = nrows * d->pitch;
+    d->recv_rows = nrows;
+  }
+  HIPC(hipMemcpyAsync(d->recv.p + row * d->pitch, piece, d->L,
+                      dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, d->ctx->stream));
+  if (!dev) HIPC(hipStreamSynchronize(d->ctx->stream));  // the host buffer is only borrowed
+  return RLNC_OK;
+}
+
+int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
+            bool dev) {
+  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  if (d->core.is_decoded()) return RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;  // full/decoder.go:52-54
+  if (!vec || vlen != d->core.piece_count() || (d->ctx && !piece)) return RLNC_ERR_INVALID_ARGUMENT;
+  if (d->have_len && plen != d->L) return RLNC_ERR_INVALID_ARGUMENT;
+  if (d->ctx) TRY(set_dev(d->ctx));
+  if (!d->have_len) {
+    d->L = plen;
+    d->pitch = round_up(std::max<size_t>(plen, 1), kPitchAlign);
+    d->have_len = true;
+  }
+  TRY(d->core.add(vec));
+  d->decoded_ready = false;
+  return dec_store_piece(d, piece, dev);
+}
+
+// decoded rows [0, rows) = T x R into dst (device, pitch dpitch)
+int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, size_t dpitch) {
+  const size_t recv = d->core.received();
+  TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
+  HIPC(hipMemcpyAsync(d->tmat.p, trows, rows * recv, hipMemcpyHostToDevice, d->ctx->stream));
+  return gemm(d->ctx, d->tmat.p, recv, rows, recv, d->recv.p, d->pitch, dst, dpitch, d->L);
+}
+
+int dec_materialize(rlnc_decoder* d) {
+  if (d->decoded_ready) return RLNC_OK;
+  const size_t rows = d->core.rank(), recv = d->core.received();
+  d->hT.resize(std::max<size_t>(rows * recv, 1));
+  d->core.copy_transform(d->hT.data(), recv);
+  TRY(d->decoded.reserve(std::max<size_t>(rows * d->pitch, 1)));
+  TRY(dec_apply(d, rows, d->hT.data(), d->decoded.p, d->pitch));
+  HIPC(hipStreamSynchronize(d->ctx->stream));
+  d->decoded_ready = true;
+  return RLNC_OK;
+}
+
+}  // namespace
+
+int rlnc_decoder_add_piece(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece,
+                           size_t plen) {
+  return dec_add(d, vec, vlen, piece, plen, false);
+}
+
+int rlnc_decoder_add_piece_device(rlnc_decoder* d, const uint8_t* vec, size_t vlen,
+                                  const uint8_t* d_piece, size_t plen) {
+  return dec_add(d, vec, vlen, d_piece, plen, true);
+}
+
+int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
+                            int is_device, size_t* consumed) {
+  if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
+  const size_t k = d->core.piece_count();
+  *consumed = 0;
+  if (pitch <= k) return RLNC_ERR_INVALID_ARGUMENT;
+  const size_t plen = d->have_len ? d->L : 0;
+  std::vector<uint8_t> vec(k);
+  for (size_t i = 0; i < count; i++) {
+    const uint8_t* row = rows + i * pitch;
+    const uint8_t* v = row;
+    if (is_device) {
+      if (d->ctx) TRY(set_dev(d->ctx));
+      HIPC(hipMemcpy(vec.data(), row, k, hipMemcpyDeviceToHost));
+      v = vec.data();
+    }
+    const size_t L = plen ? plen : pitch - k;
+    int s = dec_add(d, v, k, row + k, L, is_device != 0);
+    if (s != RLNC_OK) return s;
+    (*consumed)++;
+  }
+  return RLNC_OK;
+}
+
+int rlnc_decoder_is_decoded(const rlnc_decoder* d) { return d && d->core.is_decoded(); }
+size_t rlnc_decoder_required(const rlnc_decoder* d) { return d ? d->core.required() : 0; }
+size_t rlnc_decoder_useful(const rlnc_decoder* d) { return d ? d->core.useful() : 0; }
+size_t rlnc_decoder_received(const rlnc_decoder* d) { return d ? d->core.received() : 0; }
+size_t rlnc_decoder_piece_length(const rlnc_decoder* d) {
+  return (d && d->core.received() > 0) ? d->L : 0;  // full/decoder.go:18-25
+}
+size_t rlnc_decoder_piece_count(const rlnc_decoder* d) { return d ? d->core.piece_count() : 0; }
+
+int rlnc_decoder_get_piece(rlnc_decoder* d, size_t idx, uint8_t* out) {
+  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(d->core.piece_available(idx));  // decoder_state.go:222-256
+  if (!d->ctx) return RLNC_ERR_NO_DEVICE;
+  TRY(set_dev(d->ctx));
+  if (d->core.rank() >= d->core.piece_count()) {
+    TRY(dec_materialize(d));
+    HIPC(hipMemcpyAsync(out, d->decoded.p + idx * d->pitch, d->L, hipMemcpyDeviceToHost, d->ctx->stream));
+  } else {
+    // partial decode (:233-260): materialise the single row idx
+    const size_t recv = d->core.received();
+    d->hT.assign(d->core.t_row(idx), d->core.t_row(idx) + recv);
+    TRY(d->rowbuf.reserve(d->pitch));
+    TRY(dec_apply(d, 1, d->hT.data(), d->rowbuf.p, d->pitch));
+    HIPC(hipMemcpyAsync(out, d->rowbuf.p, d->L, hipMemcpyDeviceToHost, d->ctx->stream));
+  }
+  HIPC(hipStreamSynchronize(d->ctx->stream));
+  return RLNC_OK;
+}
+
+int rlnc_decoder_get_pieces(rlnc_decoder* d, uint8_t* out) {
+  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;  // full/decoder.go:84-86
+  if (!d->ctx) return RLNC_ERR_NO_DEVICE;
+  TRY(set_dev(d->ctx));
+  const size_t useful = d->core.useful();
+  for (size_t i = 0; i < useful; i++) TRY(d->core.piece_available(i));  // :89-96
+  TRY(dec_materialize(d));
+  HIPC(hipMemcpy2DAsync(out, d->L, d->decoded.p, d->pitch, d->L, useful, hipMemcpyDeviceToHost,
+                        d->ctx->stream));
+  HIPC(hipStreamSynchronize(d->ctx->stream));
+  return RLNC_OK;
+}
+
+int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_pitch) {
+  if (!d || !d_out) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
+  if (!d->ctx) return RLNC_ERR_NO_DEVICE;
+  if (out_pitch < d->L || out_pitch % 16) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(d->ctx));
+  const size_t rows = d->core.rank(), recv = d->core.received();
+  d->hT.resize(std::max<size_t>(rows * recv, 1));
+  d->core.copy_transform(d->hT.data(), recv);
+  TRY(dec_apply(d, rows, d->hT.data(), d_out, out_pitch));
+  // the T upload reads hT asynchronously; keep it alive until the copy is done
+  HIPC(hipStreamSynchronize(d->ctx->stream));
+  return RLNC_OK;
+}
+
+int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {
+  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  d->core.copy_coefficients(out);
+  return RLNC_OK;
+}
+
+int rlnc_decoder_transform(const rlnc_decoder* d, uint8_t* out) {
+  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  d->core.copy_transform(out, d->core.received());
+  return RLNC_OK;
+}
+
+/* ---- raw kernel ----------------------------------------------------------- */
+int rlnc_gf_matmul_device(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K,
+                          const uint8_t* dX, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (!ctx || (M && (!dA || !dX || !dY)) || lda < K) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  return gemm(ctx, dA, lda, M, K, dX, ldx, dY, ldy, ncols);
+}
+
+}  // extern "C"

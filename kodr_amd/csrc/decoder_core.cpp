@@ -1,0 +1,177 @@
+// decoder_core.cpp -- see decoder_core.hpp.  Line references are to
+// kodr_internals/matrix/decoder_state.go unless stated otherwise.
+#include "decoder_core.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+
+#include "host_gf.hpp"
+
+namespace kodr_amd {
+
+using hostgf::T;
+
+DecoderCore::DecoderCore(size_t piece_count) : k_(piece_count) {
+  ensure_tcap(std::max<size_t>(k_ + 8, 16));
+}
+
+void DecoderCore::ensure_tcap(size_t need) {
+  if (need <= tcap_) return;
+  size_t ncap = std::max(need, tcap_ * 2);
+  const size_t slots = std::max<size_t>(k_, 1);
+  const size_t w_old = k_ + tcap_, w_new = k_ + ncap;
+  std::vector<uint8_t> arena(slots * w_new, 0);
+  std::vector<uint8_t*> rows(rows_.size());
+  for (size_t i = 0; i < rows_.size(); i++) {
+    rows[i] = arena.data() + i * w_new;
+    memcpy(rows[i], rows_[i], w_old);
+  }
+  free_.clear();
+  for (size_t s = rows_.size(); s < slots; s++) free_.push_back(arena.data() + s * w_new);
+  arena_.swap(arena);
+  rows_.swap(rows);
+  tcap_ = ncap;
+  clean_.resize(slots + 1, 0);
+  dirty_.resize(slots + 1, 0);
+}
+
+// rows_[dst] ^= q * rows_[src] over coefficient columns [from, k) and all T
+// columns (the coded half in kodr is updated over its whole width, :66-73).
+void DecoderCore::axpy_row(size_t dst, size_t src, uint8_t q, size_t from) {
+  hostgf::axpy(rows_[dst] + from, rows_[src] + from, k_ - from + received_, q);
+}
+
+int DecoderCore::add(const uint8_t* vec) {
+  if (is_decoded()) return 3;                       // full/decoder.go:52-54
+  ensure_tcap(received_ + 1);
+  uint8_t* row = free_.back();                      // :205-208 (append)
+  free_.pop_back();
+  memcpy(row, vec, k_);
+  memset(row + k_, 0, tcap_);
+  row[k_ + received_] = 1;                          // T row = e_received
+  rows_.push_back(row);
+  received_++;                                      // full/decoder.go:57
+  if (!(received_ > 1)) {                           // full/decoder.go:58-61
+    useful_++;
+    clean_[0] = 0;
+    return 0;
+  }
+  rref();                                           // full/decoder.go:63
+  useful_ = rows_.size();                           // full/decoder.go:64
+  return 0;
+}
+
+// Rref (:178-182) on a state whose rows 0..R-2 are the output of the previous
+// Rref and row R-1 is the new piece.
+void DecoderCore::rref() {
+  const hostgf::Tables& t = T();
+  const size_t R = rows_.size(), last = R - 1;
+  const size_t boundary = std::min(R, k_);
+  // indices whose row changed identity or content in this forward pass
+  size_t dirty_list[4096];
+  size_t ndirty = 0;
+  std::vector<size_t> dirty_big;
+  auto mark = [&](size_t i) {
+    if (dirty_[i]) return;
+    dirty_[i] = 1;
+    if (ndirty < 4096) dirty_list[ndirty++] = i;
+    else dirty_big.push_back(i);
+  };
+
+  // ---- clean_forward (:15-76).  Every earlier row r satisfies
+  // coeffs[j][i] == 0 for j > i (the previous pass left the strict lower
+  // triangle zero and zero-row removal only shifts rows up), so in the literal
+  // pivot search (:23-35) and elimination (:51-74) the only row below i that
+  // can be non-zero in column i is the last one.
+  mark(last);
+  for (size_t i = 0; i < boundary; i++) {
+    if (rows_[i][i] == 0) {
+      if (i < last && rows_[last][i] != 0) {
+        std::swap(rows_[i], rows_[last]);           // :37-48
+        mark(i);
+      } else {
+        continue;                                   // :33-35
+      }
+    }
+    if (i < last) {
+      const uint8_t c = rows_[last][i];
+      if (c != 0) axpy_row(last, i, t.div(c, rows_[i][i]), i);  // :51-74
+    }
+  }
+
+  // ---- clean_backward (:78-134).  A column i whose pivot row survived the
+  // previous pass unchanged with a non-zero diagonal was zeroed above the
+  // diagonal then, so only the rows changed by this forward pass can be
+  // non-zero there; every other column is scanned in full, as kodr does.
+  std::sort(dirty_list, dirty_list + ndirty);
+  std::sort(dirty_big.begin(), dirty_big.end());
+  for (size_t ii = boundary; ii-- > 0;) {
+    const size_t i = ii;
+    const uint8_t d = rows_[i][i];
+    if (d == 0) continue;                           // :86-88
+    const bool full = dirty_[i] || !clean_[i];
+    if (full) {
+      for (size_t j = 0; j < i; j++) {              // :90-114
+        const uint8_t c = rows_[j][i];
+        if (c != 0) axpy_row(j, i, t.div(c, d), i);
+      }
+    } else {
+      for (size_t n = 0; n < ndirty; n++) {
+        const size_t j = dirty_list[n];
+        if (j >= i) break;
+        const uint8_t c = rows_[j][i];
+        if (c != 0) axpy_row(j, i, t.div(c, d), i);
+      }
+      for (size_t j : dirty_big) {
+        if (j >= i) break;
+        const uint8_t c = rows_[j][i];
+        if (c != 0) axpy_row(j, i, t.div(c, d), i);
+      }
+    }
+    if (d == 1) continue;                           // :116-118
+    // :120-132: coeffs[i][i] = 1, coeffs[i][j>i] *= inv, coded[i] *= inv.
+    // Columns < i of row i are zero here, so scaling from column i is exact.
+    hostgf::scale(rows_[i] + i, k_ - i + received_, t.inv(d));
+  }
+  for (size_t n = 0; n < ndirty; n++) dirty_[dirty_list[n]] = 0;
+  for (size_t j : dirty_big) dirty_[j] = 0;
+
+  // ---- remove_zero_rows (:136-165): stable removal of all-zero coefficient rows
+  size_t out = 0;
+  for (size_t i = 0; i < rows_.size(); i++) {
+    if (hostgf::all_zero(rows_[i], k_)) {
+      free_.push_back(rows_[i]);
+    } else {
+      rows_[out++] = rows_[i];
+    }
+  }
+  rows_.resize(out);
+  // a row with a non-zero diagonal after this pass has a clean column above
+  for (size_t i = 0; i < rows_.size(); i++) clean_[i] = (i < k_ && rows_[i][i] != 0) ? 1 : 0;
+}
+
+int DecoderCore::piece_available(size_t idx) const {
+  if (idx >= k_) return 12;                         // :222-224 ErrPieceOutOfBound
+  if (idx >= rows_.size()) return 11;               // :225-227 ErrPieceNotDecodedYet
+  if (rows_.size() >= k_) return 0;                 // :229-231
+  const uint8_t* c = rows_[idx];                    // :233-252
+  for (size_t i = 0; i < k_; i++) {
+    if (i == idx) {
+      if (c[i] != 1) return 11;
+    } else if (c[i] == 0) {
+      return 11;
+    }
+  }
+  return 0;
+}
+
+void DecoderCore::copy_transform(uint8_t* out, size_t ld) const {
+  for (size_t i = 0; i < rows_.size(); i++) memcpy(out + i * ld, rows_[i] + k_, received_);
+}
+
+void DecoderCore::copy_coefficients(uint8_t* out) const {
+  for (size_t i = 0; i < rows_.size(); i++) memcpy(out + i * k_, rows_[i], k_);
+}
+
+}  // namespace kodr_amd

@@ -1,0 +1,64 @@
+// decoder_core.hpp -- the coefficient side of kodr's decoder, mirrored exactly.
+//
+// kodr's DecoderState (kodr_internals/matrix/decoder_state.go) keeps the
+// augmented matrix [coeffs | coded] and, on every AddPiece, re-runs
+// clean_forward / clean_backward / remove_zero_rows over both halves.  Every
+// pivot decision it makes depends only on the coefficient half, and every row
+// operation is linear, so the coded half always equals T x R, where R are the
+// received pieces (in arrival order) and T is obtained by applying the same row
+// operations to an identity block.  DecoderCore therefore runs the elimination
+// on rows [coeffs (k) | T (received)] -- a few hundred bytes each -- and the
+// data plane computes T x R on the GPU once (gf_gemm), bit-identical to kodr's
+// in-place result, quirks included (diagonal-only pivots and rank over-count,
+// decoder_state.go:23-35,86-88; zero-row removal :136-165; first piece skips
+// RREF, full/decoder.go:58-61).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace kodr_amd {
+
+class DecoderCore {
+ public:
+  explicit DecoderCore(size_t piece_count);
+
+  // full/decoder.go:50-66 minus the data: append row `vec` (k bytes) as
+  // received piece number received(); returns 0 or kodr's
+  // ErrAllUsefulPiecesReceived (3).
+  int add(const uint8_t* vec);
+
+  bool is_decoded() const { return useful_ >= k_; }   // full/decoder.go:32-34
+  size_t required() const { return k_ - useful_; }    // full/decoder.go:38-40
+  size_t useful() const { return useful_; }
+  size_t received() const { return received_; }
+  size_t piece_count() const { return k_; }
+  size_t rank() const { return rows_.size(); }        // decoder_state.go:187-189
+
+  // decoder_state.go:221-261 availability rule for GetPiece(idx): 0 when row
+  // idx of the coded matrix may be returned, else kodr's error code.
+  int piece_available(size_t idx) const;
+
+  const uint8_t* coeff_row(size_t i) const { return rows_[i]; }
+  const uint8_t* t_row(size_t i) const { return rows_[i] + k_; }
+  // copy T (rank x received) densely into out (row stride = received)
+  void copy_transform(uint8_t* out, size_t ld) const;
+  void copy_coefficients(uint8_t* out) const;
+
+ private:
+  void rref();
+  void ensure_tcap(size_t need);
+  void axpy_row(size_t dst, size_t src, uint8_t q, size_t from);
+
+  size_t k_;
+  size_t useful_ = 0, received_ = 0;
+  size_t tcap_ = 0;                    // T columns allocated per row
+  std::vector<uint8_t> arena_;         // k_ slots of (k_ + tcap_) bytes
+  std::vector<uint8_t*> rows_;         // current rows, in kodr's row order
+  std::vector<uint8_t*> free_;         // unused slots
+  std::vector<uint8_t> clean_;         // per row index: diagonal pivot with a clean column above
+  std::vector<uint8_t> dirty_;         // per row index: row moved/changed in this forward pass
+};
+
+}  // namespace kodr_amd

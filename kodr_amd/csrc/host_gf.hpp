@@ -1,0 +1,120 @@
+// host_gf.hpp -- GF(2^8) row operations on the host, used only on the
+// coefficient side of the decoder (k x (k + received) bytes: the small matrix
+// whose elimination decides pivots; piece data never goes through here).
+// Field: kodr's gf256.go:15-44 (poly 0x11D, generator 2).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+namespace kodr_amd {
+namespace hostgf {
+
+struct Tables {
+  uint8_t log[256];
+  uint8_t exp[512];
+  uint8_t mul_lo[256][16];  // c * n       for nibble n (pshufb table)
+  uint8_t mul_hi[256][16];  // c * (n<<4)
+  Tables() {
+    unsigned x = 1;
+    for (int i = 0; i < 255; i++) {
+      exp[i] = (uint8_t)x;
+      log[x] = (uint8_t)i;
+      x <<= 1;
+      if (x & 0x100) x ^= 0x11D;
+    }
+    for (int i = 255; i < 512; i++) exp[i] = exp[i - 255];
+    log[0] = 0;
+    for (int c = 0; c < 256; c++)
+      for (int n = 0; n < 16; n++) {
+        mul_lo[c][n] = mul(c, n);
+        mul_hi[c][n] = mul(c, n << 4);
+      }
+  }
+  uint8_t mul(unsigned a, unsigned b) const {  // gf256.go:109-118
+    if (a == 0 || b == 0) return 0;
+    return exp[log[a] + log[b]];
+  }
+  uint8_t inv(unsigned a) const { return exp[255 - log[a]]; }  // gf256.go:77-86, a != 0
+  uint8_t div(unsigned a, unsigned b) const { return mul(a, inv(b)); }  // gf256.go:121-127
+};
+
+inline const Tables& T() {
+  static const Tables t;
+  return t;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) inline void axpy_avx2(uint8_t* dst, const uint8_t* src, size_t n,
+                                                       uint8_t q) {
+  const Tables& t = T();
+  const __m256i lo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)t.mul_lo[q]));
+  const __m256i hi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)t.mul_hi[q]));
+  const __m256i m = _mm256_set1_epi8(0x0f);
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    const __m256i x = _mm256_loadu_si256((const __m256i*)(src + i));
+    const __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(lo, _mm256_and_si256(x, m)),
+                                       _mm256_shuffle_epi8(hi, _mm256_and_si256(_mm256_srli_epi16(x, 4), m)));
+    _mm256_storeu_si256((__m256i*)(dst + i),
+                        _mm256_xor_si256(_mm256_loadu_si256((const __m256i*)(dst + i)), p));
+  }
+  for (; i < n; i++) dst[i] ^= t.mul(src[i], q);
+}
+__attribute__((target("avx2"))) inline void scale_avx2(uint8_t* row, size_t n, uint8_t q) {
+  const Tables& t = T();
+  const __m256i lo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)t.mul_lo[q]));
+  const __m256i hi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)t.mul_hi[q]));
+  const __m256i m = _mm256_set1_epi8(0x0f);
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32) {
+    const __m256i x = _mm256_loadu_si256((const __m256i*)(row + i));
+    _mm256_storeu_si256((__m256i*)(row + i),
+                        _mm256_xor_si256(_mm256_shuffle_epi8(lo, _mm256_and_si256(x, m)),
+                                         _mm256_shuffle_epi8(hi, _mm256_and_si256(_mm256_srli_epi16(x, 4), m))));
+  }
+  for (; i < n; i++) row[i] = t.mul(row[i], q);
+}
+inline bool have_avx2() {
+  static const bool h = __builtin_cpu_supports("avx2");
+  return h;
+}
+#endif
+
+// dst[0..n) ^= q * src[0..n)
+inline void axpy(uint8_t* dst, const uint8_t* src, size_t n, uint8_t q) {
+  if (q == 0 || n == 0) return;
+#if defined(__x86_64__)
+  if (have_avx2()) return axpy_avx2(dst, src, n, q);
+#endif
+  const Tables& t = T();
+  for (size_t i = 0; i < n; i++) dst[i] ^= t.mul(src[i], q);
+}
+
+// row[0..n) *= q
+inline void scale(uint8_t* row, size_t n, uint8_t q) {
+#if defined(__x86_64__)
+  if (have_avx2()) return scale_avx2(row, n, q);
+#endif
+  const Tables& t = T();
+  for (size_t i = 0; i < n; i++) row[i] = t.mul(row[i], q);
+}
+
+inline bool all_zero(const uint8_t* p, size_t n) {
+  size_t i = 0;
+  uint64_t acc = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, p + i, 8);
+    acc |= w;
+  }
+  for (; i < n; i++) acc |= p[i];
+  return acc == 0;
+}
+
+}  // namespace hostgf
+}  // namespace kodr_amd

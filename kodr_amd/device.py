@@ -1,0 +1,90 @@
+"""Device context: one HIP device + one stream (rlnc_ctx)."""
+import ctypes
+
+from . import errors
+from ._lib import lib
+
+
+class Context:
+    """Wraps rlnc_ctx_create(device, stream).  ``stream`` may be a raw
+    hipStream_t (int) so that work lands on a caller's stream, e.g.
+    ``torch.cuda.current_stream().cuda_stream``."""
+
+    def __init__(self, device=0, stream=None):
+        h = ctypes.c_void_p()
+        errors.check(lib().rlnc_ctx_create(device, ctypes.c_void_p(stream or 0), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        return lib().rlnc_ctx_stream(self._h)
+
+    def synchronize(self):
+        errors.check(lib().rlnc_ctx_synchronize(self._h))
+
+    def close(self):
+        if self._h:
+            lib().rlnc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device memory plumbing (for device-resident callers / benches)
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        errors.check(lib().rlnc_dev_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, ptr):
+        errors.check(lib().rlnc_dev_free(self._h, ctypes.c_void_p(ptr)))
+
+    def h2d(self, dptr, host):
+        import numpy as np
+        a = np.ascontiguousarray(host, dtype=np.uint8)
+        errors.check(lib().rlnc_memcpy_h2d(self._h, ctypes.c_void_p(dptr),
+                                           a.ctypes.data_as(ctypes.c_void_p), a.nbytes))
+
+    def d2h(self, dptr, nbytes):
+        import numpy as np
+        out = np.empty(nbytes, dtype=np.uint8)
+        errors.check(lib().rlnc_memcpy_d2h(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                           ctypes.c_void_p(dptr), nbytes))
+        return out
+
+    def event(self):
+        e = ctypes.c_void_p()
+        errors.check(lib().rlnc_event_create(self._h, ctypes.byref(e)))
+        return e
+
+    def record(self, ev):
+        errors.check(lib().rlnc_event_record(self._h, ev))
+
+    @staticmethod
+    def elapsed_ms(a, b):
+        ms = ctypes.c_float()
+        errors.check(lib().rlnc_event_elapsed_ms(a, b, ctypes.byref(ms)))
+        return ms.value
+
+
+_default = {}
+
+
+def default_context(device=0):
+    if device not in _default:
+        _default[device] = Context(device)
+    return _default[device]
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    st = lib().rlnc_device_count(ctypes.byref(n))
+    return n.value if st == 0 else 0

@@ -1,0 +1,238 @@
+"""CPU tests of libkodr_rlnc.so: it loads, exports every symbol of
+include/kodr_rlnc.h, and its host logic matches kodr:
+
+- splitting / validation rules (data.go:103-193) vs the golden vectors;
+- the mirrored decoder state (decoder_state.go + full/decoder.go) run
+  coefficient-side only (ctx = NULL, no GPU): per-AddPiece counters, errors and
+  coefficient matrix equal the oracle's literal restatement, and the tracked
+  transform T satisfies  T x received == the oracle's coded rows  exactly, on
+  the golden streams and on randomized / adversarial streams.
+
+No data-plane compute is called here (that needs the GPU: test_gpu_*.py).
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from kodr_amd import _lib, errors
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ERR = {None: 0, **{name: cls.code for name, cls in errors.BY_NAME.items()}}
+
+
+def h(s):
+    return np.frombuffer(bytes.fromhex(s), dtype=np.uint8)
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "kodr_rlnc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rlnc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) > 50
+    for s in syms:
+        assert hasattr(lib, s), s
+    # the ctypes binding declares exactly the header's entry points
+    assert sorted(_lib.SIGNATURES) == syms
+
+
+def test_exported_symbols_via_nm():
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rlnc_\w+)", out))
+    assert set(header_symbols()) <= exported
+
+
+def test_library_does_not_link_oracle():
+    import subprocess
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    nm = subprocess.run(["nm", "-D", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle_" not in nm
+
+
+def test_status_strings_match_errors_go():
+    lib = _lib.lib()
+    assert lib.rlnc_status_string(3).decode() == "no more pieces required for decoding"
+    assert lib.rlnc_status_string(12).decode().startswith("requested piece index >= pieceCount")
+    for name, code in ERR.items():
+        if name:
+            assert errors.BY_CODE[code].__name__ == name
+
+
+def test_split_rules(golden):
+    lib = _lib.lib()
+    for c in golden["vectors"]["split_count"]:
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        st = lib.rlnc_split_by_piece_count(c["len"], c["count"], ctypes.byref(a), ctypes.byref(b))
+        assert st == ERR[c["err"]], c
+        if st == 0:
+            assert (a.value, b.value) == (c["piece_size"], c["padding"])
+    for c in golden["vectors"]["split_size"]:
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        st = lib.rlnc_split_by_piece_size(c["len"], c["size"], ctypes.byref(a), ctypes.byref(b))
+        assert st == ERR[c["err"]], c
+        if st == 0:
+            assert (a.value, b.value) == (c["piece_count"], c["padding"])
+
+
+def test_coded_pieces_for_recoding_rules():
+    # data_test.go:88-134 shapes: 5 coded pieces of 3+2 bytes
+    lib = _lib.lib()
+    n = ctypes.c_size_t()
+    assert lib.rlnc_coded_pieces_for_recoding(25, 3, 3, ctypes.byref(n)) == ERR["ErrCodedDataLengthMismatch"]
+    assert lib.rlnc_coded_pieces_for_recoding(25, 5, 5, ctypes.byref(n)) == ERR["ErrCodingVectorLengthMismatch"]
+    assert lib.rlnc_coded_pieces_for_recoding(25, 5, 3, ctypes.byref(n)) == 0 and n.value == 5
+
+
+def test_is_systematic(golden):
+    lib = _lib.lib()
+    for c in golden["kats"]["is_systematic"]:
+        a, p = _lib.u8(bytes(c["vector"]))
+        assert bool(lib.rlnc_is_systematic(p, a.size)) == c["expected"]
+
+
+class CoreDecoder:
+    """rlnc_decoder with ctx = NULL: the coefficient side only."""
+
+    def __init__(self, k):
+        self.lib = _lib.lib()
+        self.h = ctypes.c_void_p()
+        assert self.lib.rlnc_decoder_create(None, k, ctypes.byref(self.h)) == 0
+        self.k = k
+
+    def __del__(self):
+        self.lib.rlnc_decoder_destroy(self.h)
+
+    def add(self, vec):
+        a, p = _lib.u8(vec)
+        return self.lib.rlnc_decoder_add_piece(self.h, p, a.size, None, 0)
+
+    def state(self):
+        L = self.lib
+        return (L.rlnc_decoder_useful(self.h), L.rlnc_decoder_received(self.h),
+                L.rlnc_decoder_required(self.h), bool(L.rlnc_decoder_is_decoded(self.h)))
+
+    def coefficients(self):
+        r = self.lib.rlnc_decoder_useful(self.h)
+        out = np.empty((r, self.k), np.uint8)
+        if r:
+            self.lib.rlnc_decoder_coefficients(self.h, out.ctypes.data_as(_lib._u8p))
+        return out
+
+    def transform(self):
+        r, n = self.lib.rlnc_decoder_useful(self.h), self.lib.rlnc_decoder_received(self.h)
+        out = np.empty((r, n), np.uint8)
+        if r:
+            self.lib.rlnc_decoder_transform(self.h, out.ctypes.data_as(_lib._u8p))
+        return out
+
+
+def check_stream(k, stream, strict_steps=None):
+    """Feed (vec, piece) pairs to the C-ABI core and to the oracle; compare."""
+    core, ref = CoreDecoder(k), oracle.Decoder(k)
+    accepted = []
+    for n, (v, p) in enumerate(stream):
+        st_ref = ref.add(v, p)
+        st = core.add(v)
+        assert st == st_ref, n
+        if st == 0:
+            accepted.append(np.asarray(p, np.uint8))
+        assert core.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded()), n
+        if strict_steps is not None:
+            s = strict_steps[n]
+            assert core.state() == (s["useful"], s["received"], s["required"], s["decoded"])
+        if core.state()[0] == 0 or st != 0:
+            continue
+        # coefficient halves identical; data half == T x R exactly
+        assert np.array_equal(core.coefficients(), ref.coeffs()), n
+        T = core.transform()
+        R = np.stack(accepted)
+        st_m, TR = oracle.matmul(T, R)
+        assert st_m == 0
+        assert np.array_equal(TR, ref.coded()), n
+    return core, ref
+
+
+def test_core_matches_oracle_on_golden_streams(golden):
+    for c in golden["vectors"]["decode"]:
+        stream = [(h(v), h(p)) for v, p in c["stream"]]
+        check_stream(c["k"], stream, c["steps"])
+
+
+def _random_stream(rng, k, L, n, kind):
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    out = []
+    for i in range(n):
+        if kind == "dense":
+            v = rng.integers(0, 256, k, dtype=np.uint8)
+        elif kind == "sparse":
+            v = (rng.integers(0, 256, k) * (rng.random(k) < 0.15)).astype(np.uint8)
+        elif kind == "tiny_field":  # many zeros / duplicates / dependencies
+            v = rng.integers(0, 3, k, dtype=np.uint8)
+        elif kind == "systematic":
+            v = np.zeros(k, np.uint8)
+            if rng.random() < 0.6:
+                v[rng.integers(0, k)] = 1
+            else:
+                v[:] = rng.integers(0, 256, k)
+        elif kind == "lowrank":  # combinations of only k//2 base vectors
+            base = np.random.default_rng(7).integers(0, 256, (max(1, k // 2), k), dtype=np.uint8)
+            c = rng.integers(0, 256, (1, base.shape[0]), dtype=np.uint8)
+            v = oracle.matmul(c, base)[1][0]
+        out.append((v, oracle.encode(P, v[None, :])[0]))
+    return out
+
+
+@pytest.mark.parametrize("kind", ["dense", "sparse", "tiny_field", "systematic", "lowrank"])
+@pytest.mark.parametrize("k", [2, 3, 7, 16, 33])
+def test_core_matches_oracle_randomized(kind, k):
+    rng = np.random.default_rng(1000 * k + sum(map(ord, kind)))
+    stream = _random_stream(rng, k, 8, 3 * k + 4, kind)
+    check_stream(k, stream)
+
+
+def test_core_arbitrary_rows_not_codewords():
+    # pieces inconsistent with their vectors: T-tracking must still equal
+    # kodr's in-place data rows bit for bit
+    rng = np.random.default_rng(5)
+    k = 12
+    stream = [(rng.integers(0, 4, k, dtype=np.uint8), rng.integers(0, 256, 10, dtype=np.uint8))
+              for _ in range(40)]
+    check_stream(k, stream)
+
+
+def test_core_k256_counters_only():
+    # C2 shape on the coefficient side: 256 random vectors reach full rank
+    rng = np.random.default_rng(11)
+    k = 256
+    core, ref = CoreDecoder(k), oracle.Decoder(k)
+    while not ref.is_decoded():
+        v = rng.integers(0, 256, k, dtype=np.uint8)
+        assert core.add(v) == ref.add(v, np.zeros(1, np.uint8))
+        assert core.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+    assert np.array_equal(core.coefficients(), np.eye(k, dtype=np.uint8))
+    assert core.add(rng.integers(0, 256, k, dtype=np.uint8)) == ERR["ErrAllUsefulPiecesReceived"]
+
+
+def test_core_vector_length_mismatch_is_rejected():
+    core = CoreDecoder(4)
+    a, p = _lib.u8(b"\x01\x02\x03")
+    assert _lib.lib().rlnc_decoder_add_piece(core.h, p, 3, None, 0) == -1
+
+
+def test_get_piece_without_device_reports_no_device():
+    core = CoreDecoder(2)
+    core.add(np.array([1, 0], np.uint8))
+    core.add(np.array([0, 1], np.uint8))
+    out = np.empty(4, np.uint8)
+    assert _lib.lib().rlnc_decoder_get_piece(core.h, 0, out.ctypes.data_as(_lib._u8p)) == -4
+    assert _lib.lib().rlnc_decoder_get_piece(core.h, 5, out.ctypes.data_as(_lib._u8p)) == 12
