@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Full-RLNC encode of a 32 MiB generation split into 256
+pieces (BASELINE.json configs[1]) on MI355X, device-resident, coded MB/s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gens G]
+
+One step = one pass of the hot path: B coded pieces of one resident generation
+(one gf_gemm launch: B coding vectors x the k x L generation).  The G
+generations rotate so that consecutive steps stream from HBM, not from the
+256 MiB Infinity Cache.  Metric accounting is kodr's own: each coded piece is
+worth SetBytes = S + padding + (k + L) bytes (benches/full/encoder_test.go:53),
+reported in 10^6 B/s like Go's MB/s.
+
+Multi-GPU (torchrun, one process per GPU): generations are independent, so
+every rank encodes its own G generations with no data-path collective (weak
+scaling); value = all ranks' coded bytes / max-over-ranks time.
+
+The JSON line also carries the roofline of the dominant kernel (gf_gemm,
+timed with HIP events on the stream it runs on) and a CPU baseline: the
+kodr-equivalent scalar restatement (oracle/, one core) timed on a bounded
+sample of the same workload on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+K_PIECES, L_BYTES = 256, 131072          # 32 MiB / 256 pieces
+HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def setbytes(k, L, padding=0):
+    # benches/full/encoder_test.go:53  SetBytes(total + padding + CodedPieceLen)
+    return k * L + padding + (k + L)
+
+
+def cpu_baseline(seconds=10.0):
+    """Time oracle/ (kodr-equivalent scalar Go restatement, 1 thread) encoding
+    32 MiB/256 coded pieces for ~`seconds`."""
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(1)
+    P = rng.integers(0, 256, (K_PIECES, L_BYTES), dtype=np.uint8)
+    V = rng.integers(0, 256, (64, K_PIECES), dtype=np.uint8)
+    oracle.encode(P, V[:1])  # warm tables / pages
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle.encode(P, V[n % 64:n % 64 + 1])
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds and n >= 3:
+            break
+    return {"value": round(n * setbytes(K_PIECES, L_BYTES) / dt / 1e6, 2), "unit": "MB/s",
+            "cores": 1, "kind": "port",
+            "sample": f"{n} coded pieces of 32MiB/256 by oracle/kodr_oracle.c (scalar restatement of "
+                      f"data.go:19-29 + gf256.go:109-118), {dt:.1f}s on 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=8, help="coded pieces per encode pass")
+    ap.add_argument("--gens", type=int, default=16, help="rotating resident generations (HBM-cold)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras", action="store_true", help="also time decode / MALL-hot / host path")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # CPU baseline first, before this process touches the GPU (rank 0, N=1 only)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    import numpy as np
+    import torch  # plumbing: process group + shared HIP runtime
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+
+    from kodr_amd import device as kdev
+    from kodr_amd import errors
+    from kodr_amd._lib import lib
+
+    L_ = lib()
+    ctx = kdev.Context(local)
+    k, L, B, G = K_PIECES, L_BYTES, args.batch, args.gens
+
+    # G resident generations of 32 MiB (+ B x k vectors per step, rotating)
+    rng = np.random.default_rng(0x6B6F6472 + rank)
+    import ctypes
+    encs = []
+    for g in range(G):
+        data = rng.integers(0, 256, k * L, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        errors.check(L_.rlnc_encoder_create(ctx.handle, 0, data.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                            k, L, ctypes.byref(h)))
+        encs.append(h)
+    nvec = 64
+    V = rng.integers(0, 256, (nvec, B, k), dtype=np.uint8)
+    dV = ctx.alloc(V.nbytes)
+    ctx.h2d(dV, V)
+    dOut = ctx.alloc(B * L)
+
+    def step(i):
+        errors.check(L_.rlnc_encoder_coded_pieces_device(encs[i % G], dV + (i % nvec) * B * k, B, dOut, L))
+
+    def barrier():
+        ctx.synchronize()
+        if world > 1:
+            dist.barrier()
+        ctx.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    e0, e1 = ctx.event(), ctx.event()
+    t0 = time.perf_counter()
+    ctx.record(e0)
+    for i in range(args.steps):
+        step(i)
+    ctx.record(e1)
+    ms_dev = kdev.Context.elapsed_ms(e0, e1)
+    barrier()
+    wall = time.perf_counter() - t0
+    t_local = ms_dev / 1e3
+    if world > 1:
+        t = torch.tensor([t_local], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+    else:
+        t_max = t_local
+
+    unit_bytes = setbytes(k, L)
+    value = world * args.steps * B * unit_bytes / t_max / 1e6
+    t_launch = t_local / args.steps
+    # compulsory bytes of one launch: the generation once + B vectors + B pieces out
+    launch_bytes = k * L + B * k + B * L
+    achieved = launch_bytes / t_launch / 1e9
+
+    extras = {}
+    if args.extras and rank == 0:
+        extras = run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng)
+
+    for h in encs:
+        L_.rlnc_encoder_destroy(h)
+    ctx.free(dV)
+    ctx.free(dOut)
+
+    if rank == 0:
+        line = {
+            "metric": "coded MB/s device-resident, Full-RLNC encode+decode, 32M/256 pieces @1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "MB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded uniform random bytes and coding vectors)",
+            "config": {"workload": "Full RLNC encode, 32 MiB generation / 256 pieces (BASELINE configs[1])",
+                       "piece_count": k, "piece_size": L, "coded_pieces_per_step": B,
+                       "resident_generations": G, "parallelism": f"generation-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gf_gemm_kernel",
+                         "bytes_per_launch": launch_bytes,
+                         "avg_launch_us": round(t_launch * 1e6, 3)},
+            "cpu_baseline": cpu,
+            "wall_s": round(wall, 4),
+        }
+        if extras:
+            line["extras"] = extras
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
+    """Secondary measurements (not the headline): MALL-hot encode, full
+    decode of 32 MiB/256 from device-resident pieces, host-path encode."""
+    import ctypes
+    import numpy as np
+    from kodr_amd import device as kdev
+    out = {}
+    # MALL-hot: one generation re-read every step
+    e0, e1 = ctx.event(), ctx.event()
+    for i in range(10):
+        L_.rlnc_encoder_coded_pieces_device(encs[0], dV, B, dOut, L)
+    ctx.record(e0)
+    for i in range(100):
+        errors.check(L_.rlnc_encoder_coded_pieces_device(encs[0], dV, B, dOut, L))
+    ctx.record(e1)
+    t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / 100
+    out["encode_mall_hot_MBps"] = round(B * setbytes(k, L) / t / 1e6, 1)
+    # decode: k + 2 coded pieces encoded on device, then AddPiece x n + GetPieces
+    n = k + 2
+    Vd = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    dVd, dCoded, dDec = ctx.alloc(Vd.nbytes), ctx.alloc(n * L), ctx.alloc(k * L)
+    ctx.h2d(dVd, Vd)
+    errors.check(L_.rlnc_encoder_coded_pieces_device(encs[0], dVd, n, dCoded, L))
+    ctx.synchronize()
+    times = []
+    for rep in range(3):
+        dh = ctypes.c_void_p()
+        errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
+        t0 = time.perf_counter()
+        for i in range(n):
+            v = np.ascontiguousarray(Vd[i])
+            st = L_.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), k,
+                                                  dCoded + i * L, L)
+            if st == 3:
+                break
+            errors.check(st)
+        errors.check(L_.rlnc_decoder_get_pieces_device(dh, dDec, L))
+        ctx.synchronize()
+        times.append(time.perf_counter() - t0)
+        L_.rlnc_decoder_destroy(dh)
+    td = min(times)
+    out["decode_s"] = round(td, 6)
+    out["decode_MBps_decodable_len"] = round(k * (k + L) / td / 1e6, 1)
+    out["decode_gf_macs_per_s"] = float(f"{k * k * L / td:.4g}")
+    # verify the decode of the first generation against the resident pieces
+    ptr_p, pitch = ctypes.c_size_t(), ctypes.c_size_t()
+    dp = L_.rlnc_encoder_device_pieces(encs[0], ctypes.byref(pitch))
+    a = ctx.d2h(dDec, k * L)
+    b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
+    out["decode_roundtrip_ok"] = bool(np.array_equal(a, b))
+    ctx.free(dVd)
+    ctx.free(dCoded)
+    ctx.free(dDec)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -6,7 +6,7 @@ cd "$HERE"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 ARCH="${KODR_ARCH:-gfx950}"
 mkdir -p build
-FLAGS=(-O3 -std=c++17 -fPIC -Wall -Wno-unused-function)
+FLAGS=(-O3 -std=c++17 -fPIC -Wall -Wno-unused-function ${KODR_EXTRA_FLAGS:-})
 pids=()
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_kernels.hip -o build/gf_kernels.o & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c csrc/capi.cpp -o build/capi.o & pids+=($!)

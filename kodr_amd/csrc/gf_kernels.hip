@@ -24,6 +24,8 @@
 // wave-uniform broadcasts.  No MFMA: this is byte-field arithmetic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "gf_kernels.hpp"
 
@@ -48,9 +50,7 @@ __device__ __forceinline__ void make_tables(uint32_t c, uint4& t01, uint32_t& t2
   t2 = (c64 << 8) | (c128 << 16) | ((c64 ^ c128) << 24);
 }
 
-constexpr int kLanes = 64;
-constexpr int kLaneBytes = 16;                    // one dwordx4 per lane per row
-constexpr int kChunkBytes = kLanes * kLaneBytes;  // 1 KiB of columns per wave
+constexpr int kLaneBytes = 16;  // one dwordx4 per lane per row
 
 // Workgroup barrier that waits only for LDS traffic: HIP's __syncthreads()
 // also drains vmcnt, which would empty the row-prefetch ring at every K-chunk.
@@ -58,33 +58,38 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ uint4 zero4() { return make_uint4(0u, 0u, 0u, 0u); }
-
-// One workgroup = CW column chunks x KW K-slices, one wave each, MT output rows.
-//  - KW > 1 (encode/recode, small M): KW waves share one 1 KiB column chunk and
-//    split every K-chunk of KC = KW*RC rows; partial sums are XOR-reduced in LDS.
-//  - CW > 1 (decode, large M): CW waves own CW adjacent column chunks and
-//    share the coefficient tables of the MT rows.
-// Coefficient tables are staged per K-chunk into LDS (double-buffered when
-// K > KC) and read back as wave-uniform broadcasts.  Each wave streams its rows
-// through a P-deep ring of dwordx4 loads that runs across K-chunk barriers.
-template <int MT, int KW, int CW, int RC, int P>
-__global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
+// Tile: MT output rows x one column chunk of CB = 1024/S bytes per workgroup.
+//  - The KW waves of a workgroup split K; each K-chunk of KC = KW*RC rows gives
+//    wave w the rows [w*RC, (w+1)*RC).
+//  - Inside a wave the 64 lanes form S groups of 64/S lanes; in one row-step
+//    group g reads row (base + g) over the chunk, so every load is still a
+//    16-byte-per-lane dwordx4 while the chunk narrows to 1024/S bytes (more
+//    workgroups, all CUs streaming, nothing read twice).
+//  - Partial sums: across the S lane groups by __shfl_xor, across the KW waves
+//    by ds_xor in LDS.
+// Coefficient tables for (MT x KC) are staged per K-chunk into LDS
+// (double-buffered when K > KC) and read back as (S-way) broadcasts.  Rows are
+// streamed through a P-deep ring of loads that runs across K-chunk barriers.
+template <int MT, int KW, int S, int RC, int P, int MODE = 0>
+__global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K,
     const uint8_t* __restrict__ X, size_t ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int nx, int ny, int nbuf) {
-  static_assert(KW == 1 || CW == 1, "split K or columns, not both");
-  static_assert(RC % P == 0 && P % 2 == 0, "ring depth: even, divides rows per chunk");
+  static_assert(S == 1 || S == 2 || S == 4, "lane groups");
+  static_assert(RC % (S * P) == 0, "ring: P row-steps of S rows must divide RC");
   constexpr int KC = KW * RC;
-  constexpr int NT = 64 * KW * CW;
+  constexpr int NT = 64 * KW;
+  constexpr int GL = 64 / S;             // lanes per group
+  constexpr int CB = GL * kLaneBytes;    // chunk bytes
+  constexpr int STEPS = RC / S;          // row-steps per wave per K-chunk
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint4* tab01 = reinterpret_cast<uint4*>(smem);                         // [nbuf][KC][MT]
   uint32_t* tab2 = reinterpret_cast<uint32_t*>(tab01 + nbuf * KC * MT);  // [nbuf][KC][MT]
-  uint32_t* red = tab2 + nbuf * KC * MT;                                  // [MT][4][64]
+  uint32_t* red = tab2 + nbuf * KC * MT;                                  // [MT][4][GL]
 
   // XCD-aware block order: blocks b and b+8 share an XCD under round-robin
-  // dispatch, so the ny row-tiles of one column group are dealt to one XCD
-  // back to back and re-read those columns from its L2.  Speed only.
+  // dispatch, so the ny row-tiles of one column chunk are dealt to one XCD
+  // back to back and re-read that chunk from its L2.  Speed only.
   const int b = blockIdx.x;
   const int ty = (b >> 3) % ny;
   const int tx = (b / (8 * ny)) * 8 + (b & 7);
@@ -94,34 +99,66 @@ __global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = tid >> 6;
-  const int kw = (KW > 1) ? w : 0;
-  const int cw = (CW > 1) ? w : 0;
-  const int col = (tx * CW + cw) * kChunkBytes + lane * kLaneBytes;
+  const int g = lane / GL;
+  const int li = lane % GL;
+  const int col = tx * CB + li * kLaneBytes;
 
-  auto build = [&](int c, int buf) {
-    for (int idx = tid; idx < KC * MT; idx += NT) {
-      const int kk = idx / MT, m = idx - kk * MT;
-      const int k = c * KC + kk, mm = m0 + m;
-      const uint32_t coef = (k < K && mm < M) ? A[(size_t)mm * lda + k] : 0u;
-      uint4 t01;
-      uint32_t t2;
-      make_tables(coef, t01, t2);
-      tab01[(buf * KC + kk) * MT + m] = t01;
-      tab2[(buf * KC + kk) * MT + m] = t2;
-    }
-  };
-  // row q of this wave's flat sequence -> matrix row k.  X is read through a
-  // buffer descriptor: rows k >= K fall outside num_records and load as zero,
-  // so the stream needs no branches (columns >= ncols are loaded but never
-  // stored).
+  // X through a buffer descriptor: rows k >= K lie outside num_records and
+  // load as zero, so the stream needs no branches (columns >= ncols are
+  // loaded but never stored).
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)K * ldx), 0x00020000);
   const int ildx = (int)ldx;
-  auto load_row = [&](int q) -> uint4 {
-    const int k = (q / RC) * KC + kw * RC + (q % RC);
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, k * ildx + col, 0, 0);
+  // row-step q of this wave (flat over K-chunks) -> row index of group g
+  auto row_of = [&](int q) { return (q / STEPS) * KC + w * RC + (q % STEPS) * S + g; };
+  auto load_step = [&](int q) -> uint4 {
+    if (MODE == 2) {  // tuning: no memory traffic
+      const uint32_t h = (uint32_t)(row_of(q) * 0x9E3779B1u) ^ (uint32_t)col;
+      return make_uint4(h, h * 3u, h * 5u, h * 7u);
+    }
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, row_of(q) * ildx + col, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
   };
+
+  // Coefficient tables of one K-chunk: thread t builds entries t + j*NT of the
+  // (KC x MT) chunk.  Loading and building are split so that chunk 0's
+  // coefficient bytes are requested BEFORE the row ring: vmcnt retires loads
+  // in issue order, so waiting for the coefficients then does not wait for the
+  // HBM-latency rows, and table building overlaps the row stream.
+  constexpr int NB = (KC * MT + NT - 1) / NT;
+  auto load_coefs = [&](int c, uint32_t (&cf)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      const int idx = tid + j * NT;
+      const int kk = idx / MT, m = idx % MT;
+      const int k = c * KC + kk, mm = m0 + m;
+      cf[j] = (idx < KC * MT && k < K && mm < M) ? A[(size_t)mm * lda + k] : 0u;
+    }
+  };
+  auto store_tables = [&](int buf, const uint32_t (&cf)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      const int idx = tid + j * NT;
+      if (idx < KC * MT) {
+        uint4 t01;
+        uint32_t t2;
+        make_tables(cf[j], t01, t2);
+        tab01[buf * KC * MT + idx] = t01;
+        tab2[buf * KC * MT + idx] = t2;
+      }
+    }
+  };
+
+  uint32_t cf[NB];
+  load_coefs(0, cf);
+  __builtin_amdgcn_sched_barrier(0);
+  uint4 ring[P];
+#pragma unroll
+  for (int j = 0; j < P; j++) ring[j] = load_step(j);
+  __builtin_amdgcn_sched_barrier(0);
+  store_tables(0, cf);
+  if (KW > 1)
+    for (int i = tid; i < MT * 4 * GL; i += NT) red[i] = 0u;
 
   uint32_t acc[MT][4];
 #pragma unroll
@@ -129,28 +166,32 @@ __global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
 #pragma unroll
     for (int d = 0; d < 4; d++) acc[m][d] = 0u;
 
-  if (KW > 1)
-    for (int i = tid; i < MT * 4 * 64; i += NT) red[i] = 0u;
-
   const int nchunks = (K + KC - 1) / KC;
-  uint4 ring[P];
-#pragma unroll
-  for (int j = 0; j < P; j++) ring[j] = load_row(j);
-  build(0, 0);
   lds_barrier();
 
   for (int c = 0; c < nchunks; c++) {
-    if (c + 1 < nchunks) build(c + 1, (c + 1) % nbuf);
+    if (c + 1 < nchunks) {
+      uint32_t cn[NB];
+      load_coefs(c + 1, cn);
+      store_tables((c + 1) % nbuf, cn);
+    }
     const uint4* t01c = tab01 + (c % nbuf) * KC * MT;
     const uint32_t* t2c = tab2 + (c % nbuf) * KC * MT;
-    for (int jj = 0; jj < RC; jj += P) {
+    for (int jj = 0; jj < STEPS; jj += P) {
 #pragma unroll
       for (int j = 0; j < P; j += 2) {
-        // two rows per step so every v_bitop3 (XOR3) absorbs two products
-        const int q = c * RC + jj + j;
+        // two row-steps per iteration so every v_bitop3 (XOR3) absorbs two products
+        const int q = c * STEPS + jj + j;
         const uint4 xa = ring[j], xb = ring[j + 1];
-        ring[j] = load_row(q + P);
-        ring[j + 1] = load_row(q + 1 + P);
+        ring[j] = load_step(q + P);
+        ring[j + 1] = load_step(q + 1 + P);
+        if (MODE == 1) {  // tuning: no GF arithmetic
+          acc[0][0] ^= xa.x ^ xb.x;
+          acc[0][1] ^= xa.y ^ xb.y;
+          acc[0][2] ^= xa.z ^ xb.z;
+          acc[0][3] ^= xa.w ^ xb.w;
+          continue;
+        }
         const uint32_t x[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
         uint32_t s0[8], s1[8], s2[8];
 #pragma unroll
@@ -159,13 +200,14 @@ __global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
           s1[d] = (x[d] >> 3) & 0x07070707u;
           s2[d] = (x[d] >> 6) & 0x03030303u;
         }
-        const int kk = kw * RC + jj + j;
+        const int kka = w * RC + (jj + j) * S + g;
+        const int kkb = kka + S;
 #pragma unroll
         for (int m = 0; m < MT; m++) {
-          const uint4 ta = t01c[kk * MT + m];
-          const uint32_t ta2 = t2c[kk * MT + m];
-          const uint4 tb = t01c[(kk + 1) * MT + m];
-          const uint32_t tb2 = t2c[(kk + 1) * MT + m];
+          const uint4 ta = t01c[kka * MT + m];
+          const uint32_t ta2 = t2c[kka * MT + m];
+          const uint4 tb = t01c[kkb * MT + m];
+          const uint32_t tb2 = t2c[kkb * MT + m];
 #pragma unroll
           for (int d = 0; d < 4; d++) {
             const uint32_t a0 = __builtin_amdgcn_perm(ta.y, ta.x, s0[d]);
@@ -181,7 +223,23 @@ __global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
         }
       }
     }
-    lds_barrier();
+    lds_barrier();  // (a conditional barrier here makes hipcc spill heavily)
+  }
+
+  // reduce across the S lane groups (each holds other rows of the same columns)
+  if (S > 1) {
+#pragma unroll
+    for (int m = 0; m < MT; m++)
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        uint32_t v = acc[m][d];
+        if (S >= 4) {
+          const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // lane ^ 16
+          v = r[0] ^ r[1];
+        }
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);    // lane ^ 32
+        acc[m][d] = r[0] ^ r[1];
+      }
   }
 
   auto store16 = [&](int row, int cc, uint4 v) {
@@ -196,70 +254,111 @@ __global__ __launch_bounds__(64 * KW * CW) void gf_gemm_kernel(
   };
 
   if (KW == 1) {
+    if (g == 0) {
 #pragma unroll
-    for (int m = 0; m < MT; m++)
-      store16(m0 + m, col, make_uint4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]));
+      for (int m = 0; m < MT; m++)
+        store16(m0 + m, col, make_uint4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]));
+    }
     return;
   }
 
-  // XOR-reduce the KW partial sums of each (m, lane) in LDS.
+  // XOR-reduce the KW per-wave partial sums of each (m, column) in LDS
+  if (g == 0) {
 #pragma unroll
-  for (int m = 0; m < MT; m++)
+    for (int m = 0; m < MT; m++)
 #pragma unroll
-    for (int d = 0; d < 4; d++) atomicXor(&red[(m * 4 + d) * 64 + lane], acc[m][d]);
+      for (int d = 0; d < 4; d++) atomicXor(&red[(m * 4 + d) * GL + li], acc[m][d]);
+  }
   lds_barrier();
-  for (int i = tid; i < MT * 64; i += NT) {
-    const int m = i >> 6, l = i & 63;
-    const uint4 v = make_uint4(red[(m * 4 + 0) * 64 + l], red[(m * 4 + 1) * 64 + l],
-                               red[(m * 4 + 2) * 64 + l], red[(m * 4 + 3) * 64 + l]);
-    store16(m0 + m, tx * kChunkBytes + l * kLaneBytes, v);
+  for (int i = tid; i < MT * GL; i += NT) {
+    const int m = i / GL, l = i % GL;
+    const uint4 v = make_uint4(red[(m * 4 + 0) * GL + l], red[(m * 4 + 1) * GL + l],
+                               red[(m * 4 + 2) * GL + l], red[(m * 4 + 3) * GL + l]);
+    store16(m0 + m, tx * CB + l * kLaneBytes, v);
   }
 }
 
-template <int MT, int KW, int CW, int RC, int P>
+template <int MT, int KW, int S, int RC, int P, int MODE = 0>
 hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, size_t ldx,
                   uint8_t* Y, size_t ldy, int ncols, hipStream_t stream) {
   constexpr int KC = KW * RC;
-  const int nchunk = (ncols + kChunkBytes - 1) / kChunkBytes;
-  const int nx = (nchunk + CW - 1) / CW;
+  constexpr int CB = 1024 / S;
+  const int nx = (ncols + CB - 1) / CB;
   const int ny = (M + MT - 1) / MT;
   const int nbuf = K > KC ? 2 : 1;
   const int nx8 = (nx + 7) / 8 * 8;
-  const size_t lds = (size_t)nbuf * KC * MT * (16 + 4) + (KW > 1 ? (size_t)MT * 4 * 64 * 4 : 0);
-  hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, CW, RC, P>), dim3(nx8 * ny), dim3(64 * KW * CW), lds,
-                     stream, A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf);
+  const size_t lds = (size_t)nbuf * KC * MT * (16 + 4) + (KW > 1 ? (size_t)MT * 4 * (64 / S) * 4 : 0);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, S, RC, P, MODE>), dim3(nx8 * ny), dim3(64 * KW), lds, stream,
+                     A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf);
   return hipGetLastError();
 }
 
 }  // namespace
 
+// Tiles measured on MI355X at K = 256, ncols = 128 KiB (tools/tune_gemm.py).
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   (void)K;
   (void)ncols;
-  if (M <= 1) return {1, 16, 1};
-  if (M <= 2) return {2, 16, 1};
-  if (M <= 4) return {4, 16, 1};
-  if (M <= 8) return {4, 16, 1};
-  if (M <= 16) return {8, 16, 1};
-  return {16, 1, 4};
+  if (M <= 1) return {1, 16, 2};
+  if (M <= 2) return {2, 16, 2};
+  if (M <= 4) return {4, 8, 2};
+  if (M <= 8) return {8, 8, 2};
+  if (M <= 16) return {16, 8, 2};
+  return {8, 4, 1};
+}
+
+// KODR_GEMM_CFG="mt,kw,s" forces a tile (tuning runs only; see tools/tune_gemm.py)
+static bool env_config(GemmConfig* g) {
+  const char* s = getenv("KODR_GEMM_CFG");
+  if (!s || !*s) return false;
+  return sscanf(s, "%d,%d,%d", &g->mt, &g->kw, &g->s) == 3;
 }
 
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
                    const GemmConfig* force) {
   if (M == 0 || ncols == 0) return hipSuccess;
-  const GemmConfig g = force ? *force : choose_gemm_config(M, K, ncols);
+  GemmConfig g = force ? *force : choose_gemm_config(M, K, ncols);
+  GemmConfig ge;
+  if (!force && env_config(&ge)) g = ge;
   const int iM = (int)M, iK = (int)K, ild = (int)lda, inc = (int)ncols;
-#define KODR_TRY(MT_, KW_, CW_, RC_, P_)                                              \
-  if (g.mt == MT_ && g.kw == KW_ && g.cw == CW_)                                      \
-    return launch<MT_, KW_, CW_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  int mode = 0;
+#ifdef KODR_TUNE_MODES
+  if (const char* e = getenv("KODR_GEMM_MODE")) mode = atoi(e);
+  if (mode == 1 && g.mt == 8 && g.kw == 16 && g.s == 2)
+    return launch<8, 16, 2, 16, 8, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 2 && g.mt == 8 && g.kw == 16 && g.s == 2)
+    return launch<8, 16, 2, 16, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 1 && g.mt == 4 && g.kw == 8 && g.s == 2)
+    return launch<4, 8, 2, 32, 8, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 2 && g.mt == 4 && g.kw == 8 && g.s == 2)
+    return launch<4, 8, 2, 32, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 2 && g.mt == 8 && g.kw == 4 && g.s == 1)
+    return launch<8, 4, 1, 64, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+#endif
+  (void)mode;
+#define KODR_TRY(MT_, KW_, S_, RC_, P_)                                               \
+  if (g.mt == MT_ && g.kw == KW_ && g.s == S_)                                        \
+    return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  KODR_TRY(1, 16, 4, 16, 4)
+  KODR_TRY(1, 16, 2, 16, 8)
   KODR_TRY(1, 16, 1, 16, 8)
-  KODR_TRY(2, 16, 1, 16, 8)
+  KODR_TRY(2, 16, 4, 16, 4)
+  KODR_TRY(2, 16, 2, 16, 8)
+  KODR_TRY(4, 16, 4, 16, 4)
+  KODR_TRY(4, 16, 2, 16, 8)
   KODR_TRY(4, 16, 1, 16, 8)
-  KODR_TRY(8, 16, 1, 16, 8)
-  KODR_TRY(4, 4, 1, 16, 8)
-  KODR_TRY(8, 1, 4, 32, 4)
-  KODR_TRY(16, 1, 4, 32, 4)
+  KODR_TRY(8, 16, 4, 16, 4)
+  KODR_TRY(8, 16, 2, 16, 8)
+  KODR_TRY(8, 8, 2, 32, 8)
+  KODR_TRY(4, 8, 2, 32, 8)
+  KODR_TRY(8, 8, 4, 32, 8)
+  KODR_TRY(16, 8, 2, 32, 4)
+  KODR_TRY(8, 4, 1, 64, 8)
+  KODR_TRY(16, 4, 1, 64, 4)
+  KODR_TRY(8, 4, 2, 64, 8)
+  KODR_TRY(16, 4, 2, 64, 4)
 #undef KODR_TRY
   return hipErrorInvalidValue;
 }

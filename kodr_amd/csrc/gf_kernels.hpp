@@ -7,9 +7,9 @@
 namespace kodr_amd {
 
 // Instantiated tiles of gf_gemm_kernel: mt output rows per workgroup, kw waves
-// splitting K over one column chunk, cw waves on adjacent column chunks.
+// splitting K over one column chunk, s lane groups per wave (chunk = 1024/s B).
 struct GemmConfig {
-  int mt, kw, cw;
+  int mt, kw, s;
 };
 
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols);

@@ -1,0 +1,259 @@
+"""GPU parity: the HIP engine (through the C ABI) vs the golden fixtures and
+the CPU oracle, bit-exact.  Sizes the oracle finishes in seconds are compared
+byte for byte; the BASELINE.json shapes (32 MiB/256, 16 MiB/128) are compared
+in full for a batch of coded pieces and through round trips."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from kodr_amd import _lib, errors
+from kodr_amd._codec import FULL, SYSTEMATIC
+
+pytestmark = pytest.mark.gpu
+ERR = {None: 0, **{name: cls.code for name, cls in errors.BY_NAME.items()}}
+U8P = _lib._u8p
+
+
+def h(s):
+    return np.frombuffer(bytes.fromhex(s), dtype=np.uint8)
+
+
+def ptr(a):
+    return a.ctypes.data_as(U8P)
+
+
+class Enc:
+    def __init__(self, ctx, pieces, kind=FULL):
+        P = np.ascontiguousarray(pieces, np.uint8)
+        self.k, self.L = P.shape
+        self.h = ctypes.c_void_p()
+        errors.check(_lib.lib().rlnc_encoder_create(ctx.handle, kind, ptr(P), self.k, self.L,
+                                                    ctypes.byref(self.h)))
+
+    def code(self, V):
+        V = np.array(V, np.uint8).reshape(-1, self.k)
+        out = np.empty((V.shape[0], self.k + self.L), np.uint8)
+        errors.check(_lib.lib().rlnc_encoder_coded_pieces(self.h, ptr(V), V.shape[0], ptr(out)))
+        return V, out
+
+    def __del__(self):
+        _lib.lib().rlnc_encoder_destroy(self.h)
+
+
+class Dec:
+    def __init__(self, ctx, k):
+        self.h = ctypes.c_void_p()
+        errors.check(_lib.lib().rlnc_decoder_create(ctx.handle, k, ctypes.byref(self.h)))
+
+    def add(self, v, p):
+        v = np.ascontiguousarray(v, np.uint8)
+        p = np.ascontiguousarray(p, np.uint8)
+        return _lib.lib().rlnc_decoder_add_piece(self.h, ptr(v), v.size, ptr(p), p.size)
+
+    def state(self):
+        L = _lib.lib()
+        return (L.rlnc_decoder_useful(self.h), L.rlnc_decoder_received(self.h),
+                L.rlnc_decoder_required(self.h), bool(L.rlnc_decoder_is_decoded(self.h)))
+
+    def get(self, i):
+        L = _lib.lib().rlnc_decoder_piece_length(self.h)
+        out = np.empty(max(L, 1), np.uint8)
+        st = _lib.lib().rlnc_decoder_get_piece(self.h, i, ptr(out))
+        return st, out[:L]
+
+    def get_all(self):
+        n, L = _lib.lib().rlnc_decoder_useful(self.h), _lib.lib().rlnc_decoder_piece_length(self.h)
+        out = np.empty((n, L), np.uint8)
+        st = _lib.lib().rlnc_decoder_get_pieces(self.h, ptr(out))
+        return st, out
+
+    def __del__(self):
+        _lib.lib().rlnc_decoder_destroy(self.h)
+
+
+def test_encode_golden(gpu_ctx, golden):
+    for c in golden["vectors"]["encode"]:
+        e = Enc(gpu_ctx, np.stack([h(p) for p in c["pieces"]]))
+        V, out = e.code(np.stack([h(v) for v in c["vectors"]]))
+        for i, exp in enumerate(c["coded"]):
+            assert out[i, :c["k"]].tobytes() == V[i].tobytes()
+            assert out[i, c["k"]:].tobytes().hex() == exp, (c["k"], c["L"], i)
+
+
+def test_recode_golden(gpu_ctx, golden):
+    for c in golden["vectors"]["recode"]:
+        flat = h(c["flat"])
+        rh = ctypes.c_void_p()
+        errors.check(_lib.lib().rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, c["n"], c["k"],
+                                                    ctypes.byref(rh)))
+        R = np.stack([h(r) for r in c["r"]])
+        out = np.empty((R.shape[0], c["k"] + c["L"]), np.uint8)
+        errors.check(_lib.lib().rlnc_recoder_coded_pieces(rh, ptr(R), R.shape[0], ptr(out)))
+        _lib.lib().rlnc_recoder_destroy(rh)
+        assert [o.tobytes().hex() for o in out] == c["out"]
+
+
+def test_systematic_golden(gpu_ctx, golden):
+    for c in golden["vectors"]["systematic"]:
+        e = Enc(gpu_ctx, np.stack([h(p) for p in c["pieces"]]), SYSTEMATIC)
+        V = np.stack([h(v) for v in c["random_vectors"]])
+        # split into two calls to cross the systematic -> coded boundary mid-batch
+        _, o1 = e.code(V[:c["k"] - 1])
+        _, o2 = e.code(V[c["k"] - 1:])
+        got = [r.tobytes().hex() for r in np.concatenate([o1, o2])]
+        assert got == c["out"]
+
+
+def test_decode_golden_traces(gpu_ctx, golden):
+    for c in golden["vectors"]["decode"]:
+        d = Dec(gpu_ctx, c["k"])
+        for (vh, ph), step in zip(c["stream"], c["steps"]):
+            assert d.add(h(vh), h(ph)) == ERR[step["err"]], c["name"]
+            assert d.state() == (step["useful"], step["received"], step["required"], step["decoded"])
+            for idx, (e, p) in enumerate(step.get("get", [])):
+                st, got = d.get(idx)
+                assert st == ERR[e], (c["name"], idx)
+                if p is not None:
+                    assert got.tobytes().hex() == p
+        if c["decoded"] is not None:
+            st, allp = d.get_all()
+            assert st == 0
+            assert [r.tobytes().hex() for r in allp] == c["decoded"], c["name"]
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8, 9, 16, 17, 40, 256])
+@pytest.mark.parametrize("K", [1, 2, 15, 256, 257, 300])
+def test_gf_matmul_vs_oracle(gpu_ctx, M, K):
+    rng = np.random.default_rng(M * 1000 + K)
+    for ncols in (16, 1000, 1024 * 3 + 48, 4096 + 7):
+        ld = (ncols + 255) // 256 * 256
+        A = rng.integers(0, 256, (M, K), dtype=np.uint8)
+        X = np.zeros((K, ld), np.uint8)
+        X[:, :ncols] = rng.integers(0, 256, (K, ncols), dtype=np.uint8)
+        dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(X.nbytes), gpu_ctx.alloc(M * ld)
+        try:
+            gpu_ctx.h2d(dA, A)
+            gpu_ctx.h2d(dX, X)
+            gpu_ctx.h2d(dY, np.full(M * ld, 0xA5, np.uint8))  # canary beyond ncols
+            errors.check(_lib.lib().rlnc_gf_matmul_device(gpu_ctx.handle, dA, K, M, K, dX, ld, dY, ld, ncols))
+            Y = gpu_ctx.d2h(dY, M * ld).reshape(M, ld)
+        finally:
+            for p in (dA, dX, dY):
+                gpu_ctx.free(p)
+        st, ref = oracle.matmul(A, X[:, :ncols])
+        assert np.array_equal(Y[:, :ncols], ref), (M, K, ncols)
+        assert (Y[:, ncols:] == 0xA5).all(), "wrote past ncols"
+
+
+def test_c2_encode_batch_full_compare(gpu_ctx):
+    # BASELINE config 2: 32 MiB / 256 pieces, 8 coded pieces compared in full
+    rng = np.random.default_rng(0x6B6F6472)
+    k, L = 256, 131072
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    V = rng.integers(0, 256, (8, k), dtype=np.uint8)
+    V[1] = 0
+    V[2] = 1
+    _, out = e.code(V)
+    ref = oracle.encode(P, V)
+    assert np.array_equal(out[:, k:], ref)
+    assert np.array_equal(out[:, :k], V)
+
+
+def test_c2_device_encode_decode_round_trip(gpu_ctx):
+    # BASELINE configs 2+3 device-resident: encode k+2 pieces on the device,
+    # feed them to the decoder from device memory, decode, compare originals
+    rng = np.random.default_rng(3)
+    k, L = 256, 131072
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    n = k + 2
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    dV, dOut = gpu_ctx.alloc(V.nbytes), gpu_ctx.alloc(n * L)
+    try:
+        gpu_ctx.h2d(dV, V)
+        errors.check(_lib.lib().rlnc_encoder_coded_pieces_device(e.h, dV, n, dOut, L))
+        gpu_ctx.synchronize()
+        # spot-check two coded pieces against the oracle
+        got = gpu_ctx.d2h(dOut, 2 * L).reshape(2, L)
+        assert np.array_equal(got, oracle.encode(P, V[:2]))
+        d = Dec(gpu_ctx, k)
+        for i in range(n):
+            v = np.ascontiguousarray(V[i])
+            st = _lib.lib().rlnc_decoder_add_piece_device(d.h, ptr(v), k, dOut + i * L, L)
+            if st == ERR["ErrAllUsefulPiecesReceived"]:
+                break
+            assert st == 0
+        assert d.state()[3]
+        st, dec = d.get_all()
+        assert st == 0 and np.array_equal(dec, P)
+    finally:
+        gpu_ctx.free(dV)
+        gpu_ctx.free(dOut)
+
+
+def test_c4_systematic_round_trip_with_drops(gpu_ctx):
+    # BASELINE config 4: systematic 16 MiB / 128, random 50% piece loss
+    rng = np.random.default_rng(4)
+    k, L = 128, 131072
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P, SYSTEMATIC)
+    d = Dec(gpu_ctx, k)
+    sent = 0
+    while not d.state()[3]:
+        V, out = e.code(rng.integers(0, 256, (16, k), dtype=np.uint8))
+        for i in range(16):
+            sent += 1
+            if rng.random() < 0.5:
+                continue
+            assert bool(_lib.lib().rlnc_is_systematic(ptr(V[i]), k)) == (sent <= k)
+            st = d.add(out[i, :k], out[i, k:])
+            if st == ERR["ErrAllUsefulPiecesReceived"]:
+                break
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+
+
+def test_c2_recode_matches_oracle_and_decodes(gpu_ctx):
+    # config 5's per-GPU step: recode n = k held pieces of a 32 MiB/256 generation
+    rng = np.random.default_rng(5)
+    k, L = 256, 131072
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V = rng.integers(0, 256, (k, k), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    _, flat = e.code(V)                    # k wire rows
+    rh = ctypes.c_void_p()
+    errors.check(_lib.lib().rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, k, k, ctypes.byref(rh)))
+    R = rng.integers(0, 256, (k + 2, k), dtype=np.uint8)
+    out = np.empty((k + 2, k + L), np.uint8)
+    errors.check(_lib.lib().rlnc_recoder_coded_pieces(rh, ptr(R), k + 2, ptr(out)))
+    _lib.lib().rlnc_recoder_destroy(rh)
+    assert np.array_equal(out[:2], oracle.recode(flat, k, R[:2]))
+    d = Dec(gpu_ctx, k)
+    for row in out:
+        if d.add(row[:k], row[k:]) == ERR["ErrAllUsefulPiecesReceived"]:
+            break
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+
+
+def test_decode_matches_oracle_with_dependent_and_quirky_pieces(gpu_ctx):
+    rng = np.random.default_rng(6)
+    for k, L in [(5, 33), (16, 1000), (40, 4096)]:
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        d, ref = Dec(gpu_ctx, k), oracle.Decoder(k)
+        n = 0
+        while not ref.is_decoded() and n < 10 * k:
+            n += 1
+            v = rng.integers(0, 3, k, dtype=np.uint8)   # many zero / dependent rows
+            p = oracle.encode(P, v[None, :])[0] if rng.random() < 0.8 else rng.integers(0, 256, L, dtype=np.uint8)
+            assert d.add(v, p) == ref.add(v, p)
+            assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+            for idx in range(k):
+                st_r, got_r = ref.get_piece(idx)
+                st, got = d.get(idx)
+                assert st == st_r
+                if st == 0:
+                    assert np.array_equal(got, got_r)
