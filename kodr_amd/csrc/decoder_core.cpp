@@ -34,12 +34,14 @@ void DecoderCore::ensure_tcap(size_t need) {
   tcap_ = ncap;
   clean_.resize(slots + 1, 0);
   dirty_.resize(slots + 1, 0);
+  touched_.resize(slots + 1, 0);
 }
 
 // rows_[dst] ^= q * rows_[src] over coefficient columns [from, k) and all T
 // columns (the coded half in kodr is updated over its whole width, :66-73).
 void DecoderCore::axpy_row(size_t dst, size_t src, uint8_t q, size_t from) {
   hostgf::axpy(rows_[dst] + from, rows_[src] + from, k_ - from + received_, q);
+  touched_[dst] = 1;
 }
 
 int DecoderCore::add(const uint8_t* vec) {
@@ -55,6 +57,7 @@ int DecoderCore::add(const uint8_t* vec) {
   if (!(received_ > 1)) {                           // full/decoder.go:58-61
     useful_++;
     clean_[0] = 0;
+    touched_[0] = 1;  // never reduced: may be all-zero, test it in the next pass
     return 0;
   }
   rref();                                           // full/decoder.go:63
@@ -85,10 +88,12 @@ void DecoderCore::rref() {
   // pivot search (:23-35) and elimination (:51-74) the only row below i that
   // can be non-zero in column i is the last one.
   mark(last);
+  touched_[last] = 1;  // the new row
   for (size_t i = 0; i < boundary; i++) {
     if (rows_[i][i] == 0) {
       if (i < last && rows_[last][i] != 0) {
         std::swap(rows_[i], rows_[last]);           // :37-48
+        std::swap(touched_[i], touched_[last]);
         mark(i);
       } else {
         continue;                                   // :33-35
@@ -137,10 +142,15 @@ void DecoderCore::rref() {
   for (size_t n = 0; n < ndirty; n++) dirty_[dirty_list[n]] = 0;
   for (size_t j : dirty_big) dirty_[j] = 0;
 
-  // ---- remove_zero_rows (:136-165): stable removal of all-zero coefficient rows
+  // ---- remove_zero_rows (:136-165): stable removal of all-zero coefficient
+  // rows.  Rows no operation touched in this pass were non-zero before it
+  // (the previous pass removed every zero row), so only touched rows and the
+  // new row need the test; the others keep their order.
   size_t out = 0;
   for (size_t i = 0; i < rows_.size(); i++) {
-    if (hostgf::all_zero(rows_[i], k_)) {
+    const bool t = touched_[i];
+    touched_[i] = 0;
+    if (t && hostgf::all_zero(rows_[i], k_)) {
       free_.push_back(rows_[i]);
     } else {
       rows_[out++] = rows_[i];

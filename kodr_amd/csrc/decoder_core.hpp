@@ -59,6 +59,7 @@ class DecoderCore {
   std::vector<uint8_t*> free_;         // unused slots
   std::vector<uint8_t> clean_;         // per row index: diagonal pivot with a clean column above
   std::vector<uint8_t> dirty_;         // per row index: row moved/changed in this forward pass
+  std::vector<uint8_t> touched_;       // per row index: target of a row operation in this pass
 };
 
 }  // namespace kodr_amd

@@ -300,19 +300,20 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   (void)K;
   (void)ncols;
-  if (M <= 1) return {1, 16, 2};
-  if (M <= 2) return {2, 16, 2};
-  if (M <= 4) return {4, 8, 2};
-  if (M <= 8) return {8, 8, 2};
-  if (M <= 16) return {16, 8, 2};
-  return {8, 4, 1};
+  if (M <= 1) return {1, 16, 2, 0};
+  if (M <= 2) return {2, 16, 2, 0};
+  if (M <= 4) return {4, 8, 2, 4};
+  if (M <= 8) return {8, 16, 2, 2};
+  if (M <= 16) return {16, 8, 2, 2};
+  return {8, 4, 1, 4};
 }
 
 // KODR_GEMM_CFG="mt,kw,s" forces a tile (tuning runs only; see tools/tune_gemm.py)
 static bool env_config(GemmConfig* g) {
   const char* s = getenv("KODR_GEMM_CFG");
   if (!s || !*s) return false;
-  return sscanf(s, "%d,%d,%d", &g->mt, &g->kw, &g->s) == 3;
+  g->p = 0;
+  return sscanf(s, "%d,%d,%d,%d", &g->mt, &g->kw, &g->s, &g->p) >= 3;
 }
 
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
@@ -339,7 +340,7 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
 #endif
   (void)mode;
 #define KODR_TRY(MT_, KW_, S_, RC_, P_)                                               \
-  if (g.mt == MT_ && g.kw == KW_ && g.s == S_)                                        \
+  if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))             \
     return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   KODR_TRY(1, 16, 4, 16, 4)
   KODR_TRY(1, 16, 2, 16, 8)
@@ -352,6 +353,15 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   KODR_TRY(8, 16, 4, 16, 4)
   KODR_TRY(8, 16, 2, 16, 8)
   KODR_TRY(8, 8, 2, 32, 8)
+  KODR_TRY(8, 8, 2, 32, 4)
+  KODR_TRY(8, 8, 2, 32, 2)
+  KODR_TRY(8, 16, 2, 16, 4)
+  KODR_TRY(8, 16, 2, 16, 2)
+  KODR_TRY(8, 16, 4, 16, 2)
+  KODR_TRY(8, 8, 4, 32, 4)
+  KODR_TRY(4, 8, 2, 32, 4)
+  KODR_TRY(16, 8, 2, 32, 2)
+  KODR_TRY(8, 4, 1, 64, 4)
   KODR_TRY(4, 8, 2, 32, 8)
   KODR_TRY(8, 8, 4, 32, 8)
   KODR_TRY(16, 8, 2, 32, 4)

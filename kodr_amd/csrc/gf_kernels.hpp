@@ -7,9 +7,10 @@
 namespace kodr_amd {
 
 // Instantiated tiles of gf_gemm_kernel: mt output rows per workgroup, kw waves
-// splitting K over one column chunk, s lane groups per wave (chunk = 1024/s B).
+// splitting K over one column chunk, s lane groups per wave (chunk = 1024/s B),
+// p row-steps in flight per wave (0 = the tile's default).
 struct GemmConfig {
-  int mt, kw, s;
+  int mt, kw, s, p;
 };
 
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols);

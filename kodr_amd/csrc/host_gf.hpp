@@ -19,6 +19,7 @@ struct Tables {
   uint8_t exp[512];
   uint8_t mul_lo[256][16];  // c * n       for nibble n (pshufb table)
   uint8_t mul_hi[256][16];  // c * (n<<4)
+  uint64_t affine[256];     // GF2P8AFFINEQB bit-matrix of x -> c * x (poly 0x11D)
   Tables() {
     unsigned x = 1;
     for (int i = 0; i < 255; i++) {
@@ -34,6 +35,18 @@ struct Tables {
         mul_lo[c][n] = mul(c, n);
         mul_hi[c][n] = mul(c, n << 4);
       }
+    // affine: result bit i = parity(matrix.byte[7 - i] & x); multiply-by-c is
+    // GF(2)-linear, column j of its matrix is c * 2^j
+    for (int c = 0; c < 256; c++) {
+      uint64_t m = 0;
+      for (int i = 0; i < 8; i++) {
+        unsigned row = 0;
+        for (int j = 0; j < 8; j++)
+          if (mul(c, 1u << j) & (1u << i)) row |= 1u << j;
+        m |= (uint64_t)row << (8 * (7 - i));
+      }
+      affine[c] = m;
+    }
   }
   uint8_t mul(unsigned a, unsigned b) const {  // gf256.go:109-118
     if (a == 0 || b == 0) return 0;
@@ -83,12 +96,53 @@ inline bool have_avx2() {
   static const bool h = __builtin_cpu_supports("avx2");
   return h;
 }
+// GFNI + AVX-512: one vgf2p8affineqb multiplies 64 bytes by a constant
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void axpy_gfni512(uint8_t* dst, const uint8_t* src,
+                                                                         size_t n, uint8_t q) {
+  const __m512i A = _mm512_set1_epi64((long long)T().affine[q]);
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) {
+    const __m512i x = _mm512_loadu_si512((const void*)(src + i));
+    const __m512i p = _mm512_gf2p8affine_epi64_epi8(x, A, 0);
+    _mm512_storeu_si512((void*)(dst + i), _mm512_xor_si512(_mm512_loadu_si512((const void*)(dst + i)), p));
+  }
+  if (i < n) {
+    const __mmask64 k = (__mmask64)(~0ULL >> (64 - (n - i)));
+    const __m512i x = _mm512_maskz_loadu_epi8(k, src + i);
+    const __m512i d = _mm512_maskz_loadu_epi8(k, dst + i);
+    _mm512_mask_storeu_epi8(dst + i, k, _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(x, A, 0)));
+  }
+}
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void scale_gfni512(uint8_t* row, size_t n, uint8_t q) {
+  const __m512i A = _mm512_set1_epi64((long long)T().affine[q]);
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64)
+    _mm512_storeu_si512((void*)(row + i),
+                        _mm512_gf2p8affine_epi64_epi8(_mm512_loadu_si512((const void*)(row + i)), A, 0));
+  if (i < n) {
+    const __mmask64 k = (__mmask64)(~0ULL >> (64 - (n - i)));
+    _mm512_mask_storeu_epi8(row + i, k, _mm512_gf2p8affine_epi64_epi8(_mm512_maskz_loadu_epi8(k, row + i), A, 0));
+  }
+}
+__attribute__((target("avx512f,avx512bw"))) inline bool all_zero512(const uint8_t* p, size_t n) {
+  __m512i acc = _mm512_setzero_si512();
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64) acc = _mm512_or_si512(acc, _mm512_loadu_si512((const void*)(p + i)));
+  if (i < n) acc = _mm512_or_si512(acc, _mm512_maskz_loadu_epi8((__mmask64)(~0ULL >> (64 - (n - i))), p + i));
+  return _mm512_test_epi64_mask(acc, acc) == 0;
+}
+inline bool have_gfni512() {
+  static const bool h = __builtin_cpu_supports("gfni") && __builtin_cpu_supports("avx512bw") &&
+                        __builtin_cpu_supports("avx512f");
+  return h;
+}
 #endif
 
 // dst[0..n) ^= q * src[0..n)
 inline void axpy(uint8_t* dst, const uint8_t* src, size_t n, uint8_t q) {
   if (q == 0 || n == 0) return;
 #if defined(__x86_64__)
+  if (have_gfni512()) return axpy_gfni512(dst, src, n, q);
   if (have_avx2()) return axpy_avx2(dst, src, n, q);
 #endif
   const Tables& t = T();
@@ -98,6 +152,7 @@ inline void axpy(uint8_t* dst, const uint8_t* src, size_t n, uint8_t q) {
 // row[0..n) *= q
 inline void scale(uint8_t* row, size_t n, uint8_t q) {
 #if defined(__x86_64__)
+  if (have_gfni512()) return scale_gfni512(row, n, q);
   if (have_avx2()) return scale_avx2(row, n, q);
 #endif
   const Tables& t = T();
@@ -105,6 +160,9 @@ inline void scale(uint8_t* row, size_t n, uint8_t q) {
 }
 
 inline bool all_zero(const uint8_t* p, size_t n) {
+#if defined(__x86_64__)
+  if (have_gfni512()) return all_zero512(p, n);
+#endif
   size_t i = 0;
   uint64_t acc = 0;
   for (; i + 8 <= n; i += 8) {

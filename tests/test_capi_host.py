@@ -236,3 +236,32 @@ def test_get_piece_without_device_reports_no_device():
     out = np.empty(4, np.uint8)
     assert _lib.lib().rlnc_decoder_get_piece(core.h, 0, out.ctypes.data_as(_lib._u8p)) == -4
     assert _lib.lib().rlnc_decoder_get_piece(core.h, 5, out.ctypes.data_as(_lib._u8p)) == 12
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_core_fuzz_mixed_streams(seed):
+    # every step draws from a different generator: zero rows, unit vectors,
+    # duplicates of earlier rows, tiny-field noise and dense rows, so the
+    # fast-path invariants (dirty rows, clean columns, touched rows) are hit
+    # in all orders
+    rng = np.random.default_rng(7000 + seed)
+    k = int(rng.integers(2, 40))
+    L = 4
+    seen = []
+    stream = []
+    for _ in range(4 * k + 8):
+        kind = rng.integers(0, 6)
+        if kind == 0:
+            v = np.zeros(k, np.uint8)
+        elif kind == 1:
+            v = np.zeros(k, np.uint8)
+            v[rng.integers(0, k)] = rng.integers(1, 256)
+        elif kind == 2 and seen:
+            v = seen[rng.integers(0, len(seen))].copy()
+        elif kind == 3:
+            v = rng.integers(0, 2, k, dtype=np.uint8)
+        else:
+            v = rng.integers(0, 256, k, dtype=np.uint8)
+        seen.append(v)
+        stream.append((v, rng.integers(0, 256, L, dtype=np.uint8)))
+    check_stream(k, stream)
