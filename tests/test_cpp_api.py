@@ -1,0 +1,31 @@
+"""The C++ mirror of kodr's API (include/kodr/kodr.hpp) builds against the
+C ABI on CPU; its kodr-style test program runs on the GPU."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "api_test.cpp")
+BIN = os.path.join(ROOT, "tests", "cpp", "api_test")
+
+
+def build():
+    libdir = os.path.join(ROOT, "kodr_amd")
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-I", os.path.join(ROOT, "include"), SRC, "-o", BIN,
+           "-L", libdir, "-lkodr_rlnc", f"-Wl,-rpath,{libdir}", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_cpp_api_builds_and_links():
+    build()
+    assert os.path.exists(BIN)
+
+
+@pytest.mark.gpu
+def test_cpp_api_runs_kodr_flows():
+    build()
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok (0 failures)" in r.stdout
