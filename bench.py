@@ -86,7 +86,7 @@ def main():
 
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
 
     from kodr_amd import device as kdev
     from kodr_amd import errors
@@ -146,8 +146,11 @@ def main():
     extras = {}
     if not args.no_extras and rank == 0:
         extras = run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng)
-    if world > 1:
-        c5 = run_relay(ctx, L_, errors, encs[0], k, L, rng, torch, dist, kdist)
+    if world > 1 and not args.no_extras:
+        try:
+            c5 = run_relay(ctx, L_, errors, encs[0], k, L, rng, torch, dist, kdist)
+        except Exception as e:  # secondary measurement: never lose the headline line
+            c5 = {"error": repr(e)[:300]}
         if rank == 0:
             extras["c5_encode_relay_recode"] = c5
 

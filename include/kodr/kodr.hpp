@@ -242,8 +242,9 @@ class DecoderBase {  // full/decoder.go == systematic/decoder.go
     return check(rlnc_decoder_add_piece(h_, p.Vector.data(), p.Vector.size(), p.Piece.data(), p.Piece.size()));
   }
   std::pair<kodr_internals::Piece, Err> GetPiece(size_t i) {            // :77-79
-    kodr_internals::Piece out(PieceLength());
+    kodr_internals::Piece out(PieceLength() ? PieceLength() : 1);
     Err e = check(rlnc_decoder_get_piece(h_, i, out.data()));
+    out.resize(PieceLength());
     if (e != Err::None) return {{}, e};
     return {out, Err::None};
   }

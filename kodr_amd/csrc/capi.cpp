@@ -735,8 +735,9 @@ size_t rlnc_decoder_piece_length(const rlnc_decoder* d) {
 size_t rlnc_decoder_piece_count(const rlnc_decoder* d) { return d ? d->core.piece_count() : 0; }
 
 int rlnc_decoder_get_piece(rlnc_decoder* d, size_t idx, uint8_t* out) {
-  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(d->core.piece_available(idx));  // decoder_state.go:222-256
+  if (!out) return RLNC_ERR_INVALID_ARGUMENT;
   if (!d->ctx) return RLNC_ERR_NO_DEVICE;
   TRY(set_dev(d->ctx));
   if (d->core.rank() >= d->core.piece_count()) {

@@ -297,9 +297,11 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
 }  // namespace
 
 // Tiles measured on MI355X at K = 256, ncols = 128 KiB (tools/tune_gemm.py).
+// Every tile stages K-chunks of 256 rows; for K > 256 the tables are
+// double-buffered (2 x 256 x MT x 20 B of LDS), which rules out MT = 16.
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
-  (void)K;
   (void)ncols;
+  if (K > 256 && M > 8 && M <= 16) return {8, 16, 2, 2};
   if (M <= 1) return {1, 16, 2, 0};
   if (M <= 2) return {2, 16, 2, 0};
   if (M <= 4) return {4, 8, 2, 4};
