@@ -57,6 +57,7 @@ int DecoderCore::add(const uint8_t* vec) {
   if (!(received_ > 1)) {                           // full/decoder.go:58-61
     useful_++;
     clean_[0] = 0;
+    all_clean_ = false;
     touched_[0] = 1;  // never reduced: may be all-zero, test it in the next pass
     return 0;
   }
@@ -68,8 +69,10 @@ int DecoderCore::add(const uint8_t* vec) {
 // Rref (:178-182) on a state whose rows 0..R-2 are the output of the previous
 // Rref and row R-1 is the new piece.
 void DecoderCore::rref() {
+  const size_t R = rows_.size();
+  if (all_clean_ && R - 1 < k_) return rref_clean();
   const hostgf::Tables& t = T();
-  const size_t R = rows_.size(), last = R - 1;
+  const size_t last = R - 1;
   const size_t boundary = std::min(R, k_);
   // indices whose row changed identity or content in this forward pass
   size_t dirty_list[4096];
@@ -158,7 +161,62 @@ void DecoderCore::rref() {
   }
   rows_.resize(out);
   // a row with a non-zero diagonal after this pass has a clean column above
-  for (size_t i = 0; i < rows_.size(); i++) clean_[i] = (i < k_ && rows_[i][i] != 0) ? 1 : 0;
+  update_clean();
+}
+
+void DecoderCore::update_clean() {
+  all_clean_ = true;
+  for (size_t i = 0; i < rows_.size(); i++) {
+    clean_[i] = (i < k_ && rows_[i][i] != 0) ? 1 : 0;
+    all_clean_ = all_clean_ && clean_[i];
+  }
+}
+
+// Rref when rows 0..r-1 are all diagonal pivots (= 1) with clean columns, i.e.
+// the coefficient half is [I_r | X], and row r is the new piece.  Then kodr's
+// literal passes reduce to, exactly:
+//  clean_forward  (:22-75): no swap; the quotient for pivot i is the new row's
+//                 own entry at column i (no other pivot row touches column i),
+//                 so the new row becomes  v ^ XOR_i v[i] * row_i  -- one
+//                 blocked accumulation;
+//  clean_backward (:85-133): column r is eliminated from every row above with
+//                 quotient c[j][r] / d (a rank-1 update), row r is scaled by
+//                 1/d; every other column is already clean;
+//  remove_zero_rows: only the new row can be zero.
+void DecoderCore::rref_clean() {
+  const hostgf::Tables& t = T();
+  const size_t r = rows_.size() - 1, width = k_ + received_;
+  uint8_t* v = rows_[r];
+  qbuf_.assign(v, v + r);
+  // columns < r of the result are exactly zero (pivot i cancels v[i], every
+  // other pivot row is 0 there); accumulate only columns [r, k + received)
+  ptrs_.resize(r);
+  for (size_t i = 0; i < r; i++) ptrs_[i] = rows_[i] + r;
+  hostgf::accumulate(v + r, ptrs_.data(), qbuf_.data(), r, width - r);
+  memset(v, 0, r);
+  const uint8_t d = v[r];
+  if (d != 0) {
+    // row_j[r..] ^= (c_j / d) * v[r..]  for every j < r, as one pass
+    const uint8_t dinv = t.inv(d);
+    ptrs_.resize(r);
+    for (size_t j = 0; j < r; j++) {
+      qbuf_[j] = t.mul(rows_[j][r], dinv);  // == Div(c_j, d) (gf256.go:121-127)
+      ptrs_[j] = rows_[j] + r;
+    }
+    hostgf::rank1(ptrs_.data(), qbuf_.data(), r, v + r, width - r);
+    if (d != 1) hostgf::scale(v + r, width - r, t.inv(d));
+    clean_[r] = 1;  // all_clean_ stays true
+    return;
+  }
+  // the new row has no pivot on the diagonal: it is either all-zero (dropped)
+  // or kept as an off-diagonal row (kodr's rank over-count quirk)
+  if (hostgf::all_zero(v, k_)) {
+    free_.push_back(v);
+    rows_.pop_back();
+    return;
+  }
+  clean_[r] = 0;
+  all_clean_ = false;
 }
 
 int DecoderCore::piece_available(size_t idx) const {

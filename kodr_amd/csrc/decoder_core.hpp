@@ -48,6 +48,8 @@ class DecoderCore {
 
  private:
   void rref();
+  void rref_clean();
+  void update_clean();
   void ensure_tcap(size_t need);
   void axpy_row(size_t dst, size_t src, uint8_t q, size_t from);
 
@@ -60,6 +62,9 @@ class DecoderCore {
   std::vector<uint8_t> clean_;         // per row index: diagonal pivot with a clean column above
   std::vector<uint8_t> dirty_;         // per row index: row moved/changed in this forward pass
   std::vector<uint8_t> touched_;       // per row index: target of a row operation in this pass
+  bool all_clean_ = false;             // every row is a diagonal pivot with a clean column
+  std::vector<uint8_t> qbuf_;          // quotients of the blocked passes
+  std::vector<uint8_t*> ptrs_;
 };
 
 }  // namespace kodr_amd

@@ -330,9 +330,9 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
 #ifdef KODR_TUNE_MODES
   if (const char* e = getenv("KODR_GEMM_MODE")) mode = atoi(e);
   if (mode == 1 && g.mt == 8 && g.kw == 16 && g.s == 2)
-    return launch<8, 16, 2, 16, 8, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+    return launch<8, 16, 2, 16, 2, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   if (mode == 2 && g.mt == 8 && g.kw == 16 && g.s == 2)
-    return launch<8, 16, 2, 16, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+    return launch<8, 16, 2, 16, 2, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   if (mode == 1 && g.mt == 4 && g.kw == 8 && g.s == 2)
     return launch<4, 8, 2, 32, 8, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   if (mode == 2 && g.mt == 4 && g.kw == 8 && g.s == 2)

@@ -138,6 +138,80 @@ inline bool have_gfni512() {
 }
 #endif
 
+#if defined(__x86_64__)
+// v[0..n) ^= XOR_i q[i] * rows[i][0..n): up to 8 x 64 B of v stay in
+// registers while every contributing row streams through once
+template <int NB>
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void accumulate_blk(
+    uint8_t* v, const uint8_t* const* rows, const uint8_t* q, size_t nrows, size_t off, size_t w) {
+  const Tables& t = T();
+  __m512i acc[NB];
+  __mmask64 km[NB];
+#pragma GCC unroll 8
+  for (int b = 0; b < NB; b++) {
+    const size_t o = (size_t)b * 64, ww = w - o < 64 ? w - o : 64;
+    km[b] = (__mmask64)(~0ULL >> (64 - ww));
+    acc[b] = _mm512_maskz_loadu_epi8(km[b], v + off + o);
+  }
+  for (size_t r = 0; r < nrows; r++) {
+    if (!q[r]) continue;
+    const __m512i A = _mm512_set1_epi64((long long)t.affine[q[r]]);
+    const uint8_t* src = rows[r] + off;
+#pragma GCC unroll 8
+    for (int b = 0; b < NB; b++)
+      acc[b] = _mm512_xor_si512(acc[b], _mm512_gf2p8affine_epi64_epi8(
+                                            _mm512_maskz_loadu_epi8(km[b], src + b * 64), A, 0));
+  }
+#pragma GCC unroll 8
+  for (int b = 0; b < NB; b++) _mm512_mask_storeu_epi8(v + off + b * 64, km[b], acc[b]);
+}
+inline void accumulate_gfni512(uint8_t* v, const uint8_t* const* rows, const uint8_t* q, size_t nrows,
+                               size_t n) {
+  for (size_t off = 0; off < n; off += 512) {
+    const size_t w = n - off < 512 ? n - off : 512;
+    switch ((w + 63) / 64) {
+      case 1: accumulate_blk<1>(v, rows, q, nrows, off, w); break;
+      case 2: accumulate_blk<2>(v, rows, q, nrows, off, w); break;
+      case 3: accumulate_blk<3>(v, rows, q, nrows, off, w); break;
+      case 4: accumulate_blk<4>(v, rows, q, nrows, off, w); break;
+      case 5: accumulate_blk<5>(v, rows, q, nrows, off, w); break;
+      case 6: accumulate_blk<6>(v, rows, q, nrows, off, w); break;
+      case 7: accumulate_blk<7>(v, rows, q, nrows, off, w); break;
+      default: accumulate_blk<8>(v, rows, q, nrows, off, w); break;
+    }
+  }
+}
+
+// rows[j][0..n) ^= q[j] * v[0..n) for every j (rank-1 update); v is held in
+// registers, one pass over each row
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void rank1_gfni512(
+    uint8_t* const* rows, const uint8_t* q, size_t nrows, const uint8_t* v, size_t n) {
+  const Tables& t = T();
+  for (size_t i0 = 0; i0 < n; i0 += 256) {  // 4 registers of v at a time
+    const size_t w = n - i0 < 256 ? n - i0 : 256;
+    __mmask64 km[4];
+    __m512i vb[4];
+    for (int b = 0; b < 4; b++) {
+      const size_t o = (size_t)b * 64;
+      const size_t ww = w > o ? (w - o < 64 ? w - o : 64) : 0;
+      km[b] = ww ? (__mmask64)(~0ULL >> (64 - ww)) : (__mmask64)0;
+      vb[b] = _mm512_maskz_loadu_epi8(km[b], v + i0 + o);
+    }
+    for (size_t r = 0; r < nrows; r++) {
+      if (!q[r]) continue;
+      const __m512i A = _mm512_set1_epi64((long long)t.affine[q[r]]);
+      uint8_t* dst = rows[r] + i0;
+      for (int b = 0; b < 4; b++) {
+        if (!km[b]) break;
+        const __m512i d = _mm512_maskz_loadu_epi8(km[b], dst + b * 64);
+        _mm512_mask_storeu_epi8(dst + b * 64, km[b],
+                                _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(vb[b], A, 0)));
+      }
+    }
+  }
+}
+#endif
+
 // dst[0..n) ^= q * src[0..n)
 inline void axpy(uint8_t* dst, const uint8_t* src, size_t n, uint8_t q) {
   if (q == 0 || n == 0) return;
@@ -157,6 +231,22 @@ inline void scale(uint8_t* row, size_t n, uint8_t q) {
 #endif
   const Tables& t = T();
   for (size_t i = 0; i < n; i++) row[i] = t.mul(row[i], q);
+}
+
+// v[0..n) ^= XOR_i q[i] * rows[i][0..n)
+inline void accumulate(uint8_t* v, const uint8_t* const* rows, const uint8_t* q, size_t nrows, size_t n) {
+#if defined(__x86_64__)
+  if (have_gfni512()) return accumulate_gfni512(v, rows, q, nrows, n);
+#endif
+  for (size_t r = 0; r < nrows; r++) axpy(v, rows[r], n, q[r]);
+}
+
+// rows[j][0..n) ^= q[j] * v[0..n)
+inline void rank1(uint8_t* const* rows, const uint8_t* q, size_t nrows, const uint8_t* v, size_t n) {
+#if defined(__x86_64__)
+  if (have_gfni512()) return rank1_gfni512(rows, q, nrows, v, n);
+#endif
+  for (size_t r = 0; r < nrows; r++) axpy(rows[r], v, n, q[r]);
 }
 
 inline bool all_zero(const uint8_t* p, size_t n) {
