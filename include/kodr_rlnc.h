@@ -169,9 +169,14 @@ int rlnc_decoder_add_piece(rlnc_decoder* dec, const uint8_t* vector, size_t vect
 /* same, with the piece bytes already on the device (copied D2D, async) */
 int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                                   const uint8_t* d_piece, size_t piece_len);
-/* batch of `count` wire rows (vector ++ piece) at row pitch `pitch`, host or
- * device (is_device).  Processes pieces in order, stops at the first error;
- * *consumed = pieces accepted (OK).  Returns the first non-OK status or OK. */
+/* batch AddPiece over `count` wire rows (vector ++ piece, as CodedPiece.Flatten,
+ * kodr_internals/coded.go) at row pitch `pitch`, on the host or the device
+ * (is_device).  The piece length is the decoder's L, or pitch - piece_count
+ * if no piece was added yet.  Same result as calling AddPiece row by row:
+ * stops at the first error (RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED once decoded)
+ * with *consumed = pieces accepted.  The accepted pieces are stored with ONE
+ * strided copy (host rows staged through pinned memory; device rows D2D,
+ * async, only the coding vectors are read back). */
 int rlnc_decoder_add_pieces(rlnc_decoder* dec, const uint8_t* rows, size_t count, size_t pitch,
                             int is_device, size_t* consumed);
 int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */

@@ -180,6 +180,27 @@ class _Decoder:
         pa, pp = u8(piece.Piece)
         errors.check(lib().rlnc_decoder_add_piece(self._h, vp, len(piece.Vector), pp, len(piece.Piece)))
 
+    def add_wire_rows(self, rows):
+        """AddPiece over each row of a (count, k + L) uint8 array of flattened
+        coded pieces (kodr_internals/coded.go Flatten), in one C-ABI call.
+        Returns the number of pieces accepted; stops quietly once decoded."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint8)
+        if rows.ndim != 2:
+            raise ValueError("rows must be a 2-D array of wire rows")
+        return self._add_rows(rows.ctypes.data, rows.shape[0], rows.shape[1], False)
+
+    def add_wire_rows_device(self, d_rows, count, pitch):
+        """Same, with the wire rows resident on the device (pointer, row pitch)."""
+        return self._add_rows(d_rows, count, pitch, True)
+
+    def _add_rows(self, ptr, count, pitch, dev):
+        consumed = ctypes.c_size_t()
+        st = lib().rlnc_decoder_add_pieces(self._h, ctypes.c_void_p(ptr), count, pitch, int(dev),
+                                           ctypes.byref(consumed))
+        if st != 3:
+            errors.check(st)
+        return consumed.value
+
     def GetPiece(self, i):  # :77-79
         L = self.PieceLength()
         out = np.empty(max(L, 1), dtype=np.uint8)

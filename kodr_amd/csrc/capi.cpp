@@ -18,6 +18,7 @@
 #include "../../include/kodr_rlnc.h"
 #include "decoder_core.hpp"
 #include "gf_kernels.hpp"
+#include "staging.hpp"
 
 using kodr_amd::DecoderCore;
 
@@ -82,6 +83,7 @@ struct rlnc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  kodr_amd::Staging stage;   // pinned chunks for host-pointer copies
 };
 
 struct rlnc_encoder {
@@ -112,6 +114,7 @@ struct rlnc_decoder {
   DevBuf rowbuf;             // one row for partial GetPiece
   bool decoded_ready = false;
   std::vector<uint8_t> hT;
+  std::vector<uint8_t> hvecs;  // coding vectors of a device batch
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -192,13 +195,10 @@ int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** ou
 // upload `len` bytes of data as k rows of L bytes (last row zero padded)
 int upload_generation(rlnc_encoder* e, const uint8_t* data, size_t len) {
   const size_t full_rows = len / e->L, tail = len - full_rows * e->L;
-  if (full_rows)
-    HIPC(hipMemcpy2DAsync(e->pieces.p, e->pitch, data, e->L, e->L, full_rows, hipMemcpyHostToDevice,
-                          e->ctx->stream));
+  HIPC(e->ctx->stage.h2d(e->pieces.p, e->pitch, data, e->L, e->L, full_rows, e->ctx->stream));
   if (tail)
-    HIPC(hipMemcpyAsync(e->pieces.p + full_rows * e->pitch, data + full_rows * e->L, tail,
-                        hipMemcpyHostToDevice, e->ctx->stream));
-  HIPC(hipStreamSynchronize(e->ctx->stream));
+    HIPC(e->ctx->stage.h2d(e->pieces.p + full_rows * e->pitch, e->pitch, data + full_rows * e->L, tail, tail, 1,
+                           e->ctx->stream));
   return RLNC_OK;
 }
 
@@ -262,10 +262,9 @@ int rlnc_ctx_create(int device, void* stream, rlnc_ctx** out) {
 int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   if (!ctx) return RLNC_OK;
   (void)hipSetDevice(ctx->device);
-  if (ctx->own_stream) {
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipStreamDestroy(ctx->stream);
-  }
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->stage.release();
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
 }
@@ -469,7 +468,7 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, u
     memset(vectors + i * k, 0, k);
     vectors[i * k + id] = 1;
     memcpy(out + i * clen, vectors + i * k, k);
-    HIPC(hipMemcpyAsync(out + i * clen + k, e->pieces.p + id * e->pitch, L, hipMemcpyDeviceToHost, st));
+    HIPC(e->ctx->stage.d2h(out + i * clen + k, clen, e->pieces.p + id * e->pitch, e->pitch, L, 1, st));
     i++;
   }
   // full/encoder.go:61-71 (and systematic/encoder.go:98-108) in batches
@@ -478,11 +477,10 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, u
     const size_t B = std::min(kBatch, count - i);
     TRY(e->vecs.reserve(B * k));
     TRY(e->out.reserve(B * e->pitch));
-    HIPC(hipMemcpyAsync(e->vecs.p, vectors + i * k, B * k, hipMemcpyHostToDevice, st));
+    HIPC(e->ctx->stage.h2d(e->vecs.p, k, vectors + i * k, k, k, B, st));
     TRY(gemm(e->ctx, e->vecs.p, k, B, k, e->pieces.p, e->pitch, e->out.p, e->pitch, L));
-    HIPC(hipMemcpy2DAsync(out + i * clen + k, clen, e->out.p, e->pitch, L, B, hipMemcpyDeviceToHost, st));
     for (size_t b = 0; b < B; b++) memcpy(out + (i + b) * clen, vectors + (i + b) * k, k);
-    HIPC(hipStreamSynchronize(st));
+    HIPC(e->ctx->stage.d2h(out + i * clen + k, clen, e->out.p, e->pitch, L, B, st));
     i += B;
   }
   HIPC(hipStreamSynchronize(st));
@@ -532,9 +530,7 @@ int rlnc_recoder_create(rlnc_ctx* ctx, const uint8_t* flat, size_t len, size_t n
   if (!flat) return RLNC_ERR_INVALID_ARGUMENT;
   rlnc_recoder* r = nullptr;
   TRY(recoder_alloc(ctx, n, clen, together, &r));
-  hipError_t he = hipMemcpy2DAsync(r->flat.p, r->pitch, flat, clen, clen, n, hipMemcpyHostToDevice,
-                                   ctx->stream);
-  if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+  hipError_t he = ctx->stage.h2d(r->flat.p, r->pitch, flat, clen, clen, n, ctx->stream);
   if (he != hipSuccess) {
     rlnc_recoder_destroy(r);
     return hip_fail(he, "hipMemcpy2DAsync");
@@ -583,12 +579,10 @@ int rlnc_recoder_coded_pieces(rlnc_recoder* r, const uint8_t* rv, size_t count, 
     const size_t B = std::min(kBatch, count - i);
     TRY(r->r.reserve(B * r->n));
     TRY(r->out.reserve(B * r->pitch));
-    HIPC(hipMemcpyAsync(r->r.p, rv + i * r->n, B * r->n, hipMemcpyHostToDevice, st));
+    HIPC(r->ctx->stage.h2d(r->r.p, r->n, rv + i * r->n, r->n, r->n, B, st));
     // wire rows in, wire rows out: [r x C | sum r_i P_i] (full/recoder.go:32-40)
     TRY(gemm(r->ctx, r->r.p, r->n, B, r->n, r->flat.p, r->pitch, r->out.p, r->pitch, r->clen));
-    HIPC(hipMemcpy2DAsync(out + i * r->clen, r->clen, r->out.p, r->pitch, r->clen, B,
-                          hipMemcpyDeviceToHost, st));
-    HIPC(hipStreamSynchronize(st));
+    HIPC(r->ctx->stage.d2h(out + i * r->clen, r->clen, r->out.p, r->pitch, r->clen, B, st));
     i += B;
   }
   return RLNC_OK;
@@ -628,35 +622,39 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
 
 namespace {
 
-int dec_store_piece(rlnc_decoder* d, const uint8_t* piece, bool dev) {
-  if (!d->ctx) return RLNC_OK;
-  const size_t row = d->core.received() - 1;
-  if (row + 1 > d->recv_rows) {
-    // grow: keep received rows, double capacity
-    size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, row + 1);
-    if (nrows * d->pitch >= kMaxDescBytes) nrows = std::max(row + 1, kMaxDescBytes / d->pitch - 1);
-    uint8_t* np = nullptr;
-    HIPC(hipMalloc((void**)&np, nrows * d->pitch));
-    HIPC(hipMemsetAsync(np, 0, nrows * d->pitch, d->ctx->stream));
-    if (d->recv.p && row)
-      HIPC(hipMemcpyAsync(np, d->recv.p, row * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
-    HIPC(hipStreamSynchronize(d->ctx->stream));
-    d->recv.release();
-    d->recv.p = np;
-    d->recv.cap = nrows * d->pitch;
-    d->recv_rows = nrows;
-  }
-  HIPC(hipMemcpyAsync(d->recv.p + row * d->pitch, piece, d->L,
-                      dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, d->ctx->stream));
-  if (!dev) HIPC(hipStreamSynchronize(d->ctx->stream));  // the host buffer is only borrowed
+// grow the received-piece buffer so rows [0, need) fit; keeps rows [0, have)
+int dec_reserve_rows(rlnc_decoder* d, size_t need, size_t have) {
+  if (need <= d->recv_rows) return RLNC_OK;
+  size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, need);
+  if (nrows * d->pitch >= kMaxDescBytes) nrows = std::max(need, kMaxDescBytes / d->pitch - 1);
+  uint8_t* np = nullptr;
+  HIPC(hipMalloc((void**)&np, nrows * d->pitch));
+  HIPC(hipMemsetAsync(np, 0, nrows * d->pitch, d->ctx->stream));
+  if (d->recv.p && have)
+    HIPC(hipMemcpyAsync(np, d->recv.p, have * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
+  HIPC(hipStreamSynchronize(d->ctx->stream));
+  d->recv.release();
+  d->recv.p = np;
+  d->recv.cap = nrows * d->pitch;
+  d->recv_rows = nrows;
   return RLNC_OK;
 }
 
-int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
-            bool dev) {
-  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+// store n pieces (source pitch spitch) as received rows [row0, row0 + n)
+int dec_store_pieces(rlnc_decoder* d, size_t row0, const uint8_t* src, size_t spitch, size_t n, bool dev) {
+  if (!d->ctx || !n) return RLNC_OK;
+  TRY(dec_reserve_rows(d, row0 + n, row0));
+  uint8_t* dst = d->recv.p + row0 * d->pitch;
+  if (dev)
+    HIPC(hipMemcpy2DAsync(dst, d->pitch, src, spitch, d->L, n, hipMemcpyDeviceToDevice, d->ctx->stream));
+  else  // staged: the host buffer is only borrowed for the duration of the call
+    HIPC(d->ctx->stage.h2d(dst, d->pitch, src, spitch, d->L, n, d->ctx->stream));
+  return RLNC_OK;
+}
+
+int dec_check(rlnc_decoder* d, size_t vlen, const uint8_t* piece, size_t plen) {
   if (d->core.is_decoded()) return RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;  // full/decoder.go:52-54
-  if (!vec || vlen != d->core.piece_count() || (d->ctx && !piece)) return RLNC_ERR_INVALID_ARGUMENT;
+  if (vlen != d->core.piece_count() || (d->ctx && !piece)) return RLNC_ERR_INVALID_ARGUMENT;
   if (d->have_len && plen != d->L) return RLNC_ERR_INVALID_ARGUMENT;
   if (d->ctx) TRY(set_dev(d->ctx));
   if (!d->have_len) {
@@ -664,16 +662,25 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
     d->pitch = round_up(std::max<size_t>(plen, 1), kPitchAlign);
     d->have_len = true;
   }
+  return RLNC_OK;
+}
+
+int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
+            bool dev) {
+  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  if (d->core.is_decoded()) return RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;
+  if (!vec) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_check(d, vlen, piece, plen));
   TRY(d->core.add(vec));
   d->decoded_ready = false;
-  return dec_store_piece(d, piece, dev);
+  return dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev);
 }
 
 // decoded rows [0, rows) = T x R into dst (device, pitch dpitch)
 int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, size_t dpitch) {
   const size_t recv = d->core.received();
   TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
-  HIPC(hipMemcpyAsync(d->tmat.p, trows, rows * recv, hipMemcpyHostToDevice, d->ctx->stream));
+  HIPC(d->ctx->stage.h2d(d->tmat.p, recv, trows, recv, recv, rows, d->ctx->stream));
   return gemm(d->ctx, d->tmat.p, recv, rows, recv, d->recv.p, d->pitch, dst, dpitch, d->L);
 }
 
@@ -704,25 +711,38 @@ int rlnc_decoder_add_piece_device(rlnc_decoder* d, const uint8_t* vec, size_t vl
 int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
                             int is_device, size_t* consumed) {
   if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
-  const size_t k = d->core.piece_count();
   *consumed = 0;
+  if (!count) return RLNC_OK;
+  const size_t k = d->core.piece_count();
   if (pitch <= k) return RLNC_ERR_INVALID_ARGUMENT;
-  const size_t plen = d->have_len ? d->L : 0;
-  std::vector<uint8_t> vec(k);
-  for (size_t i = 0; i < count; i++) {
-    const uint8_t* row = rows + i * pitch;
-    const uint8_t* v = row;
-    if (is_device) {
-      if (d->ctx) TRY(set_dev(d->ctx));
-      HIPC(hipMemcpy(vec.data(), row, k, hipMemcpyDeviceToHost));
-      v = vec.data();
-    }
-    const size_t L = plen ? plen : pitch - k;
-    int s = dec_add(d, v, k, row + k, L, is_device != 0);
-    if (s != RLNC_OK) return s;
-    (*consumed)++;
+  const bool dev = is_device != 0;
+  if (dev && !d->ctx) return RLNC_ERR_NO_DEVICE;
+  TRY(dec_check(d, k, rows + k, d->have_len ? d->L : pitch - k));
+  if (pitch < k + d->L) return RLNC_ERR_INVALID_ARGUMENT;
+  const uint8_t* vecs = rows;
+  size_t vpitch = pitch;
+  if (dev) {  // one strided copy of all coding vectors; the pieces never leave the device
+    d->hvecs.resize(count * k);
+    HIPC(d->ctx->stage.d2h(d->hvecs.data(), k, rows, pitch, k, count, d->ctx->stream));
+    vecs = d->hvecs.data();
+    vpitch = k;
   }
-  return RLNC_OK;
+  // coefficient side, one row at a time, exactly as repeated AddPiece calls
+  const size_t row0 = d->core.received();
+  int st = RLNC_OK;
+  size_t n = 0;
+  for (; n < count; n++) {
+    if (d->core.is_decoded()) {
+      st = RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;
+      break;
+    }
+    if ((st = d->core.add(vecs + n * vpitch)) != RLNC_OK) break;
+  }
+  if (n) d->decoded_ready = false;
+  // data side: the accepted pieces are consecutive received rows -> one 2D copy
+  TRY(dec_store_pieces(d, row0, rows + k, pitch, n, dev));
+  *consumed = n;
+  return st;
 }
 
 int rlnc_decoder_is_decoded(const rlnc_decoder* d) { return d && d->core.is_decoded(); }
@@ -742,14 +762,14 @@ int rlnc_decoder_get_piece(rlnc_decoder* d, size_t idx, uint8_t* out) {
   TRY(set_dev(d->ctx));
   if (d->core.rank() >= d->core.piece_count()) {
     TRY(dec_materialize(d));
-    HIPC(hipMemcpyAsync(out, d->decoded.p + idx * d->pitch, d->L, hipMemcpyDeviceToHost, d->ctx->stream));
+    HIPC(d->ctx->stage.d2h(out, d->L, d->decoded.p + idx * d->pitch, d->pitch, d->L, 1, d->ctx->stream));
   } else {
     // partial decode (:233-260): materialise the single row idx
     const size_t recv = d->core.received();
     d->hT.assign(d->core.t_row(idx), d->core.t_row(idx) + recv);
     TRY(d->rowbuf.reserve(d->pitch));
     TRY(dec_apply(d, 1, d->hT.data(), d->rowbuf.p, d->pitch));
-    HIPC(hipMemcpyAsync(out, d->rowbuf.p, d->L, hipMemcpyDeviceToHost, d->ctx->stream));
+    HIPC(d->ctx->stage.d2h(out, d->L, d->rowbuf.p, d->pitch, d->L, 1, d->ctx->stream));
   }
   HIPC(hipStreamSynchronize(d->ctx->stream));
   return RLNC_OK;
@@ -763,8 +783,7 @@ int rlnc_decoder_get_pieces(rlnc_decoder* d, uint8_t* out) {
   const size_t useful = d->core.useful();
   for (size_t i = 0; i < useful; i++) TRY(d->core.piece_available(i));  // :89-96
   TRY(dec_materialize(d));
-  HIPC(hipMemcpy2DAsync(out, d->L, d->decoded.p, d->pitch, d->L, useful, hipMemcpyDeviceToHost,
-                        d->ctx->stream));
+  HIPC(d->ctx->stage.d2h(out, d->L, d->decoded.p, d->pitch, d->L, useful, d->ctx->stream));
   HIPC(hipStreamSynchronize(d->ctx->stream));
   return RLNC_OK;
 }
@@ -778,10 +797,7 @@ int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_p
   const size_t rows = d->core.rank(), recv = d->core.received();
   d->hT.resize(std::max<size_t>(rows * recv, 1));
   d->core.copy_transform(d->hT.data(), recv);
-  TRY(dec_apply(d, rows, d->hT.data(), d_out, out_pitch));
-  // the T upload reads hT asynchronously; keep it alive until the copy is done
-  HIPC(hipStreamSynchronize(d->ctx->stream));
-  return RLNC_OK;
+  return dec_apply(d, rows, d->hT.data(), d_out, out_pitch);  // T is staged; no host buffer outlives the call
 }
 
 int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {

@@ -1,0 +1,117 @@
+// staging.hpp -- pinned double-buffered host<->device copies for the
+// host-pointer entry points.  Host buffers handed to the C ABI are pageable
+// (Go slices, numpy arrays); copying through two pinned chunks lets the DMA of
+// one chunk overlap the CPU copy of the next, instead of the driver's slow
+// pageable path.  Host pointers are never retained: h2d returns once the
+// bytes are in pinned memory, d2h once they are in the caller's buffer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace kodr_amd {
+
+class Staging {
+ public:
+  static constexpr size_t kChunk = 8u << 20;
+
+  ~Staging() { release(); }
+
+  hipError_t h2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                 size_t height, hipStream_t s) {
+    if (!width || !height) return hipSuccess;
+    hipError_t e = ensure();
+    if (e != hipSuccess) return e;
+    if (width > kChunk) {  // a single row larger than a chunk: direct copy
+      e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice, s);
+      return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
+    const size_t per = kChunk / width;
+    for (size_t r0 = 0; r0 < height; r0 += per) {
+      const size_t n = std::min(per, height - r0);
+      const int b = next_;
+      next_ ^= 1;
+      if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+      pack(buf_[b], width, src + r0 * spitch, spitch, width, n);
+      e = hipMemcpy2DAsync(dst + r0 * dpitch, dpitch, buf_[b], width, width, n, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) return e;
+      if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
+      pending_[b] = true;
+    }
+    return hipSuccess;
+  }
+
+  hipError_t d2h(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                 size_t height, hipStream_t s) {
+    if (!width || !height) return hipSuccess;
+    hipError_t e = ensure();
+    if (e != hipSuccess) return e;
+    if (width > kChunk) {
+      e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, s);
+      return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
+    const size_t per = kChunk / width;
+    size_t prev_r0 = 0, prev_n = 0;
+    int prev_b = -1;
+    for (size_t r0 = 0; r0 < height; r0 += per) {
+      const size_t n = std::min(per, height - r0);
+      const int b = next_;
+      next_ ^= 1;
+      if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+      e = hipMemcpy2DAsync(buf_[b], width, src + r0 * spitch, spitch, width, n, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) return e;
+      if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
+      pending_[b] = true;
+      if (prev_b >= 0) {  // unpack the previous chunk while this one is in flight
+        if ((e = hipEventSynchronize(ev_[prev_b])) != hipSuccess) return e;
+        pending_[prev_b] = false;
+        pack(dst + prev_r0 * dpitch, dpitch, buf_[prev_b], width, width, prev_n);
+      }
+      prev_b = b;
+      prev_r0 = r0;
+      prev_n = n;
+    }
+    if ((e = hipEventSynchronize(ev_[prev_b])) != hipSuccess) return e;
+    pending_[prev_b] = false;
+    pack(dst + prev_r0 * dpitch, dpitch, buf_[prev_b], width, width, prev_n);
+    return hipSuccess;
+  }
+
+  void release() {
+    for (int b = 0; b < 2; b++) {
+      if (pending_[b]) (void)hipEventSynchronize(ev_[b]);
+      if (ev_[b]) (void)hipEventDestroy(ev_[b]);
+      if (buf_[b]) (void)hipHostFree(buf_[b]);
+      ev_[b] = nullptr;
+      buf_[b] = nullptr;
+      pending_[b] = false;
+    }
+  }
+
+ private:
+  hipError_t ensure() {
+    if (buf_[0]) return hipSuccess;
+    for (int b = 0; b < 2; b++) {
+      hipError_t e = hipHostMalloc((void**)&buf_[b], kChunk, hipHostMallocDefault);
+      if (e != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&ev_[b], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  static void pack(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width, size_t n) {
+    if (dpitch == width && spitch == width) {
+      memcpy(dst, src, width * n);
+      return;
+    }
+    for (size_t i = 0; i < n; i++) memcpy(dst + i * dpitch, src + i * spitch, width);
+  }
+
+  uint8_t* buf_[2] = {nullptr, nullptr};
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  bool pending_[2] = {false, false};
+  int next_ = 0;
+};
+
+}  // namespace kodr_amd

@@ -257,3 +257,110 @@ def test_decode_matches_oracle_with_dependent_and_quirky_pieces(gpu_ctx):
                 assert st == st_r
                 if st == 0:
                     assert np.array_equal(got, got_r)
+
+
+def _add_rows(d, rows_ptr, count, pitch, dev):
+    consumed = ctypes.c_size_t()
+    st = _lib.lib().rlnc_decoder_add_pieces(d.h, rows_ptr, count, pitch, int(dev), ctypes.byref(consumed))
+    return st, consumed.value
+
+
+def test_batch_add_golden_traces(gpu_ctx, golden):
+    """rlnc_decoder_add_pieces over a whole golden stream == AddPiece row by row."""
+    for c in golden["vectors"]["decode"]:
+        rows = [np.concatenate([h(v), h(p)]) for v, p in c["stream"]]
+        if len({r.size for r in rows}) != 1:
+            continue
+        W = np.stack(rows)
+        errs = [s["err"] for s in c["steps"]]
+        first_bad = next((i for i, e in enumerate(errs) if e is not None), len(errs))
+        for dev in (False, True):
+            d = Dec(gpu_ctx, c["k"])
+            if dev:
+                dW = gpu_ctx.alloc(W.nbytes)
+                gpu_ctx.h2d(dW, W)
+                st, n = _add_rows(d, ctypes.c_void_p(dW), W.shape[0], W.shape[1], True)
+            else:
+                st, n = _add_rows(d, ptr(W), W.shape[0], W.shape[1], False)
+            assert n == first_bad, c["name"]
+            assert st == (ERR[errs[first_bad]] if first_bad < len(errs) else 0), c["name"]
+            last = c["steps"][first_bad - 1] if first_bad else None
+            if last is not None:
+                assert d.state() == (last["useful"], last["received"], last["required"], last["decoded"])
+            if c["decoded"] is not None:
+                st, allp = d.get_all()
+                assert st == 0
+                assert [r.tobytes().hex() for r in allp] == c["decoded"], c["name"]
+            if dev:
+                gpu_ctx.synchronize()
+                gpu_ctx.free(dW)
+
+
+@pytest.mark.parametrize("k,L", [(7, 45), (32, 4096), (64, 1024)])
+def test_batch_add_random_batches_vs_oracle(gpu_ctx, k, L):
+    """Random batch sizes, host and device rows at a padded pitch, mixed with
+    single AddPiece calls; state and pieces bit-exact vs the oracle decoder."""
+    rng = np.random.default_rng(k * 1000 + L)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    d, ref = Dec(gpu_ctx, k), oracle.Decoder(k)
+    pitch = ((k + L + 255) // 256) * 256 + 32
+    dbuf = gpu_ctx.alloc(pitch * 4 * k)
+    it = 0
+    while not ref.is_decoded() and it < 50:
+        it += 1
+        n = int(rng.integers(1, k + 3))
+        V = rng.integers(0, 256 if rng.random() < 0.5 else 3, (n, k), dtype=np.uint8)
+        C = oracle.encode(P, V)
+        rows = np.zeros((n, pitch), np.uint8)
+        rows[:, :k], rows[:, k:k + L] = V, C
+        mode = it % 3
+        if mode == 2:  # piecewise
+            for i in range(n):
+                assert d.add(V[i], C[i]) == ref.add(V[i], C[i])
+            continue
+        exp_n, exp_st = 0, 0
+        for i in range(n):
+            s = ref.add(V[i], C[i])
+            if s != 0:
+                exp_st = s
+                break
+            exp_n += 1
+        if mode == 1:
+            gpu_ctx.h2d(dbuf, rows)
+            st, got_n = _add_rows(d, ctypes.c_void_p(dbuf), n, pitch, True)
+        else:
+            st, got_n = _add_rows(d, ptr(rows), n, pitch, False)
+        assert (st, got_n) == (exp_st, exp_n)
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+    assert ref.is_decoded()
+    st, allp = d.get_all()
+    assert st == 0 and np.array_equal(allp, P)
+    gpu_ctx.synchronize()
+    gpu_ctx.free(dbuf)
+
+
+def test_batch_add_argument_errors(gpu_ctx):
+    k, L = 4, 16
+    d = Dec(gpu_ctx, k)
+    rows = np.zeros((2, k + L), np.uint8)
+    assert _add_rows(d, ptr(rows), 0, k + L, False) == (0, 0)
+    assert _add_rows(d, ptr(rows), 2, k, False)[0] == -1          # pitch <= k
+    assert d.add(np.eye(k, dtype=np.uint8)[0], np.zeros(L, np.uint8)) == 0   # fixes L = 16
+    assert _add_rows(d, ptr(rows), 1, k + L - 1, False)[0] == -1  # pitch < k + L
+    assert _add_rows(d, ptr(rows), 2, k + L, False) == (0, 2)
+
+
+def test_rows_wider_than_staging_chunk(gpu_ctx):
+    """Pieces longer than the 8 MiB pinned staging chunk take the direct-copy
+    path: encode + batched decode round trip through host buffers."""
+    rng = np.random.default_rng(11)
+    k, L = 3, (9 << 20) + 5
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    V, out = e.code(rng.integers(0, 256, (k + 1, k), dtype=np.uint8))
+    assert np.array_equal(out[:, k:], oracle.encode(P, V))
+    d = Dec(gpu_ctx, k)
+    st, n = _add_rows(d, ptr(out), out.shape[0], out.shape[1], False)
+    assert st in (0, 3) and n >= k
+    st, allp = d.get_all()
+    assert st == 0 and np.array_equal(allp, P)
