@@ -319,7 +319,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
         errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
         consumed = ctypes.c_size_t()
         t0 = time.perf_counter()
-        st = L_.rlnc_decoder_add_pieces(dh, dWire, n, W, 1, ctypes.byref(consumed))
+        st = L_.rlnc_decoder_add_pieces(dh, dWire, n, W, L, 1, ctypes.byref(consumed))
         if st != 3:
             errors.check(st)
         errors.check(L_.rlnc_decoder_get_pieces_device(dh, dDec, L))
@@ -385,7 +385,7 @@ def host_roundtrip(ctx, L_, errors, k, L, rng):
     dh = ctypes.c_void_p()
     errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
     consumed = ctypes.c_size_t()
-    st = L_.rlnc_decoder_add_pieces(dh, wire.ctypes.data_as(u8p), n, k + L, 0, ctypes.byref(consumed))
+    st = L_.rlnc_decoder_add_pieces(dh, wire.ctypes.data_as(u8p), n, k + L, L, 0, ctypes.byref(consumed))
     if st != 3:
         errors.check(st)
     errors.check(L_.rlnc_decoder_get_pieces(dh, outp.ctypes.data_as(u8p)))

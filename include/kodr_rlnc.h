@@ -170,15 +170,15 @@ int rlnc_decoder_add_piece(rlnc_decoder* dec, const uint8_t* vector, size_t vect
 int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                                   const uint8_t* d_piece, size_t piece_len);
 /* batch AddPiece over `count` wire rows (vector ++ piece, as CodedPiece.Flatten,
- * kodr_internals/coded.go) at row pitch `pitch`, on the host or the device
- * (is_device).  The piece length is the decoder's L, or pitch - piece_count
- * if no piece was added yet.  Same result as calling AddPiece row by row:
+ * kodr_internals/coded.go) at row pitch `pitch` >= piece_count + piece_len,
+ * on the host or the device (is_device).  piece_len follows AddPiece's rule
+ * (fixed by the first piece).  Same result as calling AddPiece row by row:
  * stops at the first error (RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED once decoded)
  * with *consumed = pieces accepted.  The accepted pieces are stored with ONE
  * strided copy (host rows staged through pinned memory; device rows D2D,
  * async, only the coding vectors are read back). */
 int rlnc_decoder_add_pieces(rlnc_decoder* dec, const uint8_t* rows, size_t count, size_t pitch,
-                            int is_device, size_t* consumed);
+                            size_t piece_len, int is_device, size_t* consumed);
 int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */
 size_t rlnc_decoder_required(const rlnc_decoder* dec);       /* Required  :38-40 */
 size_t rlnc_decoder_useful(const rlnc_decoder* dec);         /* rank */

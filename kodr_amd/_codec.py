@@ -187,15 +187,15 @@ class _Decoder:
         rows = np.ascontiguousarray(rows, dtype=np.uint8)
         if rows.ndim != 2:
             raise ValueError("rows must be a 2-D array of wire rows")
-        return self._add_rows(rows.ctypes.data, rows.shape[0], rows.shape[1], False)
+        return self._add_rows(rows.ctypes.data, rows.shape[0], rows.shape[1], rows.shape[1] - self._k, False)
 
-    def add_wire_rows_device(self, d_rows, count, pitch):
+    def add_wire_rows_device(self, d_rows, count, pitch, piece_len):
         """Same, with the wire rows resident on the device (pointer, row pitch)."""
-        return self._add_rows(d_rows, count, pitch, True)
+        return self._add_rows(d_rows, count, pitch, piece_len, True)
 
-    def _add_rows(self, ptr, count, pitch, dev):
+    def _add_rows(self, ptr, count, pitch, piece_len, dev):
         consumed = ctypes.c_size_t()
-        st = lib().rlnc_decoder_add_pieces(self._h, ctypes.c_void_p(ptr), count, pitch, int(dev),
+        st = lib().rlnc_decoder_add_pieces(self._h, ctypes.c_void_p(ptr), count, pitch, piece_len, int(dev),
                                            ctypes.byref(consumed))
         if st != 3:
             errors.check(st)

@@ -709,16 +709,15 @@ int rlnc_decoder_add_piece_device(rlnc_decoder* d, const uint8_t* vec, size_t vl
 }
 
 int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
-                            int is_device, size_t* consumed) {
+                            size_t piece_len, int is_device, size_t* consumed) {
   if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
   *consumed = 0;
   if (!count) return RLNC_OK;
   const size_t k = d->core.piece_count();
-  if (pitch <= k) return RLNC_ERR_INVALID_ARGUMENT;
+  if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
   const bool dev = is_device != 0;
   if (dev && !d->ctx) return RLNC_ERR_NO_DEVICE;
-  TRY(dec_check(d, k, rows + k, d->have_len ? d->L : pitch - k));
-  if (pitch < k + d->L) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_check(d, k, rows + k, piece_len));
   const uint8_t* vecs = rows;
   size_t vpitch = pitch;
   if (dev) {  // one strided copy of all coding vectors; the pieces never leave the device

@@ -259,9 +259,11 @@ def test_decode_matches_oracle_with_dependent_and_quirky_pieces(gpu_ctx):
                     assert np.array_equal(got, got_r)
 
 
-def _add_rows(d, rows_ptr, count, pitch, dev):
+def _add_rows(d, rows_ptr, count, pitch, dev, plen=None):
     consumed = ctypes.c_size_t()
-    st = _lib.lib().rlnc_decoder_add_pieces(d.h, rows_ptr, count, pitch, int(dev), ctypes.byref(consumed))
+    k = _lib.lib().rlnc_decoder_piece_count(d.h)
+    plen = pitch - k if plen is None else plen
+    st = _lib.lib().rlnc_decoder_add_pieces(d.h, rows_ptr, count, pitch, plen, int(dev), ctypes.byref(consumed))
     return st, consumed.value
 
 
@@ -327,9 +329,9 @@ def test_batch_add_random_batches_vs_oracle(gpu_ctx, k, L):
             exp_n += 1
         if mode == 1:
             gpu_ctx.h2d(dbuf, rows)
-            st, got_n = _add_rows(d, ctypes.c_void_p(dbuf), n, pitch, True)
+            st, got_n = _add_rows(d, ctypes.c_void_p(dbuf), n, pitch, True, L)
         else:
-            st, got_n = _add_rows(d, ptr(rows), n, pitch, False)
+            st, got_n = _add_rows(d, ptr(rows), n, pitch, False, L)
         assert (st, got_n) == (exp_st, exp_n)
         assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
     assert ref.is_decoded()
@@ -344,9 +346,9 @@ def test_batch_add_argument_errors(gpu_ctx):
     d = Dec(gpu_ctx, k)
     rows = np.zeros((2, k + L), np.uint8)
     assert _add_rows(d, ptr(rows), 0, k + L, False) == (0, 0)
-    assert _add_rows(d, ptr(rows), 2, k, False)[0] == -1          # pitch <= k
+    assert _add_rows(d, ptr(rows), 2, k + L, False, L + 1)[0] == -1   # pitch < k + piece_len
     assert d.add(np.eye(k, dtype=np.uint8)[0], np.zeros(L, np.uint8)) == 0   # fixes L = 16
-    assert _add_rows(d, ptr(rows), 1, k + L - 1, False)[0] == -1  # pitch < k + L
+    assert _add_rows(d, ptr(rows), 1, k + L, False, L - 1)[0] == -1  # piece length differs
     assert _add_rows(d, ptr(rows), 2, k + L, False) == (0, 2)
 
 

@@ -17,7 +17,7 @@ if [[ "$STAGE" == all || "$STAGE" == tests ]]; then
   cat "$OUT/smoke.log"
 fi
 if [[ "$STAGE" == all || "$STAGE" == bench ]]; then
-  run timeout -k 10 600 python bench.py --extras > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
+  run timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -30 "$OUT/bench.err"; exit 1; }
   cat "$OUT/bench.json"
 fi
 if [[ "$STAGE" == all || "$STAGE" == prof ]]; then
