@@ -225,20 +225,16 @@ def run_relay(ctx, L_, errors, enc, k, L, rng, torch, dist, kdist):
     send = torch.zeros(k * pitch, dtype=torch.uint8, device="cuda")
     recv = torch.empty_like(send)
     out = torch.empty_like(send)
-    V = rng.integers(0, 256, (k, k), dtype=np.uint8)
     Rv = rng.integers(0, 256, (k, k), dtype=np.uint8)
-    dV, dR = ctx.alloc(V.nbytes), ctx.alloc(Rv.nbytes)
-    ctx.h2d(dV, V)
+    dR = ctx.alloc(Rv.nbytes)
     ctx.h2d(dR, Rv)
-    # wire rows: vectors into columns [0, k), pieces into [k, k+L)
-    sview = send.view(k, pitch)
-    sview[:, :k] = torch.from_numpy(V).cuda()
     times = {"encode": [], "exchange": [], "recode": []}
     for rep in range(6):
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        errors.check(L_.rlnc_encoder_coded_pieces_device(enc, dV, k, send.data_ptr() + k, pitch))
+        # k wire rows [vector | piece], vectors drawn on the device
+        errors.check(L_.rlnc_encoder_coded_wire_device(enc, k, send.data_ptr(), pitch))
         ctx.synchronize()
         t1 = time.perf_counter()
         kdist.ring_shift(send, recv)
@@ -255,7 +251,6 @@ def run_relay(ctx, L_, errors, enc, k, L, rng, torch, dist, kdist):
             times["encode"].append(t1 - t0)
             times["exchange"].append(t2 - t1)
             times["recode"].append(t3 - t2)
-    ctx.free(dV)
     ctx.free(dR)
     res = {}
     for name, ts in times.items():
@@ -301,37 +296,35 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["encode_batch_sweep"] = sweep
     ctx.free(dVs)
     ctx.free(dOs)
-    # decode: k + 2 coded pieces encoded on device as wire rows [vector | piece],
-    # then one batched AddPiece call + GetPieces (device-resident throughout)
-    n = k + 2
+    # coded pieces in wire layout with device-drawn vectors
     W = k + L
-    Vd = rng.integers(0, 256, (n, k), dtype=np.uint8)
-    wire = np.zeros((n, W), np.uint8)
-    wire[:, :k] = Vd
-    dVd, dWire, dDec = ctx.alloc(Vd.nbytes), ctx.alloc(n * W), ctx.alloc(k * L)
-    ctx.h2d(dVd, Vd)
-    ctx.h2d(dWire, wire)
-    errors.check(L_.rlnc_encoder_coded_pieces_device(encs[0], dVd, n, dWire + k, W))
-    ctx.synchronize()
-    times, times_pw = [], []
-    for rep in range(3):
+    dWire = ctx.alloc((k + 2) * W)
+    for i in range(3):
+        errors.check(L_.rlnc_encoder_coded_wire_device(encs[i % len(encs)], B, dWire, W))
+    ctx.record(e0)
+    for i in range(40):
+        errors.check(L_.rlnc_encoder_coded_wire_device(encs[i % len(encs)], B, dWire, W))
+    ctx.record(e1)
+    tw = kdev.Context.elapsed_ms(e0, e1) / 1e3 / 40
+    out["encode_wire_device_rng_MBps"] = round(B * setbytes(k, L) / tw / 1e6, 1)
+    # decode C2: k + 2 wire rows on the device -> one batched AddPiece call + GetPieces
+    n = k + 2
+    L_.rlnc_encoder_seed(encs[0], 7)
+    errors.check(L_.rlnc_encoder_coded_wire_device(encs[0], n, dWire, W))
+    dDec = ctx.alloc(k * L)
+    out["c2_decode"] = time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec)
+    td = out["c2_decode"]["s"]
+    out["c2_decode"]["MBps_decodable_len"] = round(k * (k + L) / td / 1e6, 1)
+    out["c2_decode"]["gf_macs_per_s"] = float(f"{k * k * L / td:.4g}")
+    # the same decode fed one AddPiece call per piece
+    Vd = ctx.d2h(dWire, n * W).reshape(n, W)[:, :k].copy()
+    times_pw = []
+    for rep in range(2):
         dh = ctypes.c_void_p()
-        errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
-        consumed = ctypes.c_size_t()
-        t0 = time.perf_counter()
-        st = L_.rlnc_decoder_add_pieces(dh, dWire, n, W, L, 1, ctypes.byref(consumed))
-        if st != 3:
-            errors.check(st)
-        errors.check(L_.rlnc_decoder_get_pieces_device(dh, dDec, L))
-        ctx.synchronize()
-        times.append(time.perf_counter() - t0)
-        L_.rlnc_decoder_destroy(dh)
-        # the same decode fed one AddPiece call per piece
         errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
         t0 = time.perf_counter()
         for i in range(n):
-            v = np.ascontiguousarray(Vd[i])
-            st = L_.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), k,
+            st = L_.rlnc_decoder_add_piece_device(dh, Vd[i].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), k,
                                                   dWire + i * W + k, L)
             if st == 3:
                 break
@@ -340,25 +333,103 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
         ctx.synchronize()
         times_pw.append(time.perf_counter() - t0)
         L_.rlnc_decoder_destroy(dh)
-    td = min(times)
-    out["decode_s"] = round(td, 6)
-    out["decode_piecewise_s"] = round(min(times_pw), 6)
-    out["decode_MBps_decodable_len"] = round(k * (k + L) / td / 1e6, 1)
-    out["decode_gf_macs_per_s"] = float(f"{k * k * L / td:.4g}")
-    # verify the decode of the first generation against the resident pieces
-    ptr_p, pitch = ctypes.c_size_t(), ctypes.c_size_t()
+    out["c2_decode"]["piecewise_s"] = round(min(times_pw), 6)
+    # verify the decode against the resident generation
+    pitch = ctypes.c_size_t()
     dp = L_.rlnc_encoder_device_pieces(encs[0], ctypes.byref(pitch))
     a = ctx.d2h(dDec, k * L)
     b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
-    out["decode_roundtrip_ok"] = bool(np.array_equal(a, b))
-    ctx.free(dVd)
+    out["c2_decode"]["roundtrip_ok"] = bool(np.array_equal(a, b))
     ctx.free(dWire)
     ctx.free(dDec)
+    out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
     out["host_path"] = host_roundtrip(ctx, L_, errors, k, L, rng)
+    out["host_path_registered"] = host_roundtrip(ctx, L_, errors, k, L, rng, pinned=True)
     return out
 
 
-def host_roundtrip(ctx, L_, errors, k, L, rng):
+VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9      # integer VALU lane-ops/s (MI355X_MICROARCH.md)
+LANE_OPS_PER_MAC = 4.5 / 4                 # 3 v_perm + 1.5 v_bitop3 per coefficient x 4 bytes
+
+
+def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
+    """One batched AddPiece call over n device wire rows + GetPieces into
+    device memory (synchronous), best of reps fresh decoders."""
+    import ctypes
+    best = None
+    for rep in range(reps):
+        dh = ctypes.c_void_p()
+        errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
+        consumed = ctypes.c_size_t()
+        t0 = time.perf_counter()
+        st = L_.rlnc_decoder_add_pieces(dh, dWire, n, W, L, 1, ctypes.byref(consumed))
+        if st != 3:
+            errors.check(st)
+        t1 = time.perf_counter()
+        errors.check(L_.rlnc_decoder_get_pieces_device(dh, dDec, L))
+        ctx.synchronize()
+        t2 = time.perf_counter()
+        gf, cp = ctypes.c_size_t(), ctypes.c_size_t()
+        errors.check(L_.rlnc_decoder_apply_stats(dh, ctypes.byref(gf), ctypes.byref(cp)))
+        decoded = bool(L_.rlnc_decoder_is_decoded(dh))
+        recv = L_.rlnc_decoder_received(dh)
+        L_.rlnc_decoder_destroy(dh)
+        if best is None or t2 - t0 < best["s"]:
+            best = {"s": round(t2 - t0, 6), "add_s": round(t1 - t0, 6), "get_s": round(t2 - t1, 6),
+                    "gf_rows": gf.value, "copy_rows": cp.value, "received": recv, "decoded": decoded}
+    macs = best["gf_rows"] * best["received"] * L
+    best["apply_gf_macs"] = macs
+    best["apply_gf_macs_per_s"] = float(f"{macs / best['get_s']:.4g}")
+    best["valu_ceiling_macs_per_s"] = float(f"{VALU_LANE_OPS / LANE_OPS_PER_MAC:.4g}")
+    return best
+
+
+def c4_decode(ctx, L_, errors, rng):
+    """BASELINE config 4 (systematic 16 MiB/128): 10% of the systematic pieces
+    lost and replaced by coded ones.  The decoder copies the systematic rows and
+    runs GF work only for the missing ones; the same generation
+    decoded from coded pieces only is timed beside it.  kodr: 1.821 s
+    (README.md:188)."""
+    import ctypes
+    import numpy as np
+    k, L = 128, 131072
+    W = k + L
+    data = rng.integers(0, 256, k * L, dtype=np.uint8)
+    eh = ctypes.c_void_p()
+    errors.check(L_.rlnc_encoder_create(ctx.handle, 1, data.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), k, L,
+                                        ctypes.byref(eh)))
+    errors.check(L_.rlnc_encoder_seed(eh, 4))
+    n = 2 * k + 4
+    dAll = ctx.alloc(n * W)
+    errors.check(L_.rlnc_encoder_coded_wire_device(eh, n, dAll, W))
+    rows = ctx.d2h(dAll, n * W).reshape(n, W)
+    lost = set(rng.choice(k, k // 10, replace=False).tolist())
+    keep = [i for i in range(k) if i not in lost] + list(range(k, n))
+    kept = np.ascontiguousarray(rows[keep])
+    coded = np.ascontiguousarray(rows[k:])
+    dKept, dCoded, dDec = ctx.alloc(kept.nbytes), ctx.alloc(coded.nbytes), ctx.alloc(k * L)
+    ctx.h2d(dKept, kept)
+    ctx.h2d(dCoded, coded)
+    res = {"lost_systematic": len(lost)}
+    res["systematic"] = time_decode(ctx, L_, errors, dKept, kept.shape[0], W, k, L, dDec)
+    ok = bool(np.array_equal(ctx.d2h(dDec, k * L), data))
+    res["full_coded_only"] = time_decode(ctx, L_, errors, dCoded, coded.shape[0], W, k, L, dDec)
+    ok = ok and bool(np.array_equal(ctx.d2h(dDec, k * L), data))
+    res["roundtrip_ok"] = ok
+    res["speedup_vs_full"] = round(res["full_coded_only"]["s"] / res["systematic"]["s"], 2)
+    for p in (dAll, dKept, dCoded, dDec):
+        ctx.free(p)
+    L_.rlnc_encoder_destroy(eh)
+    return res
+
+
+def _page_aligned(np, n):
+    buf = np.empty((n + 4095) // 4096 * 4096 + 4096, np.uint8)
+    off = (-buf.ctypes.data) % 4096
+    return buf[off:off + n]
+
+
+def host_roundtrip(ctx, L_, errors, k, L, rng, pinned=False):
     """The path as it sits in a service: 32 MiB from host memory -> device
     generation -> k+2 coded pieces back to host (batches of 16) -> decoder fed
     from host buffers in one batched AddPiece call -> decoded pieces back to
@@ -367,11 +438,19 @@ def host_roundtrip(ctx, L_, errors, k, L, rng):
     import ctypes
     import numpy as np
     u8p = ctypes.POINTER(ctypes.c_uint8)
-    data = rng.integers(0, 256, k * L, dtype=np.uint8)
     n = k + 2
-    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
-    wire = np.empty((n, k + L), np.uint8)
-    outp = np.empty(k * L, np.uint8)
+    if pinned:  # caller-owned page-locked slabs (rlnc_host_register)
+        data, V = _page_aligned(np, k * L), _page_aligned(np, n * k).reshape(n, k)
+        wire, outp = _page_aligned(np, n * (k + L)).reshape(n, k + L), _page_aligned(np, k * L)
+        for a in (data, V, wire, outp):
+            ctx.register(a)
+        data[:] = rng.integers(0, 256, k * L, dtype=np.uint8)
+        V[:] = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    else:
+        data = rng.integers(0, 256, k * L, dtype=np.uint8)
+        V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        wire = np.empty((n, k + L), np.uint8)
+        outp = np.empty(k * L, np.uint8)
     t0 = time.perf_counter()
     eh = ctypes.c_void_p()
     errors.check(L_.rlnc_encoder_create_with_piece_count(ctx.handle, 0, data.ctypes.data_as(u8p), data.size, k,
@@ -393,6 +472,9 @@ def host_roundtrip(ctx, L_, errors, k, L, rng):
     ok = bool(np.array_equal(outp, data))
     L_.rlnc_decoder_destroy(dh)
     L_.rlnc_encoder_destroy(eh)
+    if pinned:
+        for a in (data, V, wire, outp):
+            ctx.unregister(a)
     return {"upload_ms": round((t1 - t0) * 1e3, 3),
             "encode_k+2_to_host_ms": round((t2 - t1) * 1e3, 3),
             "encode_coded_MBps_incl_pcie": round(n * setbytes(k, L) / (t2 - t1) / 1e6, 1),

@@ -77,6 +77,11 @@ int rlnc_dev_free(rlnc_ctx* ctx, void* dptr);
 int rlnc_memcpy_h2d(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
 int rlnc_memcpy_d2h(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
 int rlnc_memcpy_d2d_async(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* page-lock a caller buffer (e.g. a socket/file staging slab):
+ * host-pointer entry points then DMA straight from / into it instead of
+ * bouncing through the context's pinned chunks.  Unregister before freeing. */
+int rlnc_host_register(rlnc_ctx* ctx, void* ptr, size_t bytes);
+int rlnc_host_unregister(rlnc_ctx* ctx, void* ptr);
 /* stream-ordered timing: record a named mark, read elapsed ms between two */
 int rlnc_event_create(rlnc_ctx* ctx, void** ev);
 int rlnc_event_record(rlnc_ctx* ctx, void* ev);
@@ -135,6 +140,18 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* enc, uint8_t* vectors, size_t count,
  * Full-RLNC semantics (no systematic phase).  Async on the ctx stream. */
 int rlnc_encoder_coded_pieces_device(rlnc_encoder* enc, const uint8_t* d_vectors, size_t count,
                                      uint8_t* d_out, size_t out_pitch);
+/* device-resident coded pieces in wire layout with the coding vectors drawn
+ * on the device (replaces GenerateCodingVector's crypto/rand, data.go:90-95,
+ * for large batches): d_wire gets `count` rows of k+L bytes
+ * (vector ++ piece, as CodedPiece.Flatten) at pitch wire_pitch >= k+L.
+ * Vector bytes are a counter-based pseudo-random stream of the encoder's seed
+ * (drawn from getrandom at create; rlnc_encoder_seed resets it), uniform,
+ * zeros allowed, not cryptographic.  A systematic encoder still emits e_id ++
+ * P_id for its first k pieces (systematic/encoder.go:83-96).  count <= 65535.
+ * Async on the ctx stream. */
+int rlnc_encoder_coded_wire_device(rlnc_encoder* enc, size_t count, uint8_t* d_wire, size_t wire_pitch);
+/* reseed the device vector stream (reproducible batches for tests/benches) */
+int rlnc_encoder_seed(rlnc_encoder* enc, uint64_t seed);
 
 /* ---- recoder: full/recoder.go ------------------------------------------ */
 /* NewFullRLNCRecoderWithFlattenData (full/recoder.go:63-70): flat holds
@@ -195,6 +212,9 @@ int rlnc_decoder_get_pieces_device(rlnc_decoder* dec, uint8_t* d_out, size_t out
  * coefficient matrix (useful x piece_count) and the transform T
  * (useful x received) with coded rows == T x received pieces */
 int rlnc_decoder_coefficients(const rlnc_decoder* dec, uint8_t* out);
+/* rows of the last data-side materialization (GetPiece/GetPieces) that went
+ * through the GF kernel vs were plain copies of received systematic pieces */
+int rlnc_decoder_apply_stats(const rlnc_decoder* dec, size_t* gf_rows, size_t* copy_rows);
 int rlnc_decoder_transform(const rlnc_decoder* dec, uint8_t* out);
 
 /* ---- raw kernel entry: Y = A (x) X over GF(2^8) ------------------------ */

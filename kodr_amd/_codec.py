@@ -82,6 +82,15 @@ class _Encoder:
                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return vec.reshape(count, k), out.reshape(count, clen)
 
+    def seed(self, seed):
+        """Reseed the device-side vector stream of coded_wire_device."""
+        errors.check(lib().rlnc_encoder_seed(self._h, ctypes.c_uint64(seed)))
+
+    def coded_wire_device(self, count, d_wire, pitch):
+        """`count` coded pieces in wire layout (vector ++ piece) written to
+        device rows d_wire at `pitch`, vectors drawn on the device."""
+        errors.check(lib().rlnc_encoder_coded_wire_device(self._h, count, ctypes.c_void_p(d_wire), pitch))
+
     def CodedPiece(self):
         """full/encoder.go:61-71 / systematic/encoder.go:82-109."""
         if not self._queue:

@@ -34,6 +34,8 @@ SIGNATURES = {
     "rlnc_memcpy_h2d": (_int, [_vp, _vp, _vp, _sz]),
     "rlnc_memcpy_d2h": (_int, [_vp, _vp, _vp, _sz]),
     "rlnc_memcpy_d2d_async": (_int, [_vp, _vp, _vp, _sz]),
+    "rlnc_host_register": (_int, [_vp, _vp, _sz]),
+    "rlnc_host_unregister": (_int, [_vp, _vp]),
     "rlnc_event_create": (_int, [_vp, _vpp]),
     "rlnc_event_record": (_int, [_vp, _vp]),
     "rlnc_event_elapsed_ms": (_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
@@ -56,6 +58,8 @@ SIGNATURES = {
     "rlnc_encoder_systematic_remaining": (_sz, [_vp]),
     "rlnc_encoder_coded_pieces": (_int, [_vp, _u8p, _sz, _u8p]),
     "rlnc_encoder_coded_pieces_device": (_int, [_vp, _vp, _sz, _vp, _sz]),
+    "rlnc_encoder_coded_wire_device": (_int, [_vp, _sz, _vp, _sz]),
+    "rlnc_encoder_seed": (_int, [_vp, ctypes.c_uint64]),
     "rlnc_recoder_create": (_int, [_vp, _u8p, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_create_device": (_int, [_vp, _vp, _sz, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_destroy": (_int, [_vp]),
@@ -78,6 +82,7 @@ SIGNATURES = {
     "rlnc_decoder_get_pieces": (_int, [_vp, _u8p]),
     "rlnc_decoder_get_pieces_device": (_int, [_vp, _vp, _sz]),
     "rlnc_decoder_coefficients": (_int, [_vp, _u8p]),
+    "rlnc_decoder_apply_stats": (_int, [_vp, _szp, _szp]),
     "rlnc_decoder_transform": (_int, [_vp, _u8p]),
     "rlnc_gf_matmul_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
 }

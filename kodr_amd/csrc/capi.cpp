@@ -91,6 +91,7 @@ struct rlnc_encoder {
   int kind = RLNC_FULL;
   size_t k = 0, L = 0, pitch = 0, padding = 0;
   size_t sys_next = 0;       // systematic/encoder.go:8 currentPieceId
+  uint64_t seed = 0, drawn = 0;  // device vector RNG: seed, rows drawn so far
   DevBuf pieces;             // k x pitch, zero padded
   DevBuf vecs, out;          // staging for host-pointer calls
 };
@@ -115,6 +116,10 @@ struct rlnc_decoder {
   bool decoded_ready = false;
   std::vector<uint8_t> hT;
   std::vector<uint8_t> hvecs;  // coding vectors of a device batch
+  std::vector<uint8_t> hTc;    // transform rows that need GF work
+  std::vector<const uint8_t*> hsrc;  // per output row: source row of the gather
+  DevBuf scratch, srcs;        // GF rows before the gather; device copy of hsrc
+  size_t last_gf_rows = 0, last_copy_rows = 0;
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -170,6 +175,7 @@ int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** ou
   if (!e) return RLNC_ERR_OUT_OF_MEMORY;
   e->ctx = ctx;
   e->kind = kind;
+  (void)rlnc_random_bytes(reinterpret_cast<uint8_t*>(&e->seed), sizeof(e->seed));
   e->k = k;
   e->L = L;
   e->pitch = round_up(L, kPitchAlign);
@@ -300,14 +306,25 @@ int rlnc_dev_free(rlnc_ctx* ctx, void* dptr) {
 }
 int rlnc_memcpy_h2d(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
   TRY(set_dev(ctx));
-  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIPC(ctx->stage.h2d((uint8_t*)dst, bytes, (const uint8_t*)src, bytes, bytes, 1, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   return RLNC_OK;
 }
 int rlnc_memcpy_d2h(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
   TRY(set_dev(ctx));
-  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
+  HIPC(ctx->stage.d2h((uint8_t*)dst, bytes, (const uint8_t*)src, bytes, bytes, 1, ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_host_register(rlnc_ctx* ctx, void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return RLNC_OK;
+}
+int rlnc_host_unregister(rlnc_ctx* ctx, void* ptr) {
+  if (!ptr) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(hipHostUnregister(ptr));
   return RLNC_OK;
 }
 int rlnc_memcpy_d2d_async(rlnc_ctx* ctx, void* dst, const void* src, size_t bytes) {
@@ -463,13 +480,17 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, u
   hipStream_t st = e->ctx->stream;
   size_t i = 0;
   // systematic/encoder.go:83-96: the first k calls return e_id ++ copy(P_id)
-  while (i < count && e->kind == RLNC_SYSTEMATIC && e->sys_next < k) {
-    const size_t id = e->sys_next++;
-    memset(vectors + i * k, 0, k);
-    vectors[i * k + id] = 1;
-    memcpy(out + i * clen, vectors + i * k, k);
-    HIPC(e->ctx->stage.d2h(out + i * clen + k, clen, e->pieces.p + id * e->pitch, e->pitch, L, 1, st));
-    i++;
+  if (e->kind == RLNC_SYSTEMATIC && e->sys_next < k && count) {
+    const size_t n = std::min(count, k - e->sys_next), id0 = e->sys_next;
+    for (size_t r = 0; r < n; r++) {
+      memset(vectors + r * k, 0, k);
+      vectors[r * k + id0 + r] = 1;
+      memcpy(out + r * clen, vectors + r * k, k);
+    }
+    // consecutive piece ids: one strided copy of rows id0 .. id0+n-1
+    HIPC(e->ctx->stage.d2h(out + k, clen, e->pieces.p + id0 * e->pitch, e->pitch, L, n, st));
+    e->sys_next += n;
+    i = n;
   }
   // full/encoder.go:61-71 (and systematic/encoder.go:98-108) in batches
   const size_t kBatch = 256;
@@ -492,6 +513,37 @@ int rlnc_encoder_coded_pieces_device(rlnc_encoder* e, const uint8_t* d_vectors, 
   if (!e || (count && (!d_vectors || !d_out)) || out_pitch < e->L) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(e->ctx));
   return gemm(e->ctx, d_vectors, e->k, count, e->k, e->pieces.p, e->pitch, d_out, out_pitch, e->L);
+}
+
+int rlnc_encoder_seed(rlnc_encoder* e, uint64_t seed) {
+  if (!e) return RLNC_ERR_INVALID_ARGUMENT;
+  e->seed = seed;
+  e->drawn = 0;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wire, size_t wire_pitch) {
+  if (!e || (count && !d_wire)) return RLNC_ERR_INVALID_ARGUMENT;
+  const size_t k = e->k, L = e->L;
+  if (wire_pitch < k + L || count > 65535) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!count) return RLNC_OK;
+  TRY(set_dev(e->ctx));
+  hipStream_t st = e->ctx->stream;
+  // systematic/encoder.go:83-96: the first k pieces are e_id ++ P_id
+  size_t n_sys = 0;
+  if (e->kind == RLNC_SYSTEMATIC && e->sys_next < k) n_sys = std::min(count, k - e->sys_next);
+  HIPC(kodr_amd::fill_vectors(d_wire, wire_pitch, count, k, e->seed, e->drawn, n_sys, e->sys_next, st));
+  // the vectors are read in place as the coefficient matrix (lda = wire_pitch)
+  if ((k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0) {
+    TRY(gemm(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pitch, d_wire + k, wire_pitch, L));
+  } else {  // piece columns not 16-byte aligned: compute aside, then one strided copy
+    TRY(e->out.reserve(count * e->pitch));
+    TRY(gemm(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pitch, e->out.p, e->pitch, L));
+    HIPC(hipMemcpy2DAsync(d_wire + k, wire_pitch, e->out.p, e->pitch, L, count, hipMemcpyDeviceToDevice, st));
+  }
+  e->sys_next += n_sys;
+  e->drawn += count;
+  return RLNC_OK;
 }
 
 /* ---- recoder ------------------------------------------------------------ */
@@ -616,6 +668,8 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   d->tmat.release();
   d->decoded.release();
   d->rowbuf.release();
+  d->scratch.release();
+  d->srcs.release();
   delete d;
   return RLNC_OK;
 }
@@ -676,12 +730,54 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   return dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev);
 }
 
-// decoded rows [0, rows) = T x R into dst (device, pitch dpitch)
+// decoded rows [0, rows) = T x R into dst (device, pitch dpitch).
+// A row of T that is a unit vector e_j selects received piece j unchanged: a
+// systematic piece (systematic/encoder.go:83-96), which kodr's elimination
+// never modifies since it has no entry off its pivot column.  Those rows are
+// copied, and only the other m rows go through the GF kernel: m x recv x L
+// MACs instead of rows x recv x L (systematic/decoder.go:96-104
+// leaves this undone).  The bytes are identical either way.
 int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, size_t dpitch) {
   const size_t recv = d->core.received();
-  TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
-  HIPC(d->ctx->stage.h2d(d->tmat.p, recv, trows, recv, recv, rows, d->ctx->stream));
-  return gemm(d->ctx, d->tmat.p, recv, rows, recv, d->recv.p, d->pitch, dst, dpitch, d->L);
+  hipStream_t st = d->ctx->stream;
+  d->hsrc.assign(rows, nullptr);
+  size_t m = 0;
+  for (size_t i = 0; i < rows; i++) {
+    const uint8_t* t = trows + i * recv;
+    size_t j = 0;
+    while (j < recv && !t[j]) j++;
+    bool unit = j < recv && t[j] == 1;
+    for (size_t q = j + 1; unit && q < recv; q++) unit = !t[q];
+    if (unit) d->hsrc[i] = d->recv.p + j * d->pitch;
+    else m++;
+  }
+  d->last_gf_rows = m;
+  d->last_copy_rows = rows - m;
+  if (m == rows || rows > 65535 || dpitch % 16) {  // no unit rows: straight into dst
+    d->last_gf_rows = rows;
+    d->last_copy_rows = 0;
+    TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
+    HIPC(d->ctx->stage.h2d(d->tmat.p, recv, trows, recv, recv, rows, st));
+    return gemm(d->ctx, d->tmat.p, recv, rows, recv, d->recv.p, d->pitch, dst, dpitch, d->L);
+  }
+  if (m) {
+    d->hTc.resize(m * recv);
+    TRY(d->scratch.reserve(m * d->pitch));
+    for (size_t i = 0, t = 0; i < rows; i++)
+      if (!d->hsrc[i]) {
+        memcpy(d->hTc.data() + t * recv, trows + i * recv, recv);
+        d->hsrc[i] = d->scratch.p + t * d->pitch;
+        t++;
+      }
+    TRY(d->tmat.reserve(m * recv));
+    HIPC(d->ctx->stage.h2d(d->tmat.p, recv, d->hTc.data(), recv, recv, m, st));
+    TRY(gemm(d->ctx, d->tmat.p, recv, m, recv, d->recv.p, d->pitch, d->scratch.p, d->pitch, d->L));
+  }
+  const size_t tb = rows * sizeof(uint8_t*);
+  TRY(d->srcs.reserve(tb));
+  HIPC(d->ctx->stage.h2d(d->srcs.p, tb, reinterpret_cast<const uint8_t*>(d->hsrc.data()), tb, tb, 1, st));
+  HIPC(kodr_amd::gather_rows(reinterpret_cast<const uint8_t* const*>(d->srcs.p), dst, dpitch, rows, d->L, st));
+  return RLNC_OK;
 }
 
 int dec_materialize(rlnc_decoder* d) {
@@ -797,6 +893,13 @@ int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_p
   d->hT.resize(std::max<size_t>(rows * recv, 1));
   d->core.copy_transform(d->hT.data(), recv);
   return dec_apply(d, rows, d->hT.data(), d_out, out_pitch);  // T is staged; no host buffer outlives the call
+}
+
+int rlnc_decoder_apply_stats(const rlnc_decoder* d, size_t* gf_rows, size_t* copy_rows) {
+  if (!d || !gf_rows || !copy_rows) return RLNC_ERR_INVALID_ARGUMENT;
+  *gf_rows = d->last_gf_rows;
+  *copy_rows = d->last_copy_rows;
+  return RLNC_OK;
 }
 
 int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {

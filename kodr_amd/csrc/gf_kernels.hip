@@ -294,6 +294,75 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
   return hipGetLastError();
 }
 
+// dst row r = bytes [0, ncols) of the device row src[r] (16-byte aligned rows).
+// Used where a row of the product is a plain copy: unit rows of the decode
+// transform (systematic pieces) and gathers of GEMM scratch rows.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* const* __restrict__ src,
+                                                         uint8_t* __restrict__ dst, size_t dpitch,
+                                                         int ncols) {
+  const int r = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
+  if (c >= ncols) return;
+  const uint8_t* s = src[r] + c;
+  uint8_t* d = dst + (size_t)r * dpitch + c;
+  if (c + kLaneBytes <= ncols) {
+    *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+  } else {
+    for (int i = 0; c + i < ncols; i++) d[i] = s[i];
+  }
+}
+
+}  // namespace
+
+hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
+                       hipStream_t stream) {
+  if (!rows || !ncols) return hipSuccess;
+  if (rows > 65535) return hipErrorInvalidValue;
+  const unsigned gx = (unsigned)((ncols + 256 * kLaneBytes - 1) / (256 * kLaneBytes));
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, d_src, dY, ldy,
+                     (int)ncols);
+  return hipGetLastError();
+}
+
+namespace {
+
+// Coding vectors drawn on the device: byte j of vector row r is
+// the low byte of splitmix64(seed + (row0 + r) * 2^32 + j); rows r < n_sys are
+// the unit vectors e_(sys_first + r) of a systematic encoder's first k pieces
+// (systematic/encoder.go:60-68).  Uniform bytes, zeros allowed, like
+// GenerateCodingVector (data.go:90-95); not a cryptographic generator.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_vectors_kernel(uint8_t* __restrict__ V, size_t ldv, int k,
+                                                          uint64_t seed, uint64_t row0, int n_sys,
+                                                          int sys_first) {
+  const int r = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= k) return;
+  uint8_t b;
+  if (r < n_sys) b = (j == sys_first + r) ? 1 : 0;
+  else b = (uint8_t)splitmix64(seed + ((row0 + (uint64_t)r) << 32) + (uint64_t)j);
+  V[(size_t)r * ldv + j] = b;
+}
+
+}  // namespace
+
+hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
+                        size_t n_sys, size_t sys_first, hipStream_t stream) {
+  if (!rows || !k) return hipSuccess;
+  if (rows > 65535 || k > (1u << 30)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fill_vectors_kernel, dim3((unsigned)((k + 255) / 256), (unsigned)rows), dim3(256), 0,
+                     stream, dV, ldv, (int)k, seed, row0, (int)n_sys, (int)sys_first);
+  return hipGetLastError();
+}
+
+namespace {
+
 }  // namespace
 
 // Tiles measured on MI355X at K = 256, ncols = 128 KiB (tools/tune_gemm.py).

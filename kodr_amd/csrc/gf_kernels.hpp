@@ -21,4 +21,14 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
                    const GemmConfig* force = nullptr);
 
+// dY row r = the first ncols bytes of device row d_src[r] (d_src: device array
+// of rows pointers, 16-byte aligned).  rows <= 65535.
+hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
+                       hipStream_t stream);
+
+// rows x k coding vectors at row pitch ldv: rows [0, n_sys) = e_(sys_first+r),
+// the rest counter-based pseudo-random bytes of (seed, row0 + r).  rows <= 65535.
+hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
+                        size_t n_sys, size_t sys_first, hipStream_t stream);
+
 }  // namespace kodr_amd

@@ -22,11 +22,21 @@ class Staging {
   hipError_t h2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                  size_t height, hipStream_t s) {
     if (!width || !height) return hipSuccess;
+    if (is_pinned(src)) {  // registered / pinned caller memory: DMA straight from it
+      hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice, s);
+      return e == hipSuccess ? hipStreamSynchronize(s) : e;  // the caller may reuse src on return
+    }
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
-    if (width > kChunk) {  // a single row larger than a chunk: direct copy
-      e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice, s);
-      return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    if (width > kChunk) {  // rows wider than a chunk: each row as chunk-wide segments
+      for (size_t r = 0; r < height; r++) {
+        const size_t full = width / kChunk, tail = width - full * kChunk;
+        if ((e = h2d(dst + r * dpitch, kChunk, src + r * spitch, kChunk, kChunk, full, s)) != hipSuccess) return e;
+        if ((e = h2d(dst + r * dpitch + full * kChunk, tail, src + r * spitch + full * kChunk, tail, tail, 1, s)) !=
+            hipSuccess)
+          return e;
+      }
+      return hipSuccess;
     }
     const size_t per = kChunk / width;
     for (size_t r0 = 0; r0 < height; r0 += per) {
@@ -46,11 +56,21 @@ class Staging {
   hipError_t d2h(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                  size_t height, hipStream_t s) {
     if (!width || !height) return hipSuccess;
+    if (is_pinned(dst)) {
+      hipError_t e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, s);
+      return e == hipSuccess ? hipStreamSynchronize(s) : e;
+    }
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
     if (width > kChunk) {
-      e = hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDeviceToHost, s);
-      return e == hipSuccess ? hipStreamSynchronize(s) : e;
+      for (size_t r = 0; r < height; r++) {
+        const size_t full = width / kChunk, tail = width - full * kChunk;
+        if ((e = d2h(dst + r * dpitch, kChunk, src + r * spitch, kChunk, kChunk, full, s)) != hipSuccess) return e;
+        if ((e = d2h(dst + r * dpitch + full * kChunk, tail, src + r * spitch + full * kChunk, tail, tail, 1, s)) !=
+            hipSuccess)
+          return e;
+      }
+      return hipSuccess;
     }
     const size_t per = kChunk / width;
     size_t prev_r0 = 0, prev_n = 0;
@@ -91,6 +111,19 @@ class Staging {
   }
 
  private:
+  // page-locked host memory (hipHostMalloc or hipHostRegister, e.g. through
+  // rlnc_host_register) needs no bounce buffer.  An unknown pointer makes
+  // hipPointerGetAttributes fail; clear that error so it is not reported by
+  // the next launch's hipGetLastError.
+  static bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return a.type == hipMemoryTypeHost;
+  }
+
   hipError_t ensure() {
     if (buf_[0]) return hipSuccess;
     for (int b = 0; b < 2; b++) {

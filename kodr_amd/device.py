@@ -53,6 +53,13 @@ class Context:
         errors.check(lib().rlnc_memcpy_h2d(self._h, ctypes.c_void_p(dptr),
                                            a.ctypes.data_as(ctypes.c_void_p), a.nbytes))
 
+    def register(self, host):
+        """Page-lock a numpy array so the engine DMAs straight from/into it."""
+        errors.check(lib().rlnc_host_register(self._h, ctypes.c_void_p(host.ctypes.data), host.nbytes))
+
+    def unregister(self, host):
+        errors.check(lib().rlnc_host_unregister(self._h, ctypes.c_void_p(host.ctypes.data)))
+
     def d2h(self, dptr, nbytes):
         import numpy as np
         out = np.empty(nbytes, dtype=np.uint8)

@@ -201,7 +201,7 @@ def test_c4_systematic_round_trip_with_drops(gpu_ctx):
     P = rng.integers(0, 256, (k, L), dtype=np.uint8)
     e = Enc(gpu_ctx, P, SYSTEMATIC)
     d = Dec(gpu_ctx, k)
-    sent = 0
+    sent = n_sys = 0
     while not d.state()[3]:
         V, out = e.code(rng.integers(0, 256, (16, k), dtype=np.uint8))
         for i in range(16):
@@ -212,8 +212,16 @@ def test_c4_systematic_round_trip_with_drops(gpu_ctx):
             st = d.add(out[i, :k], out[i, k:])
             if st == ERR["ErrAllUsefulPiecesReceived"]:
                 break
+            n_sys += sent <= k
     st, dec = d.get_all()
     assert st == 0 and np.array_equal(dec, P)
+    # systematic fast path: with exactly k pieces received T = C^-1 is unique,
+    # so every received systematic piece is a unit row and is copied
+    gf_rows, copy_rows = ctypes.c_size_t(), ctypes.c_size_t()
+    errors.check(_lib.lib().rlnc_decoder_apply_stats(d.h, ctypes.byref(gf_rows), ctypes.byref(copy_rows)))
+    assert gf_rows.value + copy_rows.value == k
+    if d.state()[1] == k:
+        assert copy_rows.value == n_sys and 0 < n_sys < k
 
 
 def test_c2_recode_matches_oracle_and_decodes(gpu_ctx):
@@ -366,3 +374,111 @@ def test_rows_wider_than_staging_chunk(gpu_ctx):
     assert st in (0, 3) and n >= k
     st, allp = d.get_all()
     assert st == 0 and np.array_equal(allp, P)
+
+
+@pytest.mark.parametrize("k,L,drop", [(8, 77, 0.0), (16, 1000, 0.3), (32, 4099, 0.6), (24, 333, 1.0)])
+def test_systematic_fast_path_vs_oracle(gpu_ctx, k, L, drop):
+    """Systematic pieces (some dropped) + coded repairs, fed through the
+    decoder: per-step state, partial GetPiece and the decoded bytes match the
+    oracle; the copy/GF split of the materialization is reported."""
+    rng = np.random.default_rng(k + L)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P, SYSTEMATIC)
+    d, ref = Dec(gpu_ctx, k), oracle.Decoder(k)
+    V, out = e.code(rng.integers(0, 256, (3 * k, k), dtype=np.uint8))
+    keep = [i for i in range(3 * k) if i >= k or rng.random() >= drop]
+    n_sys = 0
+    for i in keep:
+        v, p = out[i, :k], out[i, k:]
+        assert d.add(v, p) == ref.add(v, p)
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+        n_sys += i < k
+        if ref.is_decoded():
+            break
+        idx = int(rng.integers(0, k))
+        st_r, got_r = ref.get_piece(idx)
+        st, got = d.get(idx)
+        assert st == st_r and (st != 0 or np.array_equal(got, got_r))
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+    gf_rows, copy_rows = ctypes.c_size_t(), ctypes.c_size_t()
+    errors.check(_lib.lib().rlnc_decoder_apply_stats(d.h, ctypes.byref(gf_rows), ctypes.byref(copy_rows)))
+    assert gf_rows.value + copy_rows.value == k
+    if d.state()[1] == k:
+        assert copy_rows.value == n_sys
+
+
+def _wire_device(ctx, e, count, pitch):
+    d = ctx.alloc(count * pitch)
+    try:
+        errors.check(_lib.lib().rlnc_encoder_coded_wire_device(e.h, count, ctypes.c_void_p(d), pitch))
+        return ctx.d2h(d, count * pitch).reshape(count, pitch)
+    finally:
+        ctx.synchronize()
+        ctx.free(d)
+
+
+@pytest.mark.parametrize("kind", [FULL, SYSTEMATIC])
+@pytest.mark.parametrize("k,L,pad", [(16, 1000, 24), (7, 45, 0), (32, 4096, 256)])
+def test_coded_wire_device_rng(gpu_ctx, kind, k, L, pad):
+    """Device-drawn vectors travel with their pieces: every wire row is
+    (v, v x P) bit-exact vs the oracle; systematic encoders emit e_i ++ P_i
+    first; reseeding reproduces the stream; the rows decode to P."""
+    rng = np.random.default_rng(k * L)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    pitch = k + L + pad
+    e = Enc(gpu_ctx, P, kind)
+    errors.check(_lib.lib().rlnc_encoder_seed(e.h, 1234))
+    n1, n2 = k // 2 + 1, k + 5
+    W = np.concatenate([_wire_device(gpu_ctx, e, n1, pitch), _wire_device(gpu_ctx, e, n2, pitch)])[:, :k + L]
+    V, C = W[:, :k], W[:, k:]
+    n_sys = k if kind == SYSTEMATIC else 0
+    if n_sys:
+        assert np.array_equal(V[:n_sys], np.eye(k, dtype=np.uint8))
+        assert np.array_equal(C[:n_sys], P)
+    assert np.array_equal(C, oracle.encode(P, V))
+    coded = V[n_sys:]
+    assert len({r.tobytes() for r in coded}) == coded.shape[0]          # fresh vectors per piece
+    assert 100 < coded.mean() < 155                                      # uniform bytes
+    e2 = Enc(gpu_ctx, P, kind)
+    errors.check(_lib.lib().rlnc_encoder_seed(e2.h, 1234))
+    W2 = _wire_device(gpu_ctx, e2, n1 + n2, pitch)[:, :k + L]
+    assert np.array_equal(W2, W)                                         # reproducible stream
+    d = Dec(gpu_ctx, k)
+    st, n = _add_rows(d, ptr(np.ascontiguousarray(W)), W.shape[0], k + L, False)
+    assert st in (0, 3)
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+
+
+def _page_aligned(shape):
+    n = int(np.prod(shape))
+    npg = (n + 4095) // 4096 * 4096
+    buf = np.zeros(npg + 4096, np.uint8)
+    off = (-buf.ctypes.data) % 4096
+    return buf[off:off + npg][:n].reshape(shape)
+
+
+def test_registered_host_buffers(gpu_ctx):
+    """Page-locked caller buffers take the direct DMA path: same bytes."""
+    rng = np.random.default_rng(21)
+    k, L = 16, 70001
+    P, V = _page_aligned((k, L)), _page_aligned((k + 3, k))
+    P[:] = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V[:] = rng.integers(0, 256, (k + 3, k), dtype=np.uint8)
+    out = _page_aligned((k + 3, k + L))
+    dec = _page_aligned((k, L))
+    for a in (P, V, out, dec):
+        gpu_ctx.register(a)
+    try:
+        e = Enc(gpu_ctx, P)
+        errors.check(_lib.lib().rlnc_encoder_coded_pieces(e.h, ptr(V), V.shape[0], ptr(out)))
+        assert np.array_equal(out[:, k:], oracle.encode(P, V))
+        d = Dec(gpu_ctx, k)
+        st, n = _add_rows(d, ptr(out), out.shape[0], k + L, False)
+        assert st in (0, 3)
+        assert _lib.lib().rlnc_decoder_get_pieces(d.h, ptr(dec)) == 0
+        assert np.array_equal(dec, P)
+    finally:
+        for a in (P, V, out, dec):
+            gpu_ctx.unregister(a)
