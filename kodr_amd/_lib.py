@@ -85,6 +85,9 @@ SIGNATURES = {
     "rlnc_decoder_apply_stats": (_int, [_vp, _szp, _szp]),
     "rlnc_decoder_transform": (_int, [_vp, _u8p]),
     "rlnc_gf_matmul_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
+    "rlnc_bitslice_device": (_int, [_vp, _vp, _sz, _sz, _sz]),
+    "rlnc_bs_body_offsets": (_int, [_vp, _vp]),
+    "rlnc_gf_matmul_bs_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
 }
 
 _lib = None

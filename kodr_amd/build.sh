@@ -7,11 +7,14 @@ HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 ARCH="${KODR_ARCH:-gfx950}"
 mkdir -p build
 FLAGS=(-O3 -std=c++17 -fPIC -Wall -Wno-unused-function ${KODR_EXTRA_FLAGS:-})
+# the 256 coefficient bodies of the bit-sliced kernel (registers: acc v24, in v88, ret s54)
+python3 csrc/gen_bs_bodies.py 24 88 54 > csrc/gf_bs_bodies.inc
 pids=()
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_kernels.hip -o build/gf_kernels.o & pids+=($!)
+"$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_bs.hip -o build/gf_bs.o & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c csrc/capi.cpp -o build/capi.o & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c csrc/decoder_core.cpp -o build/decoder_core.o & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o libkodr_rlnc.so build/gf_kernels.o build/capi.o build/decoder_core.o \
+"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o libkodr_rlnc.so build/gf_kernels.o build/gf_bs.o build/capi.o build/decoder_core.o \
   -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "built $HERE/libkodr_rlnc.so"

@@ -84,6 +84,7 @@ struct rlnc_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   kodr_amd::Staging stage;   // pinned chunks for host-pointer copies
+  DevBuf prog;               // body-offset program of gf_gemm_bs launches (stream-ordered)
 };
 
 struct rlnc_encoder {
@@ -164,6 +165,24 @@ int gemm(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const
     return RLNC_ERR_INVALID_ARGUMENT;
   }
   HIPC(kodr_amd::gf_gemm(dA, lda, M, K, dX, ldx, dY, ldy, ncols, ctx->stream));
+  return RLNC_OK;
+}
+
+// Y = A (x) X over a bit-sliced X (kodr_amd::bitslice_rows), plain Y
+int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
+            size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (K * ldx >= ((size_t)1 << 32) || (ldx % 32) || (ldy % 16) || ldx < ncols || ldy < ncols) {
+    g_last_error = "gf_gemm_bs: unsupported layout (pitch multiple of 32, K*pitch < 2^32)";
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  if (M == 0 || ncols == 0) return RLNC_OK;
+  const kodr_amd::BsPlan plan = kodr_amd::plan_gemm_bs(M, K, ncols);
+  if (plan.prog_bytes > ctx->prog.cap) {
+    HIPC(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old program
+    TRY(ctx->prog.reserve(plan.prog_bytes));
+  }
+  HIPC(kodr_amd::gf_gemm_bs(dA, lda, M, K, dX, ldx, dY, ldy, ncols, reinterpret_cast<uint32_t*>(ctx->prog.p),
+                            ctx->prog.cap, ctx->device, ctx->stream));
   return RLNC_OK;
 }
 
@@ -270,6 +289,7 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   ctx->stage.release();
+  ctx->prog.release();
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
@@ -915,6 +935,27 @@ int rlnc_decoder_transform(const rlnc_decoder* d, uint8_t* out) {
 }
 
 /* ---- raw kernel ----------------------------------------------------------- */
+int rlnc_bitslice_device(rlnc_ctx* ctx, uint8_t* dX, size_t ldx, size_t rows, size_t ncols) {
+  if (!ctx || (rows && ncols && !dX)) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(kodr_amd::bitslice_rows(dX, ldx, rows, ncols, ctx->stream));
+  return RLNC_OK;
+}
+
+int rlnc_bs_body_offsets(rlnc_ctx* ctx, uint32_t* out) {
+  if (!ctx || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(kodr_amd::bs_body_offsets(ctx->device, out));
+  return RLNC_OK;
+}
+
+int rlnc_gf_matmul_bs_device(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K,
+                             const uint8_t* dXbs, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (!ctx || (M && (!dA || !dXbs || !dY)) || lda < K) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  return gemm_bs(ctx, dA, lda, M, K, dXbs, ldx, dY, ldy, ncols);
+}
+
 int rlnc_gf_matmul_device(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K,
                           const uint8_t* dX, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
   if (!ctx || (M && (!dA || !dX || !dY)) || lda < K) return RLNC_ERR_INVALID_ARGUMENT;

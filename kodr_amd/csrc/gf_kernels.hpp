@@ -31,4 +31,24 @@ hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, siz
 hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
                         size_t n_sys, size_t sys_first, hipStream_t stream);
 
+// ---- bit-sliced path (gf_bs.hip) ----
+// In place: every 32-byte block of rows [0, rows) x [0, round_up(ncols, 32))
+// becomes 8 bit planes (self-inverse).  ldx multiple of 32.
+hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hipStream_t stream);
+
+// byte offsets of the 256 coefficient bodies from body 0 (diagnostics)
+hipError_t bs_body_offsets(int device, uint32_t* host_out);
+
+struct BsPlan {
+  int ncx = 0, nrg = 0, kw = 1, rpw = 8, blocks = 0;
+  size_t prog_bytes = 0;  // scratch the launch needs for its body-offset program
+};
+BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols);
+
+// Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.  d_prog:
+// per-stream scratch of at least plan_gemm_bs(M, K, ncols).prog_bytes.
+hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
+                      uint8_t* dY, size_t ldy, size_t ncols, uint32_t* d_prog, size_t prog_bytes,
+                      int device, hipStream_t stream);
+
 }  // namespace kodr_amd
