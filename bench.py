@@ -184,7 +184,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, k, L),
-                         "kernel": "gf_gemm_kernel",
+                         "kernel": "gf_bs_kernel" if B >= 16 else "gf_gemm_kernel",
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "compulsory_hbm_bytes_per_launch": compulsory,
                          "compulsory_hbm_GBps": round(compulsory / t_launch / 1e9, 1),
@@ -349,7 +349,8 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
 
 
 VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9      # integer VALU lane-ops/s (MI355X_MICROARCH.md)
-LANE_OPS_PER_MAC = 4.5 / 4                 # 3 v_perm + 1.5 v_bitop3 per coefficient x 4 bytes
+LANE_OPS_PER_MAC_PERM = 4.5 / 4            # gf_gemm_kernel: 3 v_perm + 1.5 v_bitop3 per coefficient x 4 bytes
+LANE_OPS_PER_MAC_BS = 18.0 / 32            # gf_bs_kernel: 18 XOR3 (average body) per coefficient x 32 bytes
 
 
 def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
@@ -380,7 +381,9 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
     macs = best["gf_rows"] * best["received"] * L
     best["apply_gf_macs"] = macs
     best["apply_gf_macs_per_s"] = float(f"{macs / best['get_s']:.4g}")
-    best["valu_ceiling_macs_per_s"] = float(f"{VALU_LANE_OPS / LANE_OPS_PER_MAC:.4g}")
+    per = LANE_OPS_PER_MAC_BS if best["gf_rows"] >= 16 else LANE_OPS_PER_MAC_PERM
+    best["apply_kernel"] = "gf_bs_kernel" if best["gf_rows"] >= 16 else "gf_gemm_kernel"
+    best["valu_ceiling_macs_per_s"] = float(f"{VALU_LANE_OPS / per:.4g}")
     return best
 
 

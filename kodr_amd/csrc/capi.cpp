@@ -94,6 +94,8 @@ struct rlnc_encoder {
   size_t sys_next = 0;       // systematic/encoder.go:8 currentPieceId
   uint64_t seed = 0, drawn = 0;  // device vector RNG: seed, rows drawn so far
   DevBuf pieces;             // k x pitch, zero padded
+  DevBuf pieces_bs;          // bit-sliced twin of pieces, built on first large batch
+  bool bs_valid = false;
   DevBuf vecs, out;          // staging for host-pointer calls
 };
 
@@ -101,6 +103,8 @@ struct rlnc_recoder {
   rlnc_ctx* ctx = nullptr;
   size_t n = 0, k = 0, clen = 0, pitch = 0;
   DevBuf flat;               // n x pitch wire rows
+  DevBuf flat_bs;            // bit-sliced twin, built on first large batch
+  bool bs_valid = false;
   DevBuf r, out;
 };
 
@@ -111,6 +115,8 @@ struct rlnc_decoder {
   bool have_len = false;
   DevBuf recv;               // received pieces, row i = piece i, pitch
   size_t recv_rows = 0;
+  DevBuf recv_bs;            // bit-sliced twin of recv rows [0, bs_rows)
+  size_t bs_rows = 0;
   DevBuf tmat;               // transform upload
   DevBuf decoded;            // useful x pitch, valid when decoded_ready
   DevBuf rowbuf;             // one row for partial GetPiece
@@ -184,6 +190,25 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
   HIPC(kodr_amd::gf_gemm_bs(dA, lda, M, K, dX, ldx, dY, ldy, ncols, reinterpret_cast<uint32_t*>(ctx->prog.p),
                             ctx->prog.cap, ctx->device, ctx->stream));
   return RLNC_OK;
+}
+
+// Below this many output rows the perm-table kernel (gf_gemm) wins: the
+// bit-sliced launch has a higher fixed cost (profiles/r01/bs_bringup.log).
+constexpr size_t kBsMinRows = 16;
+
+// Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
+// plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
+int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
+                  DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32))
+    return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
+  if (!twin_valid) {
+    TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
+    HIPC(hipMemcpyAsync(twin.p, plain, K * ldx, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(kodr_amd::bitslice_rows(twin.p, ldx, K, ncols, ctx->stream));
+    twin_valid = true;
+  }
+  return gemm_bs(ctx, dA, lda, M, K, twin.p, ldx, dY, ldy, ncols);
 }
 
 int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** out) {
@@ -472,6 +497,7 @@ int rlnc_encoder_destroy(rlnc_encoder* e) {
   (void)hipSetDevice(e->ctx->device);
   (void)hipStreamSynchronize(e->ctx->stream);
   e->pieces.release();
+  e->pieces_bs.release();
   e->vecs.release();
   e->out.release();
   delete e;
@@ -519,7 +545,8 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, u
     TRY(e->vecs.reserve(B * k));
     TRY(e->out.reserve(B * e->pitch));
     HIPC(e->ctx->stage.h2d(e->vecs.p, k, vectors + i * k, k, k, B, st));
-    TRY(gemm(e->ctx, e->vecs.p, k, B, k, e->pieces.p, e->pitch, e->out.p, e->pitch, L));
+    TRY(gemm_resident(e->ctx, e->vecs.p, k, B, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch, e->out.p,
+                      e->pitch, L));
     for (size_t b = 0; b < B; b++) memcpy(out + (i + b) * clen, vectors + (i + b) * k, k);
     HIPC(e->ctx->stage.d2h(out + i * clen + k, clen, e->out.p, e->pitch, L, B, st));
     i += B;
@@ -532,7 +559,8 @@ int rlnc_encoder_coded_pieces_device(rlnc_encoder* e, const uint8_t* d_vectors, 
                                      uint8_t* d_out, size_t out_pitch) {
   if (!e || (count && (!d_vectors || !d_out)) || out_pitch < e->L) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(e->ctx));
-  return gemm(e->ctx, d_vectors, e->k, count, e->k, e->pieces.p, e->pitch, d_out, out_pitch, e->L);
+  return gemm_resident(e->ctx, d_vectors, e->k, count, e->k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch,
+                       d_out, out_pitch, e->L);
 }
 
 int rlnc_encoder_seed(rlnc_encoder* e, uint64_t seed) {
@@ -555,10 +583,12 @@ int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wir
   HIPC(kodr_amd::fill_vectors(d_wire, wire_pitch, count, k, e->seed, e->drawn, n_sys, e->sys_next, st));
   // the vectors are read in place as the coefficient matrix (lda = wire_pitch)
   if ((k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0) {
-    TRY(gemm(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pitch, d_wire + k, wire_pitch, L));
+    TRY(gemm_resident(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch,
+                      d_wire + k, wire_pitch, L));
   } else {  // piece columns not 16-byte aligned: compute aside, then one strided copy
     TRY(e->out.reserve(count * e->pitch));
-    TRY(gemm(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pitch, e->out.p, e->pitch, L));
+    TRY(gemm_resident(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch,
+                      e->out.p, e->pitch, L));
     HIPC(hipMemcpy2DAsync(d_wire + k, wire_pitch, e->out.p, e->pitch, L, count, hipMemcpyDeviceToDevice, st));
   }
   e->sys_next += n_sys;
@@ -633,6 +663,7 @@ int rlnc_recoder_destroy(rlnc_recoder* r) {
   (void)hipSetDevice(r->ctx->device);
   (void)hipStreamSynchronize(r->ctx->stream);
   r->flat.release();
+  r->flat_bs.release();
   r->r.release();
   r->out.release();
   delete r;
@@ -653,7 +684,8 @@ int rlnc_recoder_coded_pieces(rlnc_recoder* r, const uint8_t* rv, size_t count, 
     TRY(r->out.reserve(B * r->pitch));
     HIPC(r->ctx->stage.h2d(r->r.p, r->n, rv + i * r->n, r->n, r->n, B, st));
     // wire rows in, wire rows out: [r x C | sum r_i P_i] (full/recoder.go:32-40)
-    TRY(gemm(r->ctx, r->r.p, r->n, B, r->n, r->flat.p, r->pitch, r->out.p, r->pitch, r->clen));
+    TRY(gemm_resident(r->ctx, r->r.p, r->n, B, r->n, r->flat.p, r->flat_bs, r->bs_valid, r->pitch, r->out.p,
+                      r->pitch, r->clen));
     HIPC(r->ctx->stage.d2h(out + i * r->clen, r->clen, r->out.p, r->pitch, r->clen, B, st));
     i += B;
   }
@@ -664,7 +696,8 @@ int rlnc_recoder_coded_pieces_device(rlnc_recoder* r, const uint8_t* d_r, size_t
                                      uint8_t* d_out, size_t out_pitch) {
   if (!r || (count && (!d_r || !d_out)) || out_pitch < r->clen) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(r->ctx));
-  return gemm(r->ctx, d_r, r->n, count, r->n, r->flat.p, r->pitch, d_out, out_pitch, r->clen);
+  return gemm_resident(r->ctx, d_r, r->n, count, r->n, r->flat.p, r->flat_bs, r->bs_valid, r->pitch, d_out,
+                       out_pitch, r->clen);
 }
 
 /* ---- decoder ------------------------------------------------------------ */
@@ -690,6 +723,7 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   d->rowbuf.release();
   d->scratch.release();
   d->srcs.release();
+  d->recv_bs.release();
   delete d;
   return RLNC_OK;
 }
@@ -750,6 +784,28 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   return dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev);
 }
 
+// X = the received rows for a T x R product of M output rows: the plain rows
+// for small M, else the bit-sliced twin with rows [bs_rows, received) added.
+int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t ldy) {
+  const size_t recv = d->core.received();
+  rlnc_ctx* ctx = d->ctx;
+  if (M < kBsMinRows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32))
+    return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
+  if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
+    HIPC(hipStreamSynchronize(ctx->stream));
+    TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
+    d->bs_rows = 0;
+  }
+  if (d->bs_rows < recv) {
+    const size_t n = recv - d->bs_rows;
+    HIPC(hipMemcpyAsync(d->recv_bs.p + d->bs_rows * d->pitch, d->recv.p + d->bs_rows * d->pitch, n * d->pitch,
+                        hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(kodr_amd::bitslice_rows(d->recv_bs.p + d->bs_rows * d->pitch, d->pitch, n, d->L, ctx->stream));
+    d->bs_rows = recv;
+  }
+  return gemm_bs(ctx, dA, recv, M, recv, d->recv_bs.p, d->pitch, dY, ldy, d->L);
+}
+
 // decoded rows [0, rows) = T x R into dst (device, pitch dpitch).
 // A row of T that is a unit vector e_j selects received piece j unchanged: a
 // systematic piece (systematic/encoder.go:83-96), which kodr's elimination
@@ -778,7 +834,7 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
     d->last_copy_rows = 0;
     TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
     HIPC(d->ctx->stage.h2d(d->tmat.p, recv, trows, recv, recv, rows, st));
-    return gemm(d->ctx, d->tmat.p, recv, rows, recv, d->recv.p, d->pitch, dst, dpitch, d->L);
+    return dec_gemm(d, d->tmat.p, rows, dst, dpitch);
   }
   if (m) {
     d->hTc.resize(m * recv);
@@ -791,7 +847,7 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
       }
     TRY(d->tmat.reserve(m * recv));
     HIPC(d->ctx->stage.h2d(d->tmat.p, recv, d->hTc.data(), recv, recv, m, st));
-    TRY(gemm(d->ctx, d->tmat.p, recv, m, recv, d->recv.p, d->pitch, d->scratch.p, d->pitch, d->L));
+    TRY(dec_gemm(d, d->tmat.p, m, d->scratch.p, d->pitch));
   }
   const size_t tb = rows * sizeof(uint8_t*);
   TRY(d->srcs.reserve(tb));

@@ -482,3 +482,71 @@ def test_registered_host_buffers(gpu_ctx):
     finally:
         for a in (P, V, out, dec):
             gpu_ctx.unregister(a)
+
+
+def bitslice_np(x):
+    """numpy model of the bit-sliced layout (32-byte blocks -> 8 planes)."""
+    d = x.reshape(-1, 8, 4).copy().view(np.uint32).reshape(-1, 8)
+    for sh, m, di in ((4, 0x0F0F0F0F, 4), (2, 0x33333333, 2), (1, 0x55555555, 1)):
+        for q in range(8):
+            if q & di:
+                continue
+            t = ((d[:, q] >> sh) ^ d[:, q + di]) & m
+            d[:, q + di] ^= t
+            d[:, q] ^= (t << sh).astype(np.uint32)
+    return d.view(np.uint8).reshape(x.shape)
+
+
+def test_bitslice_layout(gpu_ctx):
+    rng = np.random.default_rng(31)
+    X = rng.integers(0, 256, (7, 640), dtype=np.uint8)
+    # plane i of a block holds bit i of its 32 bytes
+    blk = np.zeros(32, np.uint8)
+    blk[5] = 0x81
+    planes = bitslice_np(blk).view(np.uint32)
+    assert planes[0] == planes[7] and planes[0] != 0 and not planes[1:7].any()
+    dX = gpu_ctx.alloc(X.nbytes)
+    try:
+        gpu_ctx.h2d(dX, X)
+        errors.check(_lib.lib().rlnc_bitslice_device(gpu_ctx.handle, ctypes.c_void_p(dX), 640, 7, 600))
+        gpu_ctx.synchronize()
+        got = gpu_ctx.d2h(dX, X.nbytes).reshape(7, 640)
+        assert np.array_equal(got, bitslice_np(X.reshape(7, 20, 32)).reshape(7, 640))
+        errors.check(_lib.lib().rlnc_bitslice_device(gpu_ctx.handle, ctypes.c_void_p(dX), 640, 7, 600))
+        gpu_ctx.synchronize()
+        assert np.array_equal(gpu_ctx.d2h(dX, X.nbytes).reshape(7, 640), X)   # self-inverse
+    finally:
+        gpu_ctx.free(dX)
+
+
+@pytest.mark.parametrize("M,K,n", [(1, 1, 32), (8, 8, 2048), (3, 5, 77), (16, 40, 5000), (17, 300, 4096),
+                                   (32, 256, 8192), (40, 7, 3000), (64, 256, 6149), (256, 258, 4096)])
+def test_gf_matmul_bs_vs_oracle(gpu_ctx, M, K, n):
+    """Bit-sliced kernel: bit-exact vs the oracle, with zero coefficients,
+    lda > K, ragged columns and a canary row beyond the output."""
+    rng = np.random.default_rng(M * 1000 + K + n)
+    lda = K + 3
+    A = np.zeros((M, lda), np.uint8)
+    A[:, :K] = rng.integers(0, 256, (M, K), dtype=np.uint8)
+    A[:, :K][rng.random((M, K)) < 0.15] = 0
+    X = rng.integers(0, 256, (K, n), dtype=np.uint8)
+    ldx = (n + 31) // 32 * 32 + 32
+    Xp = np.zeros((K, ldx), np.uint8)
+    Xp[:, :n] = X
+    ldy = (n + 15) // 16 * 16 + 16
+    dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(Xp.nbytes), gpu_ctx.alloc((M + 1) * ldy)
+    try:
+        gpu_ctx.h2d(dA, A)
+        gpu_ctx.h2d(dX, Xp)
+        gpu_ctx.h2d(dY, np.full((M + 1) * ldy, 0xA5, np.uint8))
+        L = _lib.lib()
+        errors.check(L.rlnc_bitslice_device(gpu_ctx.handle, ctypes.c_void_p(dX), ldx, K, n))
+        errors.check(L.rlnc_gf_matmul_bs_device(gpu_ctx.handle, ctypes.c_void_p(dA), lda, M, K, ctypes.c_void_p(dX),
+                                                ldx, ctypes.c_void_p(dY), ldy, n))
+        gpu_ctx.synchronize()
+        Y = gpu_ctx.d2h(dY, (M + 1) * ldy).reshape(M + 1, ldy)
+        assert np.array_equal(Y[:M, :n], oracle.encode(X, A[:, :K]))
+        assert (Y[:M, n:] == 0xA5).all() and (Y[M] == 0xA5).all()
+    finally:
+        for p in (dA, dX, dY):
+            gpu_ctx.free(p)

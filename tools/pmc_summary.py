@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise tools/profile_bench.sh output: average gf_gemm duration from the
+"""Summarise tools/profile_bench.sh output: average duration of the dominant
+kernel (gf_bs_kernel for B >= 16, else gf_gemm_kernel; argv[3] overrides) from the
 kernel trace and HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (KB units;
 FETCH_SIZE x2 on gfx950 for wide streaming reads, MI355X_MICROARCH.md §HBM)."""
 import csv
@@ -10,6 +11,7 @@ import statistics
 import sys
 
 out, B = sys.argv[1], int(sys.argv[2])
+KERNEL = sys.argv[3] if len(sys.argv) > 3 else ("gf_bs_kernel" if B >= 16 else "gf_gemm_kernel")
 
 
 def rows(pattern):
@@ -18,13 +20,14 @@ def rows(pattern):
 
 
 dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows("trace/**/*kernel_trace.csv")
-       if "gf_gemm" in r["Kernel_Name"]]
+       if KERNEL in r["Kernel_Name"]]
 fetch = [float(r["Counter_Value"]) for r in rows("fetch/**/*counter_collection.csv")
-         if "gf_gemm" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
 write = [float(r["Counter_Value"]) for r in rows("write/**/*counter_collection.csv")
-         if "gf_gemm" in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"]
+         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"]
 res = {
     "batch": B,
+    "kernel": KERNEL,
     "kernel_launches_traced": len(dur),
     "avg_kernel_us": round(statistics.mean(dur) / 1e3, 3) if dur else None,
     "median_kernel_us": round(statistics.median(dur) / 1e3, 3) if dur else None,
