@@ -7,8 +7,8 @@ HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 ARCH="${KODR_ARCH:-gfx950}"
 mkdir -p build
 FLAGS=(-O3 -std=c++17 -fPIC -Wall -Wno-unused-function ${KODR_EXTRA_FLAGS:-})
-# the 256 coefficient bodies of the bit-sliced kernel (registers: acc v24, in v88, ret s54)
-python3 csrc/gen_bs_bodies.py 24 88 54 > csrc/gf_bs_bodies.inc
+# the 256 coefficient bodies and row loop of the bit-sliced kernel
+python3 csrc/gen_bs_bodies.py > csrc/gf_bs_bodies.inc
 pids=()
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_kernels.hip -o build/gf_kernels.o & pids+=($!)
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_bs.hip -o build/gf_bs.o & pids+=($!)

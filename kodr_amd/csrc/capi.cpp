@@ -84,7 +84,6 @@ struct rlnc_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   kodr_amd::Staging stage;   // pinned chunks for host-pointer copies
-  DevBuf prog;               // body-offset program of gf_gemm_bs launches (stream-ordered)
 };
 
 struct rlnc_encoder {
@@ -182,13 +181,11 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
     return RLNC_ERR_INVALID_ARGUMENT;
   }
   if (M == 0 || ncols == 0) return RLNC_OK;
-  const kodr_amd::BsPlan plan = kodr_amd::plan_gemm_bs(M, K, ncols);
-  if (plan.prog_bytes > ctx->prog.cap) {
-    HIPC(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old program
-    TRY(ctx->prog.reserve(plan.prog_bytes));
+  if (!kodr_amd::plan_gemm_bs(M, K, ncols).ok) {
+    g_last_error = "gf_gemm_bs: K too large for the LDS program";
+    return RLNC_ERR_INVALID_ARGUMENT;
   }
-  HIPC(kodr_amd::gf_gemm_bs(dA, lda, M, K, dX, ldx, dY, ldy, ncols, reinterpret_cast<uint32_t*>(ctx->prog.p),
-                            ctx->prog.cap, ctx->device, ctx->stream));
+  HIPC(kodr_amd::gf_gemm_bs(dA, lda, M, K, dX, ldx, dY, ldy, ncols, ctx->device, ctx->stream));
   return RLNC_OK;
 }
 
@@ -200,7 +197,7 @@ constexpr size_t kBsMinRows = 16;
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32))
+  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32) || !kodr_amd::plan_gemm_bs(M, K, ncols).ok)
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {
     TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
@@ -314,7 +311,6 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   ctx->stage.release();
-  ctx->prog.release();
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
@@ -789,7 +785,8 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
 int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t ldy) {
   const size_t recv = d->core.received();
   rlnc_ctx* ctx = d->ctx;
-  if (M < kBsMinRows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32))
+  if (M < kBsMinRows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
+      !kodr_amd::plan_gemm_bs(M, recv, d->L).ok)
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
     HIPC(hipStreamSynchronize(ctx->stream));

@@ -5,9 +5,11 @@
 // dwords into 8 planes, plane i = bit i of all 32 bytes (it is an involution,
 // so the same transform converts back).  In that layout multiplying by a
 // coefficient c is GF(2)-linear on the planes: out plane j = XOR of the input
-// planes i with bit j of c*2^i set (gf256.go:15-44, poly 0x11D).  That is about
-// 18 XOR3 instructions per coefficient per 32 bytes, against 36 for the
-// 3x v_perm lookup formulation of gf_gemm_kernel.
+// planes i with bit j of c*2^i set (gf256.go:15-44, poly 0x11D).  Per input
+// row the wave tabulates the XORs of every subset of planes 0-3 and of planes
+// 4-7 (30 registers, 30 VALU shared by 8 output rows); then each output plane
+// is one XOR3, at most 8 instructions per coefficient per 32 bytes, against 36
+// for the 3x v_perm lookup formulation of gf_gemm_kernel.
 //
 // Code.  The XOR pattern depends on c, which is wave-uniform, so each of the
 // 256 patterns is a straight-line body (generated: gen_bs_bodies.py) and the
@@ -16,18 +18,22 @@
 // rows of a wave (index 8m).  No LDS tables, no lookups, no per-lane branches.
 //
 // Work split.  A wave owns 8 output rows x 64 blocks (2 KiB of columns) x a
-// range of rpw input rows; the KW waves of a workgroup split K and are XOR-
-// reduced in LDS.  Per wave, the body offsets for its (row, k) pairs are built
-// once into a private scratch slab ("program") and streamed into SGPRs with
-// s_load_dwordx8, one row ahead.  X rows stream through a 4-deep register ring
-// of buffer loads (rows >= K are outside num_records and read as zero).
+// range of at most rpw input rows; the KW waves of a workgroup split K and are
+// XOR-reduced in LDS.  Per wave, the body offsets for its (row, k) pairs are
+// built once into LDS ("program") and moved to SGPRs with v_readfirstlane, one
+// row ahead.  X rows stream through a 4-deep register ring of buffer loads
+// (rows >= K are outside num_records and read as zero); the first 4 are in
+// flight while the program is built.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
+#include <algorithm>
 #include <mutex>
 
 #include "gf_kernels.hpp"
-// accumulators v[24..87] (8 rows x 8 planes), inputs v[88..95], return s[54:55]
+// generated: bodies, row loop, register map (gen_bs_bodies.py)
 #include "gf_bs_bodies.inc"
 
 namespace kodr_amd {
@@ -75,20 +81,6 @@ __global__ __launch_bounds__(256) void bitslice_kernel(uint8_t* __restrict__ X, 
   p[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
-#define KODR_BS_CLOBBERS                                                                     \
-  "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", \
-  "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", \
-  "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", \
-  "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", \
-  "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", \
-  "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100",       \
-  "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111",    \
-  "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122",    \
-  "v123", "v124", "v125", "v126", "v127", "s40", "s41", "s42", "s43", "s44", "s45", "s46",   \
-  "s47", "s48", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", \
-  "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s74", \
-  "s75", "scc", "memory"
-
 // Writes the 256 body offsets (bytes from body 0) to offs; run once per device.
 __global__ __launch_bounds__(64) void gf_bs_export_kernel(uint32_t* offs) {
   asm volatile(
@@ -101,12 +93,62 @@ __global__ __launch_bounds__(64) void gf_bs_export_kernel(uint32_t* offs) {
       : "v24", "memory");
 }
 
-template <int KW>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// The main loop (gen_bs_bodies.py).  The ring operands pin the 4 prefetched
+// rows to v[RING..RING+31], where the generated row code expects them.
+#define KODR_BS_ASM(LOOP, TAIL)                                                          \
+  asm volatile(                                                                          \
+      "s_mov_b32 s40, %[xlo]\n\t"                                                        \
+      "s_and_b32 s41, %[xhi], 0xffff\n\t"                                                \
+      "s_mov_b32 s42, %[nrec]\n\t"                                                       \
+      "s_mov_b32 s43, 0x00020000\n\t"                                                    \
+      "s_mov_b32 s44, %[roff]\n\t"                                                       \
+      "s_mov_b32 s45, %[ldx]\n\t"                                                        \
+      "s_getpc_b64 s[74:75]\n\t"                                                         \
+      ".Lpc_%=:\n\t"                                                                     \
+      "s_add_u32 s50, s74, .Lbs_b0_%= - .Lpc_%=\n\t"                                     \
+      "s_addc_u32 s51, s75, 0\n\t"                                                       \
+      KODR_BS_PROLOGUE                                                                   \
+      "s_mov_b32 s72, %[ngrp]\n\t"                                                       \
+      "s_cmp_eq_u32 s72, 0\n\t"                                                          \
+      "s_cbranch_scc1 .Ltail_%=\n\t"                                                     \
+      ".Lloop_%=:\n\t"                                                                   \
+      LOOP                                                                               \
+      "s_sub_u32 s72, s72, 1\n\t"                                                        \
+      "s_cmp_lg_u32 s72, 0\n\t"                                                          \
+      "s_cbranch_scc1 .Lloop_%=\n\t"                                                     \
+      ".Ltail_%=:\n\t"                                                                   \
+      TAIL                                                                               \
+      KODR_BS_REDUCE /* this wave's 64 accumulator planes into the LDS sums */           \
+      "s_waitcnt lgkmcnt(0)\n\t"                                                         \
+      "s_branch .Lend_%=\n\t"                                                            \
+      KODR_BS_BODIES                                                                     \
+      ".Lend_%=:\n\t"                                                                    \
+      : "+{v[120:123]}"(r0), "+{v[124:127]}"(r1), "+{v[128:131]}"(r2), "+{v[132:135]}"(r3), \
+        "+{v[136:139]}"(r4), "+{v[140:143]}"(r5), "+{v[144:147]}"(r6), "+{v[148:151]}"(r7)  \
+      : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx), \
+        [ngrp] "s"(ngrp), [col] "v"(col), [lds] "v"((uint32_t)lane * 4u), [pl] "v"(pl)    \
+      : KODR_BS_CLOBBERS)
+
+static_assert(KODR_BS_RING == 120, "ring operands above assume the generator's register map");
+
+// MODE (tuning builds only, -DKODR_TUNE_MODES): 1 = every program entry is the
+// empty body (dispatch without XOR work), 2 = as 1 without reading A, 3 = no
+// dispatch at all (row stream + table prep + reduction only), 4 = as 3 without
+// the row stream, 5 = no main loop (prologue, reduction and store only).
+template <int KW, int MODE = 0>
 __global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
-    uint32_t* __restrict__ prog, const uint32_t* __restrict__ offs) {
-  extern __shared__ uint32_t red[];  // [8 rows x 8 planes][64 lanes]
+    const uint32_t* __restrict__ offs) {
+  // LDS: [0, 16 KiB) per-row XOR sums [8 rows x 8 planes][64 lanes];
+  // [16, 17 KiB) the body offset table; then each wave's program, rpw x 8
+  // 16-bit body offsets (the bodies span < 64 KiB)
+  extern __shared__ uint32_t lds[];
+  uint32_t* red = lds;
+  uint32_t* offs_l = lds + 64 * 64;
+  uint16_t* prog_l = reinterpret_cast<uint16_t*>(offs_l + 256);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware order: the nrg row groups of one column chunk go to blocks
   // b, b+8, ... (one XCD) and re-read that chunk from its L2.  Speed only.
@@ -115,66 +157,83 @@ __global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
   const int cx = (b / (8 * nrg)) * 8 + (b & 7);
   if (cx >= ncx) return;
   const int m0 = rg * kBsRows, kb = w * rpw;
+  // this wave's input rows: [kb, kb + nr), nr a multiple of 4 (rows >= K read zero)
+  const int kpad = (K + 3) & ~3;
+  const int nr = __builtin_amdgcn_readfirstlane(max(0, min(rpw, kpad - kb)));
 
-  // program: body offset for (row m0 + e%8, input row kb + e/8)
-  uint32_t* wp = prog + ((size_t)b * KW + w) * (size_t)rpw * kBsRows;
-  for (int e = lane; e < rpw * kBsRows; e += 64) {
+  // Prologue loads in retirement order (vmcnt counts in issue order): the
+  // offset table and this wave's first 512 coefficients, then the ring's first
+  // 4 rows, so the program build waits only for the former while the rows'
+  // HBM latency overlaps it (rows >= K are outside num_records: zeros).
+  const int ne = nr * kBsRows;
+  auto coef = [&](int e) -> uint32_t {
     const int k = kb + (e >> 3), row = m0 + (e & 7);
-    const uint32_t c = (k < K && row < M) ? A[(size_t)row * lda + k] : 0u;
-    wp[e] = offs[c];
+    return (MODE < 2 && e < ne && k < K && row < M) ? (uint32_t)A[(size_t)row * lda + k] : 0u;
+  };
+  uint32_t ot[(256 + 63) / 64];
+#pragma unroll
+  for (int j = 0; j < (256 + 63) / 64; j++) {
+    const int i = tid + j * 64 * KW;
+    ot[j] = i < 256 ? offs[i] : 0u;
+  }
+  uint32_t c[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
+
+  const uint32_t col = (uint32_t)(cx * 64 + lane) * kBsBlock;
+  const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)K * (uint32_t)ldx);
+  const uint32_t sldx = __builtin_amdgcn_readfirstlane((uint32_t)ldx);
+  const uint32_t kboff = __builtin_amdgcn_readfirstlane((uint32_t)kb * (uint32_t)ldx);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)nrec, 0x00020000);
+  // (unconditional: a wave past K reads zeros, and a branch here would make
+  // the compiler's waitcnt pass drain these loads at the next LDS write)
+  u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff, 0);
+  u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff, 0);
+  u32x4 r2 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + sldx, 0);
+  u32x4 r3 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + sldx, 0);
+  u32x4 r4 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + 2 * sldx, 0);
+  u32x4 r5 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + 2 * sldx, 0);
+  u32x4 r6 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + 3 * sldx, 0);
+  u32x4 r7 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + 3 * sldx, 0);
+
+#pragma unroll
+  for (int j = 0; j < (256 + 63) / 64; j++) {
+    const int i = tid + j * 64 * KW;
+    if (i < 256) offs_l[i] = ot[j];
   }
   for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
   __syncthreads();
+  // program: body offset for (row m0 + e%8, input row kb + e/8), in LDS
+  uint16_t* wp = prog_l + w * rpw * kBsRows;
+  for (int e0 = 0; e0 < ne; e0 += 64 * 8) {
+    if (e0) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) c[j] = coef(e0 + j * 64 + lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int e = e0 + j * 64 + lane;
+      if (e < ne) wp[e] = (uint16_t)offs_l[MODE == 0 ? c[j] : 0u];
+    }
+  }
+  __syncthreads();
 
-  const uint32_t col = (uint32_t)(cx * 64 + lane) * kBsBlock;
-  // wave-uniform values the asm reads from SGPRs
-  const uint64_t xa = reinterpret_cast<uint64_t>(X), pa = reinterpret_cast<uint64_t>(wp);
-  const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)K * (uint32_t)ldx);
-  const uint32_t kboff = __builtin_amdgcn_readfirstlane((uint32_t)kb * (uint32_t)ldx);
-  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(rpw / 4 - 1));
+  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / 4 - 1));
+  const uint64_t xa = reinterpret_cast<uint64_t>(X);
   const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
   const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
-  const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
-  const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
-  const uint32_t sldx = __builtin_amdgcn_readfirstlane((uint32_t)ldx);
-  asm volatile(
-      "s_waitcnt vmcnt(0)\n\t"  // program stores have reached L2
-      "s_dcache_inv\n\t"
-      "s_mov_b32 s40, %[xlo]\n\t"
-      "s_and_b32 s41, %[xhi], 0xffff\n\t"
-      "s_mov_b32 s42, %[nrec]\n\t"
-      "s_mov_b32 s43, 0x00020000\n\t"
-      "s_mov_b32 s44, %[kboff]\n\t"
-      "s_mov_b32 s45, %[ldx]\n\t"
-      "s_mov_b32 s46, %[plo]\n\t"
-      "s_mov_b32 s47, %[phi]\n\t"
-      "s_mov_b32 s48, 0\n\t"
-      "s_getpc_b64 s[74:75]\n\t"
-      ".Lpc_%=:\n\t"
-      "s_add_u32 s50, s74, .Lbs_b0_%= - .Lpc_%=\n\t"
-      "s_addc_u32 s51, s75, 0\n\t"
-      KODR_BS_PROLOGUE
-      "s_mov_b32 s72, %[ngrp]\n\t"
-      "s_cmp_eq_u32 s72, 0\n\t"
-      "s_cbranch_scc1 .Ltail_%=\n\t"
-      ".Lloop_%=:\n\t"
-      KODR_BS_LOOP
-      "s_sub_u32 s72, s72, 1\n\t"
-      "s_cmp_lg_u32 s72, 0\n\t"
-      "s_cbranch_scc1 .Lloop_%=\n\t"
-      ".Ltail_%=:\n\t"
-      KODR_BS_TAIL
-      // XOR this wave's 64 accumulator planes into the workgroup's LDS sums
-      KODR_BS_REDUCE
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "s_branch .Lend_%=\n\t"
-      KODR_BS_BODIES
-      ".Lend_%=:\n\t"
-      :
-      : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [kboff] "s"(kboff), [ldx] "s"(sldx),
-        [plo] "s"(plo), [phi] "s"(phi), [ngrp] "s"(ngrp), [col] "v"(col),
-        [lds] "v"((uint32_t)lane * 4u)
-      : KODR_BS_CLOBBERS);
+  const uint32_t roff = kboff + 4 * sldx;  // the asm streams from row kb + 4
+  const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp));  // LDS byte address
+  if (nr > 0 && MODE != 5) {
+    if constexpr (MODE == 3) {
+      KODR_BS_ASM(KODR_BS_LOOP_ND, KODR_BS_TAIL_ND);
+    } else if constexpr (MODE == 4) {
+      KODR_BS_ASM(KODR_BS_LOOP_NL, KODR_BS_TAIL_ND);
+    } else {
+      KODR_BS_ASM(KODR_BS_LOOP, KODR_BS_TAIL);
+    }
+  }
   __syncthreads();
 
   // rows m0..m0+7 of this column chunk: planes -> bytes, store
@@ -214,19 +273,24 @@ hipError_t bs_offsets(int dev, const uint32_t** out) {
     hipLaunchKernelGGL(gf_bs_export_kernel, dim3(1), dim3(64), 0, 0, d.offs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+    // the program stores offsets as 16 bits: the bodies must span < 64 KiB
+    uint32_t h[256];
+    if ((e = hipMemcpy(h, d.offs, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    for (int c = 1; c < 256; c++)
+      if (h[c] <= h[c - 1] || h[c] > 0xFFFFu) return hipErrorInvalidImage;
     d.ready = true;
   }
   *out = d.offs;
   return hipSuccess;
 }
 
-template <int KW>
+template <int KW, int MODE = 0>
 hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, int ldx, uint8_t* Y,
-                     size_t ldy, int ncols, int rpw, int ncx, int nrg, uint32_t* prog,
+                     size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes,
                      const uint32_t* offs, hipStream_t st) {
   const int nb = (ncx + 7) / 8 * 8 * nrg;
-  hipLaunchKernelGGL(gf_bs_kernel<KW>, dim3(nb), dim3(64 * KW), 64 * 64 * 4, st, A, lda, M, K, X, ldx, Y,
-                     ldy, ncols, rpw, ncx, nrg, prog, offs);
+  hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
+                     ldy, ncols, rpw, ncx, nrg, offs);
   return hipGetLastError();
 }
 
@@ -250,41 +314,91 @@ hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hip
   return hipGetLastError();
 }
 
+namespace {
+
+// Waves per SIMD the kernel's VGPR budget allows (gen_bs_bodies.py: VMAX
+// registers plus the compiler's own below v24, rounded to 8).
+constexpr int kBsWavesPerSimd = 512 / ((KODR_BS_VMAX + 7) / 8 * 8);
+constexpr int kBsKw[] = {1, 2, 3, 4, 6, 8, 12};
+constexpr size_t kLdsPerCu = 160 * 1024;
+
+size_t bs_lds_bytes(int kw, int rpw) { return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 2; }
+
+}  // namespace
+
 BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
   BsPlan p;
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
   p.nrg = (int)((M + kBsRows - 1) / kBsRows);
   const long tasks = (long)p.ncx * p.nrg;
-  int kw = 1;
-  while (kw < 16 && tasks * kw < 4096 && (long)kw * 8 * 2 <= (long)K) kw *= 2;
-  p.kw = kw;
-  const long per = ((long)K + kw - 1) / kw;
-  p.rpw = (int)std::max<long>(8, (per + 7) / 8 * 8);
+  const long kpad = ((long)K + 3) / 4 * 4;
+  // cost model in row-units: rounds of resident waves x (rows per wave + the
+  // per-wave fixed cost of program build, reduction and store, ~6 rows)
+  double best = 1e300;
+  for (int kw : kBsKw) {
+    if (kw > 4 * kBsWavesPerSimd) continue;  // one workgroup must fit a CU
+    const long rpw = ((kpad + kw - 1) / kw + 3) / 4 * 4;
+    const size_t lds = bs_lds_bytes(kw, (int)rpw);
+    if (lds > kLdsPerCu) continue;
+    const long wg_per_cu = std::min<long>((4L * kBsWavesPerSimd) / kw, (long)(kLdsPerCu / lds));
+    const long slots = 256L * wg_per_cu * kw;  // waves resident at once
+    const long waves = tasks * kw;
+    const long rounds = (waves + slots - 1) / slots;
+    const double cost = (double)rounds * (double)(rpw + 6);
+    if (cost < best - 1e-9) {
+      best = cost;
+      p.kw = kw;
+      p.rpw = (int)rpw;
+      p.lds_bytes = lds;
+    }
+  }
   p.blocks = (p.ncx + 7) / 8 * 8 * p.nrg;
-  p.prog_bytes = (size_t)p.blocks * kw * p.rpw * kBsRows * sizeof(uint32_t);
+  p.ok = best < 1e299;
   return p;
 }
 
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
-                      uint8_t* dY, size_t ldy, size_t ncols, uint32_t* d_prog, size_t prog_bytes,
-                      int device, hipStream_t stream) {
+                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream) {
   if (M == 0 || ncols == 0) return hipSuccess;
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
     return hipErrorInvalidValue;
   const BsPlan p = plan_gemm_bs(M, K, ncols);
-  if (prog_bytes < p.prog_bytes) return hipErrorInvalidValue;
+  if (!p.ok) return hipErrorInvalidValue;
   const uint32_t* offs = nullptr;
   hipError_t e = bs_offsets(device, &offs);
   if (e != hipSuccess) return e;
   const int iM = (int)M, iK = (int)K, ild = (int)lda, ilx = (int)ldx, inc = (int)ncols;
+  int mode = 0;
+  (void)mode;
+#ifdef KODR_TUNE_MODES
+  if (const char* env = getenv("KODR_BS_MODE")) mode = atoi(env);
+#endif
+#define KODR_BS_CALL(KW_, MODE_)                                                                  \
+  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, offs, stream)
+#ifdef KODR_TUNE_MODES
+#define KODR_BS_CASE(KW_)                                                                         \
+  case KW_:                                                                                       \
+    return mode == 1 ? KODR_BS_CALL(KW_, 1) : mode == 2 ? KODR_BS_CALL(KW_, 2)                    \
+         : mode == 3 ? KODR_BS_CALL(KW_, 3) : mode == 4 ? KODR_BS_CALL(KW_, 4)                    \
+         : mode == 5 ? KODR_BS_CALL(KW_, 5) : KODR_BS_CALL(KW_, 0);
+#else
+#define KODR_BS_CASE(KW_) \
+  case KW_:               \
+    return KODR_BS_CALL(KW_, 0);
+#endif
   switch (p.kw) {
-    case 1: return bs_launch<1>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, d_prog, offs, stream);
-    case 2: return bs_launch<2>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, d_prog, offs, stream);
-    case 4: return bs_launch<4>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, d_prog, offs, stream);
-    case 8: return bs_launch<8>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, d_prog, offs, stream);
-    default: return bs_launch<16>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, d_prog, offs, stream);
+    KODR_BS_CASE(1)
+    KODR_BS_CASE(2)
+    KODR_BS_CASE(3)
+    KODR_BS_CASE(4)
+    KODR_BS_CASE(6)
+    KODR_BS_CASE(8)
+    KODR_BS_CASE(12)
+    default: return hipErrorInvalidValue;
   }
+#undef KODR_BS_CASE
+#undef KODR_BS_CALL
 }
 
 }  // namespace kodr_amd

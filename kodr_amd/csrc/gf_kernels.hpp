@@ -41,14 +41,13 @@ hipError_t bs_body_offsets(int device, uint32_t* host_out);
 
 struct BsPlan {
   int ncx = 0, nrg = 0, kw = 1, rpw = 8, blocks = 0;
-  size_t prog_bytes = 0;  // scratch the launch needs for its body-offset program
+  size_t lds_bytes = 0;  // per workgroup: row sums, offset table, programs
+  bool ok = false;       // false when K is too large for the LDS program
 };
 BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols);
 
-// Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.  d_prog:
-// per-stream scratch of at least plan_gemm_bs(M, K, ncols).prog_bytes.
+// Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
-                      uint8_t* dY, size_t ldy, size_t ncols, uint32_t* d_prog, size_t prog_bytes,
-                      int device, hipStream_t stream);
+                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream);
 
 }  // namespace kodr_amd

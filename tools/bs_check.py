@@ -7,7 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "kodr_amd", "csrc"))
 import oracle
-from gen_bs_bodies import body_ops
+from gen_bs_bodies import body_bytes
 from kodr_amd import device, errors
 from kodr_amd._lib import lib
 
@@ -17,7 +17,7 @@ offs = np.zeros(256, np.uint32)
 errors.check(L_.rlnc_bs_body_offsets(ctx.handle, offs.ctypes.data_as(ctypes.c_void_p)))
 exp = np.zeros(256, np.uint32)
 for c in range(1, 256):
-    exp[c] = exp[c - 1] + 8 * len(body_ops(c - 1)) + 4
+    exp[c] = exp[c - 1] + body_bytes(c - 1)
 assert np.array_equal(offs, exp), (offs[:8], exp[:8])
 print("body offsets ok", offs[-1], flush=True)
 

@@ -2,13 +2,13 @@
 mode on gfx950 (measurement only).  Variants: (name, vbase, MT, PER, mode)
 acc planes v[vbase + 8m + j] (m < MT), x planes v[vbase + 8MT + i];
 mode 0 = straight line, 1 = swappc per body, 2 = threaded (body tail jumps
-to the next body through an SGPR target table indexed by M0)."""
+to the next body through an SGPR target table read with s_movrels), 3 = as 1
+without VGPR index mode (bodies all hit row 0: timing only)."""
 import os
 NB = 16
-VARIANTS = [("s_v176_mt8_p2", 176, 8, 2, 0), ("j_v176_mt8_p2", 176, 8, 2, 1),
-            ("j_v40_mt8_p2", 40, 8, 2, 1), ("j_v16_mt4_p2", 16, 4, 2, 1),
-            ("j_v40_mt8_p4", 40, 8, 4, 1), ("t_v40_mt8_p2", 40, 8, 2, 2),
-            ("t_v16_mt4_p2", 16, 4, 2, 2), ("s_v40_mt8_p2", 40, 8, 2, 0)]
+VARIANTS = [("s_v40_mt8_p1", 40, 8, 1, 0), ("j_v40_mt8_p1", 40, 8, 1, 1),
+            ("n_v40_mt8_p1", 40, 8, 1, 3), ("t_v40_mt8_p1", 40, 8, 1, 2),
+            ("p_v40_mt8_p1", 40, 8, 1, 4), ("p_v40_mt8_p2", 40, 8, 2, 4)]
 
 
 def kernel(name, vb, MT, PER, mode):
@@ -38,14 +38,24 @@ def kernel(name, vb, MT, PER, mode):
                     a = X + (j + c + p) % 8
                     b = X + (j + 3 * c + 2 * p + 1) % 8
                     B(f'v_bitop3_b32 v{vb + 8 * m + j}, v{vb + 8 * m + j}, v{a}, v{b} bitop3:0x96')
-    elif mode == 1:
+    elif mode == 4:   # index mode on for the whole row; bodies advance M0 by 8
+        B('s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)')
         for m in range(MT):
             c = (m * 5 + 3) % NB
             B(f's_add_u32 s92, s90, .Lbody{c}_%= - .Lpc_%=')
             B('s_addc_u32 s93, s91, 0')
-            B(f's_set_gpr_idx_on {8 * m}, gpr_idx(SRC0,DST)')
             B('s_swappc_b64 s[94:95], s[92:93]')
-            B('s_set_gpr_idx_off')
+        B('s_set_gpr_idx_off')
+    elif mode in (1, 3):
+        for m in range(MT):
+            c = (m * 5 + 3) % NB
+            B(f's_add_u32 s92, s90, .Lbody{c}_%= - .Lpc_%=')
+            B('s_addc_u32 s93, s91, 0')
+            if mode == 1:
+                B(f's_set_gpr_idx_on {8 * m}, gpr_idx(SRC0,DST)')
+            B('s_swappc_b64 s[94:95], s[92:93]')
+            if mode == 1:
+                B('s_set_gpr_idx_off')
     else:
         # M0 = 8m drives both the VGPR index and (divided) the next-target pick
         B('s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)')
@@ -65,14 +75,19 @@ def kernel(name, vb, MT, PER, mode):
                 b = X + (j + 3 * c + 2 * p + 1) % 8
                 B(f'v_bitop3_b32 v{vb + j}, v{vb + j}, v{a}, v{b} bitop3:0x96')
         if mode == 2:
-            # next target: table entry (m+1) = s[22 + 2m]; M0 = 8m -> s_movrels index 2m+2 needs M0/4
-            B('s_lshr_b32 s96, m0, 2')
-            B('s_add_u32 m0, m0, 8')
-            B('s_mov_b32 s97, m0')
-            B('s_mov_b32 m0, s96')
-            B('s_movrels_b64 s[92:93], s[62:63]')
+            # M0 = mode bits | 8m in index mode: entry m+1 of the target table
+            # s[60 + 2j] is read with M0 = 2m, then M0 = mode bits | 8(m+1)
+            B('s_mov_b32 s96, m0')
+            B('s_and_b32 s97, s96, 0xff')
+            B('s_lshr_b32 s97, s97, 2')
             B('s_mov_b32 m0, s97')
+            B('s_nop 0')
+            B('s_movrels_b64 s[92:93], s[62:63]')
+            B('s_add_u32 m0, s96, 8')
             B('s_setpc_b64 s[92:93]')
+        elif mode == 4:
+            B('s_add_u32 m0, m0, 8')
+            B('s_setpc_b64 s[94:95]')
         else:
             B('s_setpc_b64 s[94:95]')
     B('.Lend_%=:')
