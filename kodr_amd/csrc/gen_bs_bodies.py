@@ -22,15 +22,18 @@ and the body returns with s_setpc_b64.
 Usage: gen_bs_bodies.py > gf_bs_bodies.inc
 """
 
-ACC = 24           # 8 rows x 8 planes: v[24..87]
-TL0 = 88           # TL table, 15 registers v[88..102] (singles first, as aligned pairs)
-TH0 = 104          # TH table v[104..118]
-RING = 120         # 4 row slots x 8 planes: v[120..151]
+# Register map: 128 VGPRs in all (4 waves per SIMD), the compiler keeping its
+# own values in v[0..ACC).
+ACC = 12           # 8 rows x 8 planes: v[12..75]
+TL0 = 76           # TL table, 15 registers v[76..90] (singles first, as aligned pairs)
+PL = 91            # LDS address of the next program row
+TH0 = 92           # TH table v[92..106]
+P = 2              # ring depth (rows in flight per wave)
+RING = 108         # P row slots x 8 planes: v[108..123]
+PR = RING + 8 * P  # next row's packed offsets, read from the LDS program: v[124..127]
 RET = 54           # return address s[54:55]
 OCT = 56           # s[56:59]: this row's 8 body offsets, two 16-bit offsets per SGPR
-PR = RING + 32     # next row's packed offsets, read from the LDS program: v[152..155]
-PL = PR + 4        # LDS address of the next program row: v156
-VMAX = PL + 1      # first VGPR not used by the asm
+VMAX = PR + 4      # first VGPR not used by the asm
 # table slot of subset s (1..15): the singles 1, 2, 4, 8 first so that each
 # pair of them is one aligned v_pk_mov_b32, then the combinations in order
 SLOT = {1: 0, 2: 1, 4: 2, 8: 3}
@@ -131,20 +134,20 @@ def main_loop():
     pro = [f"v_mov_b32 v{PL}, %[pl]", f"ds_read_b128 v[{PR}:{PR + 3}], v{PL}", f"v_add_u32_e32 v{PL}, 16, v{PL}"]
     pro += [f"v_mov_b32 v{ACC + r}, 0" for r in range(64)]
     loop = []
-    for slot in range(4):
-        loop += row(slot, 6, True)
+    for slot in range(P):
+        loop += row(slot, 2 * (P - 1), True)
     tail = []
-    for slot in range(4):
-        tail += row(slot, 2 * (3 - slot), False)
+    for slot in range(P):
+        tail += row(slot, 2 * (P - 1 - slot), False)
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     # tuning variants (KODR_TUNE_MODES builds only): rows without body dispatch
     loop_nd, tail_nd = [], []
-    for slot in range(4):
-        loop_nd += row(slot, 6, True, False)
-        tail_nd += row(slot, 2 * (3 - slot), False, False)
+    for slot in range(P):
+        loop_nd += row(slot, 2 * (P - 1), True, False)
+        tail_nd += row(slot, 2 * (P - 1 - slot), False, False)
     loop_nl = []
-    for slot in range(4):
-        loop_nl += row(slot, 6, False, False)
+    for slot in range(P):
+        loop_nl += row(slot, 2 * (P - 1), False, False)
     return [("KODR_BS_PROLOGUE", pro), ("KODR_BS_LOOP", loop), ("KODR_BS_TAIL", tail),
             ("KODR_BS_REDUCE", red), ("KODR_BS_LOOP_ND", loop_nd), ("KODR_BS_TAIL_ND", tail_nd),
             ("KODR_BS_LOOP_NL", loop_nl)]
@@ -162,7 +165,10 @@ def main():
            f"// accumulators v[{ACC}..{ACC + 63}] (indexed), XOR tables v[{TL0}..{TH0 + 14}],",
            f"// row ring v[{RING}..{VMAX - 1}], return s[{RET}:{RET + 1}]",
            f"#define KODR_BS_VMAX {VMAX}",
-           f"#define KODR_BS_RING {RING}"]
+           f"#define KODR_BS_P {P}"]
+    # the ring rows enter the asm as in/out operands pinned to their slots
+    ops = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
+    out.append("#define KODR_BS_RING_OPERANDS " + ", ".join(ops))
     bodies = []
     n_inst = 0
     for c in range(256):
@@ -180,8 +186,8 @@ def main():
     out.append('  "s_waitcnt vmcnt(0)\\n\\t"')
     for name, lines in main_loop():
         out += emit(name, lines)
-    # the ring v[RING..RING+31] is bound to in/out operands, not clobbered
-    clob = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 32, VMAX))]
+    # the ring v[RING..RING+8P) is bound to in/out operands, not clobbered
+    clob = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, VMAX))]
     clob += [f'"s{r}"' for r in list(range(40, 46)) + list(range(50, 61)) + [72, 74, 75]]
     out.append("#define KODR_BS_CLOBBERS " + ", ".join(clob) + ', "scc", "memory"')
     out.append(f"// {n_inst} body instructions, {n_inst / 256:.2f} per coefficient; "

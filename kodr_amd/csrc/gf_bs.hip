@@ -21,8 +21,8 @@
 // range of at most rpw input rows; the KW waves of a workgroup split K and are
 // XOR-reduced in LDS.  Per wave, the body offsets for its (row, k) pairs are
 // built once into LDS ("program") and moved to SGPRs with v_readfirstlane, one
-// row ahead.  X rows stream through a 4-deep register ring of buffer loads
-// (rows >= K are outside num_records and read as zero); the first 4 are in
+// row ahead.  X rows stream through a P-deep register ring of buffer loads
+// (rows >= K are outside num_records and read as zero); the first P are in
 // flight while the program is built.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -125,20 +125,18 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
       "s_branch .Lend_%=\n\t"                                                            \
       KODR_BS_BODIES                                                                     \
       ".Lend_%=:\n\t"                                                                    \
-      : "+{v[120:123]}"(r0), "+{v[124:127]}"(r1), "+{v[128:131]}"(r2), "+{v[132:135]}"(r3), \
-        "+{v[136:139]}"(r4), "+{v[140:143]}"(r5), "+{v[144:147]}"(r6), "+{v[148:151]}"(r7)  \
+      : KODR_BS_RING_OPERANDS                                                            \
       : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx), \
         [ngrp] "s"(ngrp), [col] "v"(col), [lds] "v"((uint32_t)lane * 4u), [pl] "v"(pl)    \
       : KODR_BS_CLOBBERS)
 
-static_assert(KODR_BS_RING == 120, "ring operands above assume the generator's register map");
 
 // MODE (tuning builds only, -DKODR_TUNE_MODES): 1 = every program entry is the
 // empty body (dispatch without XOR work), 2 = as 1 without reading A, 3 = no
 // dispatch at all (row stream + table prep + reduction only), 4 = as 3 without
 // the row stream, 5 = no main loop (prologue, reduction and store only).
 template <int KW, int MODE = 0>
-__global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
+__global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
     const uint32_t* __restrict__ offs) {
@@ -157,8 +155,9 @@ __global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
   const int cx = (b / (8 * nrg)) * 8 + (b & 7);
   if (cx >= ncx) return;
   const int m0 = rg * kBsRows, kb = w * rpw;
-  // this wave's input rows: [kb, kb + nr), nr a multiple of 4 (rows >= K read zero)
-  const int kpad = (K + 3) & ~3;
+  // this wave's input rows: [kb, kb + nr), nr a multiple of the ring depth P
+  // (rows >= K read zero)
+  const int kpad = (K + KODR_BS_P - 1) / KODR_BS_P * KODR_BS_P;
   const int nr = __builtin_amdgcn_readfirstlane(max(0, min(rpw, kpad - kb)));
 
   // Prologue loads in retirement order (vmcnt counts in issue order): the
@@ -188,14 +187,12 @@ __global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
       __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)nrec, 0x00020000);
   // (unconditional: a wave past K reads zeros, and a branch here would make
   // the compiler's waitcnt pass drain these loads at the next LDS write)
-  u32x4 r0 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff, 0);
-  u32x4 r1 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff, 0);
-  u32x4 r2 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + sldx, 0);
-  u32x4 r3 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + sldx, 0);
-  u32x4 r4 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + 2 * sldx, 0);
-  u32x4 r5 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + 2 * sldx, 0);
-  u32x4 r6 = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + 3 * sldx, 0);
-  u32x4 r7 = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + 3 * sldx, 0);
+  u32x4 ring[2 * KODR_BS_P];
+#pragma unroll
+  for (int i = 0; i < KODR_BS_P; i++) {
+    ring[2 * i] = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + i * sldx, 0);
+    ring[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + i * sldx, 0);
+  }
 
 #pragma unroll
   for (int j = 0; j < (256 + 63) / 64; j++) {
@@ -219,11 +216,11 @@ __global__ __launch_bounds__(64 * KW) void gf_bs_kernel(
   }
   __syncthreads();
 
-  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / 4 - 1));
+  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / KODR_BS_P - 1));
   const uint64_t xa = reinterpret_cast<uint64_t>(X);
   const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
   const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
-  const uint32_t roff = kboff + 4 * sldx;  // the asm streams from row kb + 4
+  const uint32_t roff = kboff + KODR_BS_P * sldx;  // the asm streams from row kb + P
   const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp));  // LDS byte address
   if (nr > 0 && MODE != 5) {
     if constexpr (MODE == 3) {
@@ -319,7 +316,7 @@ namespace {
 // Waves per SIMD the kernel's VGPR budget allows (gen_bs_bodies.py: VMAX
 // registers plus the compiler's own below v24, rounded to 8).
 constexpr int kBsWavesPerSimd = 512 / ((KODR_BS_VMAX + 7) / 8 * 8);
-constexpr int kBsKw[] = {1, 2, 3, 4, 6, 8, 12};
+constexpr int kBsKw[] = {1, 2, 3, 4, 6, 8, 16};
 constexpr size_t kLdsPerCu = 160 * 1024;
 
 size_t bs_lds_bytes(int kw, int rpw) { return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 2; }
@@ -331,13 +328,14 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
   p.nrg = (int)((M + kBsRows - 1) / kBsRows);
   const long tasks = (long)p.ncx * p.nrg;
-  const long kpad = ((long)K + 3) / 4 * 4;
+  constexpr long P = KODR_BS_P;
+  const long kpad = ((long)K + P - 1) / P * P;
   // cost model in row-units: rounds of resident waves x (rows per wave + the
   // per-wave fixed cost of program build, reduction and store, ~6 rows)
   double best = 1e300;
   for (int kw : kBsKw) {
     if (kw > 4 * kBsWavesPerSimd) continue;  // one workgroup must fit a CU
-    const long rpw = ((kpad + kw - 1) / kw + 3) / 4 * 4;
+    const long rpw = ((kpad + kw - 1) / kw + P - 1) / P * P;
     const size_t lds = bs_lds_bytes(kw, (int)rpw);
     if (lds > kLdsPerCu) continue;
     const long wg_per_cu = std::min<long>((4L * kBsWavesPerSimd) / kw, (long)(kLdsPerCu / lds));
@@ -394,7 +392,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     KODR_BS_CASE(4)
     KODR_BS_CASE(6)
     KODR_BS_CASE(8)
-    KODR_BS_CASE(12)
+    KODR_BS_CASE(16)
     default: return hipErrorInvalidValue;
   }
 #undef KODR_BS_CASE

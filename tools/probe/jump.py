@@ -30,16 +30,17 @@ def model(t, MT, PER):
 e0, e1 = ctx.event(), ctx.event()
 iters = 400
 for vi, (name, vb, MT, PER, mode) in enumerate(VARIANTS):
-    p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), 1, 1, st)
+    p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), 1, 1, st, 0)
     ctx.synchronize()
     got = ctx.d2h(out, 256 * 64 * 4).view(np.uint32).reshape(256, 64)
     ok = mode == 3 or all(list(got[t][:8 * MT]) == model(t, MT, PER) for t in (0, 1, 63, 200))
-    for blocks in (2048, 8192):
-        p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), blocks, 5, st)
+    blocks = 8192
+    for wps, lds in ((1, 160 * 1024), (2, 80 * 1024), (3, 0)):
+        p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), blocks, 5, st, lds)
         ctx.record(e0)
-        p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), blocks, iters, st)
+        p.probe_jump(vi, ctypes.c_void_p(out), ctypes.c_void_p(din), blocks, iters, st, lds)
         ctx.record(e1)
         ms = device.Context.elapsed_ms(e0, e1)
         insts = blocks * 4 * iters * MT * PER * 8
-        print(f"{name:16s} ok={ok} blocks {blocks}: {ms:.3f} ms  {insts*64/ms/1e9:.2f} T lane-op/s  "
+        print(f"{name:16s} ok={ok} waves/SIMD {wps}: {ms:.3f} ms  {insts*64/ms/1e9:.2f} T lane-op/s  "
               f"cyc/inst/SIMD@2.4 = {ms*1e-3*2.4e9*1024/insts:.2f}", flush=True)
