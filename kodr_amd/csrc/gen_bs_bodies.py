@@ -89,19 +89,29 @@ def body_bytes(c):
 
 
 def table_lines(slot):
-    """Row prep: TL/TH from ring slot `slot` (singles moved, combos XORed)."""
+    """Row prep: TL/TH from ring slot `slot`: singles moved (v_pk_mov_b32),
+    pairs and triples XORed straight from the ring (v_xor / v_bitop3), the
+    4-subset from two pairs.  Nothing waits on the instruction before it."""
     base = RING + 8 * slot
     out = []
-    for half, reg in ((0, tl), (1, th)):
-        for i in (0, 2):
+    for i in (0, 2):
+        for half, reg in ((0, tl), (1, th)):
             src = base + 4 * half + i
             out.append(f"v_pk_mov_b32 v[{reg(1 << i)}:{reg(1 << i) + 1}], v[{src}:{src + 1}], "
                        f"v[{src}:{src + 1}] op_sel:[0,1]")
-        for s in range(3, 16):
-            if s & (s - 1) == 0:
+    subsets = [s_ for s_ in range(3, 16) if s_ & (s_ - 1)]
+    for pop in (2, 3, 4):
+        for s_ in subsets:
+            if bin(s_).count("1") != pop:
                 continue
-            low = s & -s
-            out.append(f"v_xor_b32_e32 v{reg(s)}, v{reg(low)}, v{reg(s ^ low)}")
+            for half, reg in ((0, tl), (1, th)):
+                srcs = [base + 4 * half + i for i in range(4) if s_ >> i & 1]
+                if pop == 2:
+                    out.append(f"v_xor_b32_e32 v{reg(s_)}, v{srcs[0]}, v{srcs[1]}")
+                elif pop == 3:
+                    out.append(f"v_bitop3_b32 v{reg(s_)}, v{srcs[0]}, v{srcs[1]}, v{srcs[2]} bitop3:0x96")
+                else:
+                    out.append(f"v_xor_b32_e32 v{reg(s_)}, v{reg(3)}, v{reg(12)}")
     return out
 
 
@@ -111,12 +121,14 @@ def main_loop():
     is in LDS at %[pl].  SGPRs: s[40:43] X descriptor, s44 row offset, s45
     ldx, s[50:51] body 0, s[52:53] jump target, s[56:63] this row's offsets,
     s72 group counter."""
-    def row(slot, wait, loads, dispatch=True):
+    def row(slot, wait, loads, dispatch=True, rfl=True, prog=True):
         t = [f"s_waitcnt vmcnt({wait}) lgkmcnt(0)"]
         # this row's offsets to SGPRs, then fetch the next row's (an LDS read
         # past the last row reads unused LDS and is never consumed)
-        t += [f"v_readfirstlane_b32 s{OCT + i}, v{PR + i}" for i in range(4)]
-        t += [f"ds_read_b128 v[{PR}:{PR + 3}], v{PL}", f"v_add_u32_e32 v{PL}, 16, v{PL}"]
+        if rfl:
+            t += [f"v_readfirstlane_b32 s{OCT + i}, v{PR + i}" for i in range(4)]
+        if prog:
+            t += [f"ds_read_b128 v[{PR}:{PR + 3}], v{PL}", f"v_add_u32_e32 v{PL}, 16, v{PL}"]
         t += table_lines(slot)
         if loads:
             b = RING + 8 * slot
@@ -145,12 +157,14 @@ def main_loop():
     for slot in range(P):
         loop_nd += row(slot, 2 * (P - 1), True, False)
         tail_nd += row(slot, 2 * (P - 1 - slot), False, False)
-    loop_nl = []
+    loop_nl, loop_nl2, loop_nl3 = [], [], []
     for slot in range(P):
         loop_nl += row(slot, 2 * (P - 1), False, False)
+        loop_nl2 += row(slot, 2 * (P - 1), False, False, rfl=False)
+        loop_nl3 += row(slot, 2 * (P - 1), False, False, rfl=False, prog=False)
     return [("KODR_BS_PROLOGUE", pro), ("KODR_BS_LOOP", loop), ("KODR_BS_TAIL", tail),
             ("KODR_BS_REDUCE", red), ("KODR_BS_LOOP_ND", loop_nd), ("KODR_BS_TAIL_ND", tail_nd),
-            ("KODR_BS_LOOP_NL", loop_nl)]
+            ("KODR_BS_LOOP_NL", loop_nl), ("KODR_BS_LOOP_NL2", loop_nl2), ("KODR_BS_LOOP_NL3", loop_nl3)]
 
 
 def emit(name, lines):

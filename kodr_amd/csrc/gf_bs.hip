@@ -227,6 +227,10 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       KODR_BS_ASM(KODR_BS_LOOP_ND, KODR_BS_TAIL_ND);
     } else if constexpr (MODE == 4) {
       KODR_BS_ASM(KODR_BS_LOOP_NL, KODR_BS_TAIL_ND);
+    } else if constexpr (MODE == 6) {
+      KODR_BS_ASM(KODR_BS_LOOP_NL2, KODR_BS_TAIL_ND);
+    } else if constexpr (MODE == 7) {
+      KODR_BS_ASM(KODR_BS_LOOP_NL3, KODR_BS_TAIL_ND);
     } else {
       KODR_BS_ASM(KODR_BS_LOOP, KODR_BS_TAIL);
     }
@@ -379,7 +383,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   case KW_:                                                                                       \
     return mode == 1 ? KODR_BS_CALL(KW_, 1) : mode == 2 ? KODR_BS_CALL(KW_, 2)                    \
          : mode == 3 ? KODR_BS_CALL(KW_, 3) : mode == 4 ? KODR_BS_CALL(KW_, 4)                    \
-         : mode == 5 ? KODR_BS_CALL(KW_, 5) : KODR_BS_CALL(KW_, 0);
+         : mode == 5 ? KODR_BS_CALL(KW_, 5) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
+         : mode == 7 ? KODR_BS_CALL(KW_, 7) : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

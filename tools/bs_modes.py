@@ -1,6 +1,7 @@
 """Time gf_gemm_bs per tuning mode (needs the KODR_TUNE_MODES build, loaded via
 KODR_RLNC_LIB): 0 normal, 1 empty bodies, 2 empty bodies without reading A,
-3 no dispatch, 4 = 3 without the row stream, 5 no main loop.  32 MiB/256 generation, B rows per launch."""
+3 no dispatch, 4 = 3 without the row stream, 5 no main loop,
+6 = 4 without v_readfirstlane, 7 = 6 without the LDS program read.  32 MiB/256 generation, B rows per launch."""
 import ctypes, os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -25,7 +26,7 @@ for B in Bs:
     dV, dO = ctx.alloc(V.nbytes), ctx.alloc(B * L)
     ctx.h2d(dV, V)
     line = []
-    for mode in (0, 1, 2, 3, 4, 5):
+    for mode in (0, 1, 3, 4, 5, 6, 7):
         os.environ["KODR_BS_MODE"] = str(mode)
         for i in range(3):
             errors.check(L_.rlnc_gf_matmul_bs_device(ctx.handle, dV, k, B, k, gens[i % G], L, dO, L, L))
