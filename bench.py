@@ -84,9 +84,17 @@ def main():
     import torch  # plumbing: process group + shared HIP runtime
     import torch.distributed as dist
 
+    # KODR_BENCH_REHEARSE=1: rehearsal of the N>1 path on a one-GPU box (every
+    # rank on device 0, gloo instead of RCCL).  Never used for reported numbers.
+    rehearse = os.environ.get("KODR_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo", init_method="env://")
+        else:
+            dist.init_process_group("nccl", init_method="env://", device_id=torch.device("cuda", local))
 
     from kodr_amd import device as kdev
     from kodr_amd import errors

@@ -5,16 +5,18 @@ HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 cd "$HERE"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 ARCH="${KODR_ARCH:-gfx950}"
-mkdir -p build
+OUT="${KODR_OUT:-libkodr_rlnc.so}"   # e.g. tune/libkodr_rlnc.so for a -DKODR_TUNE_MODES build
+OBJ="${KODR_OBJ:-build}"
+mkdir -p "$OBJ" "$(dirname "$OUT")"
 FLAGS=(-O3 -std=c++17 -fPIC -Wall -Wno-unused-function ${KODR_EXTRA_FLAGS:-})
 # the 256 coefficient bodies and row loop of the bit-sliced kernel
 python3 csrc/gen_bs_bodies.py > csrc/gf_bs_bodies.inc
 pids=()
-"$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_kernels.hip -o build/gf_kernels.o & pids+=($!)
-"$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_bs.hip -o build/gf_bs.o & pids+=($!)
-"$HIPCC" "${FLAGS[@]}" -c csrc/capi.cpp -o build/capi.o & pids+=($!)
-"$HIPCC" "${FLAGS[@]}" -c csrc/decoder_core.cpp -o build/decoder_core.o & pids+=($!)
-for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o libkodr_rlnc.so build/gf_kernels.o build/gf_bs.o build/capi.o build/decoder_core.o \
+"$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_kernels.hip -o "$OBJ"/gf_kernels.o & pids+=($!)
+"$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_bs.hip -o "$OBJ"/gf_bs.o & pids+=($!)
+"$HIPCC" "${FLAGS[@]}" -c csrc/capi.cpp -o "$OBJ"/capi.o & pids+=($!)
+"$HIPCC" "${FLAGS[@]}" -c csrc/decoder_core.cpp -o "$OBJ"/decoder_core.o & pids+=($!)
+for p in "${pids[@]}"; do wait "$p" || { echo "build failed" >&2; exit 1; }; done
+"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o "$OUT" "$OBJ"/gf_kernels.o "$OBJ"/gf_bs.o "$OBJ"/capi.o "$OBJ"/decoder_core.o \
   -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
-echo "built $HERE/libkodr_rlnc.so"
+echo "built $HERE/$OUT"

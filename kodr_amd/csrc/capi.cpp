@@ -197,7 +197,8 @@ constexpr size_t kBsMinRows = 16;
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32) || !kodr_amd::plan_gemm_bs(M, K, ncols).ok)
+  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32) || !kodr_amd::plan_gemm_bs(M, K, ncols).ok ||
+      !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {
     TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
@@ -786,7 +787,7 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   const size_t recv = d->core.received();
   rlnc_ctx* ctx = d->ctx;
   if (M < kBsMinRows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
-      !kodr_amd::plan_gemm_bs(M, recv, d->L).ok)
+      !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
     HIPC(hipStreamSynchronize(ctx->stream));

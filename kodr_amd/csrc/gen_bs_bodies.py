@@ -8,32 +8,54 @@ bit M_c[j][i] = bit j of (c * 2^i) is set (poly 0x11D, gf256.go:15-44).
 
 Per input row the wave first builds a table of XOR combinations ("Four
 Russians"): TL[s] = XOR of planes {0..3} selected by the 4-bit mask s, TH[s]
-the same over planes {4..7} (30 registers, 8 moves + 22 XORs, shared by the 8
+the same over planes {4..7} (30 registers, 4 moves + 22 XORs, shared by the 8
 output rows).  Then every output plane needs one instruction:
 
     acc_j ^= TL[S_j & 15] ^ TH[S_j >> 4]        (v_bitop3_b32, XOR3)
 
-so a coefficient's body is at most 8 VALU instructions, one per non-empty
-S_j.  Bodies address the accumulators v[ACC..ACC+7] under VGPR index mode
-(SRC0|DST) so one body serves every output row m (index 8m); the table is
-read through src1/src2, unindexed.  The wave reaches body[c] with s_swappc_b64
-and the body returns with s_setpc_b64.
+so a coefficient's body is at most 8 VALU instructions, one per non-empty S_j.
+
+Threaded dispatch.  A wave applies 8 coefficients per input row (output rows
+m = 0..7).  The bodies exist in 4 copies; copy r XORs into accumulator set r
+and ends with s_setpc_b64 to T[r+1] (T[4] for r = 3), so body m jumps straight
+to body m+1: one taken branch per body and no SALU inside it (measured on
+gfx950: 26 SIMD-cycles per 8-XOR body against 43.6 for a s_swappc call and
+return, tools/probe/dispatch.py).  Rows 4..7 reuse copies 0..3 under VGPR
+index mode (SRC0|DST, M0 index 32): a stub between the two halves advances M0
+and moves the second half's targets into T[1..3].  4 copies of 256 bodies are
+about 69 KB, which the instruction cache holds (8 copies thrash it).
+
+The bodies live in gf_bs_export_kernel, which never runs them: it only exports
+their byte offsets.  Every gf_bs_kernel instance jumps into that one copy with
+absolute targets that its prologue looked up per coefficient.
 
 Usage: gen_bs_bodies.py > gf_bs_bodies.inc
 """
 
+import os
+
 # Register map: 128 VGPRs in all (4 waves per SIMD), the compiler keeping its
 # own values in v[0..ACC).
-ACC = 12           # 8 rows x 8 planes: v[12..75]
+ACC = 12           # 8 rows x 8 planes: v[12..75]; copy r owns v[12+8r .. 19+8r]
 TL0 = 76           # TL table, 15 registers v[76..90] (singles first, as aligned pairs)
-PL = 91            # LDS address of the next program row
+PL = 91            # LDS address of the next program quad
 TH0 = 92           # TH table v[92..106]
-P = 2              # ring depth (rows in flight per wave)
+P = int(os.environ.get("KODR_BS_P", "2"))   # ring depth (rows in flight per wave)
 RING = 108         # P row slots x 8 planes: v[108..123]
-PR = RING + 8 * P  # next row's packed offsets, read from the LDS program: v[124..127]
-RET = 54           # return address s[54:55]
-OCT = 56           # s[56:59]: this row's 8 body offsets, two 16-bit offsets per SGPR
-VMAX = PR + 4      # first VGPR not used by the asm
+PG = RING + 8 * P  # program chunk: 8 rows x 8 targets, lane 8j + m (absolute lo words)
+PGN = PG + 1       # the next chunk, in flight from LDS
+VMAX = PGN + 1     # first VGPR not used by the asm
+NCOPY = 4
+# SGPRs: T[0..4] = s[60:69] (T[0] entry, T[r+1] the tail of copy r), the
+# second half's targets s[70:77], the stub s[78:79], this row's return
+# address s[80:81], the 8 rows' return addresses s[82:97]
+T0 = 60
+H2 = 70
+STUB = 78
+RT = 80
+RET = 82
+CNT = 98
+GPC = 56           # s_getpc scratch s[56:57]
 # table slot of subset s (1..15): the singles 1, 2, 4, 8 first so that each
 # pair of them is one aligned v_pk_mov_b32, then the combinations in order
 SLOT = {1: 0, 2: 1, 4: 2, 8: 3}
@@ -72,20 +94,32 @@ def body_ops(c):
     return ops
 
 
-def body_lines(c):
+def body_lines(c, r=0):
+    """Body of coefficient c in copy r: XOR3s into v[ACC+8r+j] (indexed), then
+    jump to T[r+1]."""
     out = []
     for j, lo, hi in body_ops(c):
-        a = ACC + j
+        a = ACC + 8 * r + j
         if lo and hi:
             out.append(f"v_bitop3_b32 v{a}, v{a}, v{tl(lo)}, v{th(hi)} bitop3:0x96")
         else:
             out.append(f"v_xor_b32_e64 v{a}, v{a}, v{tl(lo) if lo else th(hi)}")
-    out.append(f"s_setpc_b64 s[{RET}:{RET + 1}]")
+    out.append(f"s_setpc_b64 s[{T0 + 2 * (r + 1)}:{T0 + 2 * (r + 1) + 1}]")
     return out
 
 
 def body_bytes(c):
     return 8 * len(body_ops(c)) + 4      # VOP3 = 8 bytes, s_setpc_b64 = 4
+
+
+def body_offsets():
+    """Byte offset of body (r, c) from body (0, 0), index r*256 + c."""
+    offs, off = [], 0
+    for _r in range(NCOPY):
+        for c in range(256):
+            offs.append(off)
+            off += body_bytes(c)
+    return offs, off
 
 
 def table_lines(slot):
@@ -115,97 +149,166 @@ def table_lines(slot):
     return out
 
 
-def main_loop():
-    """Row macros.  The ring's first 4 rows arrive as asm inputs (loaded by the
-    compiler before the program build); the program (8 body offsets per row)
-    is in LDS at %[pl].  SGPRs: s[40:43] X descriptor, s44 row offset, s45
-    ldx, s[50:51] body 0, s[52:53] jump target, s[56:63] this row's offsets,
-    s72 group counter."""
-    def row(slot, wait, loads, dispatch=True, rfl=True, prog=True):
-        t = [f"s_waitcnt vmcnt({wait}) lgkmcnt(0)"]
-        # this row's offsets to SGPRs, then fetch the next row's (an LDS read
-        # past the last row reads unused LDS and is never consumed)
-        if rfl:
-            t += [f"v_readfirstlane_b32 s{OCT + i}, v{PR + i}" for i in range(4)]
-        if prog:
-            t += [f"ds_read_b128 v[{PR}:{PR + 3}], v{PL}", f"v_add_u32_e32 v{PL}, 16, v{PL}"]
-        t += table_lines(slot)
-        if loads:
-            b = RING + 8 * slot
-            t += [f"buffer_load_dwordx4 v[{b}:{b + 3}], %[col], s[40:43], s44 offen",
-                  f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16",
-                  "s_add_u32 s44, s44, s45"]
-        for m in range(8 if dispatch else 0):
-            half = (f"s_and_b32 s60, s{OCT + m // 2}, 0xffff" if m % 2 == 0
-                    else f"s_lshr_b32 s60, s{OCT + m // 2}, 16")
-            t += [half, "s_add_u32 s52, s50, s60", "s_addc_u32 s53, s51, 0",
-                  f"s_set_gpr_idx_on {8 * m}, gpr_idx(SRC0,DST)",
-                  f"s_swappc_b64 s[{RET}:{RET + 1}], s[52:53]", "s_set_gpr_idx_off"]
-        return t
+def row_lines(j, dispatch=True, loads=True):
+    """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
+    holds the chunk's program: lane 8j + m = the target of output row m
+    (absolute lo word; hi words preset), read with v_readlane, so no LDS round
+    trip sits inside a row."""
+    slot = j % P
+    h = lambda i: T0 + 2 * i  # noqa: E731
+    t = [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
+    t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)]
+    t += table_lines(slot)
+    b = RING + 8 * slot
+    # the row P ahead into this slot (rows past the wave's range read zero)
+    if loads:
+        t += [f"buffer_load_dwordx4 v[{b}:{b + 3}], %[col], s[40:43], s44 offen",
+              f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16",
+              "s_add_u32 s44, s44, s45"]
+    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)]
+    if dispatch:
+        t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{STUB}:{STUB + 1}]",
+              f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]",
+              "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
+              f"s_setpc_b64 s[{h(0)}:{h(0) + 1}]",
+              f".Lret{j}_%=:",
+              "s_set_gpr_idx_off"]
+    return t
 
-    pro = [f"v_mov_b32 v{PL}, %[pl]", f"ds_read_b128 v[{PR}:{PR + 3}], v{PL}", f"v_add_u32_e32 v{PL}, 16, v{PL}"]
+
+def stub_lines():
+    """Between the two halves of a row: rows 4..7 reuse copies 0..3 at M0
+    index 32, with targets T[1..3] from the second half's registers and T[4]
+    the row's return address."""
+    h = lambda i: T0 + 2 * i  # noqa: E731
+    t = [".Lstub_%=:", "s_add_u32 m0, m0, 32"]
+    t += [f"s_mov_b64 s[{h(m)}:{h(m) + 1}], s[{H2 + 2 * m}:{H2 + 2 * m + 1}]" for m in (1, 2, 3)]
+    t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{RT}:{RT + 1}]", f"s_setpc_b64 s[{H2}:{H2 + 1}]"]
+    return t
+
+
+def prologue_lines(dispatch=True):
+    """Descriptor, stub and per-row return addresses, target hi words, the
+    first two program chunks, zeroed accumulators.  SGPRs: s[40:43] X
+    descriptor (num_records = end of this wave's rows), s44 row offset,
+    s45 ldx."""
+    pro = ["s_mov_b32 s40, %[xlo]", "s_and_b32 s41, %[xhi], 0xffff", "s_mov_b32 s42, %[nrec]",
+           "s_mov_b32 s43, 0x00020000", "s_mov_b32 s44, %[roff]", "s_mov_b32 s45, %[ldx]",
+           f"s_getpc_b64 s[{GPC}:{GPC + 1}]", ".Lpc_%=:"]
+    if dispatch:
+        for reg, lab in [(STUB, "stub")] + [(RET + 2 * j, f"ret{j}") for j in range(8)]:
+            pro += [f"s_add_u32 s{reg}, s{GPC}, .L{lab}_%= - .Lpc_%=",
+                    f"s_addc_u32 s{reg + 1}, s{GPC + 1}, 0"]
+    pro += [f"s_mov_b32 s{T0 + 2 * i + 1}, %[thi]" for i in range(4)]
+    pro += [f"s_mov_b32 s{H2 + 2 * i + 1}, %[thi]" for i in range(4)]
+    pro += [f"v_mov_b32 v{PL}, %[pl]", f"ds_read_b32 v{PG}, v{PL}", f"ds_read_b32 v{PGN}, v{PL} offset:256",
+            f"v_add_u32_e32 v{PL}, 512, v{PL}"]
     pro += [f"v_mov_b32 v{ACC + r}, 0" for r in range(64)]
-    loop = []
-    for slot in range(P):
-        loop += row(slot, 2 * (P - 1), True)
-    tail = []
-    for slot in range(P):
-        tail += row(slot, 2 * (P - 1 - slot), False)
-    red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
-    # tuning variants (KODR_TUNE_MODES builds only): rows without body dispatch
-    loop_nd, tail_nd = [], []
-    for slot in range(P):
-        loop_nd += row(slot, 2 * (P - 1), True, False)
-        tail_nd += row(slot, 2 * (P - 1 - slot), False, False)
-    loop_nl, loop_nl2, loop_nl3 = [], [], []
-    for slot in range(P):
-        loop_nl += row(slot, 2 * (P - 1), False, False)
-        loop_nl2 += row(slot, 2 * (P - 1), False, False, rfl=False)
-        loop_nl3 += row(slot, 2 * (P - 1), False, False, rfl=False, prog=False)
-    return [("KODR_BS_PROLOGUE", pro), ("KODR_BS_LOOP", loop), ("KODR_BS_TAIL", tail),
-            ("KODR_BS_REDUCE", red), ("KODR_BS_LOOP_ND", loop_nd), ("KODR_BS_TAIL_ND", tail_nd),
-            ("KODR_BS_LOOP_NL", loop_nl), ("KODR_BS_LOOP_NL2", loop_nl2), ("KODR_BS_LOOP_NL3", loop_nl3)]
+    pro += [f"s_mov_b32 s{CNT}, %[ngrp]"]
+    return pro
+
+
+def main_loop(dispatch=True, loads=True):
+    """Prologue, the shared stub (branched over) and the 8-row loop; the
+    ring's first P rows arrive as asm operands (loaded by the compiler before
+    the program build).  At the end of each iteration the next chunk moves
+    into v[PG] and the one after is requested."""
+    t = prologue_lines(dispatch)
+    if dispatch:
+        t += ["s_branch .Lloop_%="] + stub_lines()
+    t += [".Lloop_%=:"]
+    for j in range(8):
+        t += row_lines(j, dispatch, loads)
+    t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
+          f"v_add_u32_e32 v{PL}, 256, v{PL}"]
+    t += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_lg_u32 s{CNT}, 0", "s_cbranch_scc1 .Lloop_%="]
+    return t
+
+
+def dump_lines():
+    """Bring-up only (MODE 9): the prologue and the first row's target reads,
+    then s[60:99] and M0 stored to %[ydbg] (lane 0's values), no jump taken."""
+    t = prologue_lines(True) + ["s_waitcnt lgkmcnt(0)"]
+    t += [f"v_readlane_b32 s{T0 + 2 * m}, v{PG}, {m}" for m in range(4)]
+    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {4 + m}" for m in range(4)]
+    t += [f"v_mov_b32 v{ACC + 1}, 0"]
+    for i, sg in enumerate(list(range(T0, CNT + 1)) + ["m0"]):
+        src = f"s{sg}" if sg != "m0" else "m0"
+        t += [f"v_mov_b32 v{ACC}, {src}",
+              f"global_store_dword v{ACC + 1}, v{ACC}, %[ydbg] offset:{4 * i}"]
+    t += ["s_waitcnt vmcnt(0)"]
+    t += [".Lstub_%=:"] + [f".Lret{j}_%=:" for j in range(8)]   # never jumped to
+    return t
 
 
 def emit(name, lines):
     res = [f"#define {name} \\"]
-    res += [f'  "{l}\\n\\t" \\' for l in lines]
+    res += [f'  "{ln}\\n\\t" \\' for ln in lines]
     res.append('  ""')
     return res
 
 
 def main():
     out = ["// generated by gen_bs_bodies.py -- do not edit",
-           f"// accumulators v[{ACC}..{ACC + 63}] (indexed), XOR tables v[{TL0}..{TH0 + 14}],",
-           f"// row ring v[{RING}..{VMAX - 1}], return s[{RET}:{RET + 1}]",
+           f"// accumulators v[{ACC}..{ACC + 63}] (copy r: v[{ACC}+8r..], +32 under index mode),",
+           f"// XOR tables v[{TL0}..{TH0 + 14}], row ring v[{RING}..{RING + 8 * P - 1}], "
+           f"program chunks v[{PG}..{VMAX - 1}]",
            f"#define KODR_BS_VMAX {VMAX}",
-           f"#define KODR_BS_P {P}"]
-    # the ring rows enter the asm as in/out operands pinned to their slots
+           f"#define KODR_BS_P {P}",
+           f"#define KODR_BS_NCOPY {NCOPY}"]
     ops = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
     out.append("#define KODR_BS_RING_OPERANDS " + ", ".join(ops))
     bodies = []
     n_inst = 0
-    for c in range(256):
-        bodies.append(f".Lbs_b{c}_%=:")
-        lines = body_lines(c)
-        n_inst += len(lines) - 1
-        bodies += lines
+    for r in range(NCOPY):
+        for c in range(256):
+            bodies.append(f".Lbs_b{r}_{c}_%=:")
+            lines = body_lines(c, r)
+            n_inst += len(lines) - 1
+            bodies += lines
     out += emit("KODR_BS_BODIES", bodies)
-    # export: offsets of every body from body 0, stored by lane-uniform global
-    # stores to SOUT + 4c (used once per process, checked against body_bytes)
-    out.append("#define KODR_BS_EXPORT(VTMP, VZERO, SOUT) \\")
-    for c in range(256):
-        out.append(f'  "v_mov_b32 " VTMP ", .Lbs_b{c}_%= - .Lbs_b0_%=\\n\\t" \\')
-        out.append(f'  "global_store_dword " VZERO ", " VTMP ", " SOUT " offset:{4 * c}\\n\\t" \\')
+    offs, total = body_offsets()
+    out.append(f"#define KODR_BS_CODE_BYTES {total}")
+    out.append(f"#define KODR_BS_COPY_BYTES {total // NCOPY}u")
+    out.append("static const uint32_t kBsBodyOffsets[%d] = {" % len(offs))
+    for i in range(0, len(offs), 16):
+        out.append("  " + ", ".join(str(o) for o in offs[i:i + 16]) + ",")
+    out.append("};")
+    # export: the absolute address of body (0, 0) (s_getpc) and every body's
+    # offset from it, stored by lane-uniform global stores (once per process,
+    # checked against kBsBodyOffsets)
+    out.append("#define KODR_BS_EXPORT(VTMP, VZERO, VOFF, SOUT) \\")
+    out.append('  "s_getpc_b64 s[88:89]\\n\\t" \\')
+    out.append('  ".Lexpc_%=:\\n\\t" \\')
+    # the bodies precede the export code: subtract with borrow (an add of the
+    # negative difference would carry into the hi word)
+    out.append('  "s_sub_u32 s88, s88, .Lexpc_%= - .Lbs_b0_0_%=\\n\\t" \\')
+    out.append('  "s_subb_u32 s89, s89, 0\\n\\t" \\')
+    out.append(f'  "v_mov_b32 " VOFF ", {4 * NCOPY * 256}\\n\\t" \\')
+    out.append('  "v_mov_b32 " VTMP ", s88\\n\\t" \\')
+    out.append('  "global_store_dword " VOFF ", " VTMP ", " SOUT "\\n\\t" \\')
+    out.append('  "v_mov_b32 " VTMP ", s89\\n\\t" \\')
+    out.append('  "global_store_dword " VOFF ", " VTMP ", " SOUT " offset:4\\n\\t" \\')
+    for r in range(NCOPY):
+        for c in range(256):
+            i = r * 256 + c
+            out.append(f'  "v_mov_b32 " VTMP ", .Lbs_b{r}_{c}_%= - .Lbs_b0_0_%=\\n\\t" \\')
+            out.append(f'  "global_store_dword " VZERO ", " VTMP ", " SOUT " offset:{4 * i}\\n\\t" \\')
     out.append('  "s_waitcnt vmcnt(0)\\n\\t"')
-    for name, lines in main_loop():
-        out += emit(name, lines)
+    out += emit("KODR_BS_MAIN", main_loop(True))
+    out += emit("KODR_BS_MAIN_ND", main_loop(False))
+    out += emit("KODR_BS_MAIN_NL", main_loop(True, False))
+    out += emit("KODR_BS_MAIN_NDNL", main_loop(False, False))
+    out += emit("KODR_BS_DUMP", dump_lines())
+    red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
+    out += emit("KODR_BS_REDUCE", red)
     # the ring v[RING..RING+8P) is bound to in/out operands, not clobbered
     clob = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, VMAX))]
-    clob += [f'"s{r}"' for r in list(range(40, 46)) + list(range(50, 61)) + [72, 74, 75]]
+    assert CNT <= 101 and GPC + 1 < T0
+    clob += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
     out.append("#define KODR_BS_CLOBBERS " + ", ".join(clob) + ', "scc", "memory"')
-    out.append(f"// {n_inst} body instructions, {n_inst / 256:.2f} per coefficient; "
-               f"row prep {len(table_lines(0))} per row")
+    out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "
+               f"row prep {len(table_lines(0))} per row; {total} bytes of bodies")
     print("\n".join(out))
 
 

@@ -12,18 +12,21 @@
 // for the 3x v_perm lookup formulation of gf_gemm_kernel.
 //
 // Code.  The XOR pattern depends on c, which is wave-uniform, so each of the
-// 256 patterns is a straight-line body (generated: gen_bs_bodies.py) and the
-// wave jumps to body[c] with s_swappc_b64.  The bodies address the 8
-// accumulator planes through VGPR index mode, so one body serves all 8 output
-// rows of a wave (index 8m).  No LDS tables, no lookups, no per-lane branches.
+// 256 patterns is a straight-line body (generated: gen_bs_bodies.py).  The
+// bodies are threaded: 4 copies, copy r XORing into accumulator set r and
+// ending with a jump to the next output row's body, so the 8 coefficients of
+// an input row cost 8 bodies and one taken branch each (rows 4..7 reuse the
+// copies under VGPR index mode).  They live in gf_bs_export_kernel, which
+// exports their addresses once; no LDS tables, no lookups, no per-lane
+// branches.
 //
 // Work split.  A wave owns 8 output rows x 64 blocks (2 KiB of columns) x a
 // range of at most rpw input rows; the KW waves of a workgroup split K and are
-// XOR-reduced in LDS.  Per wave, the body offsets for its (row, k) pairs are
-// built once into LDS ("program") and moved to SGPRs with v_readfirstlane, one
-// row ahead.  X rows stream through a P-deep register ring of buffer loads
-// (rows >= K are outside num_records and read as zero); the first P are in
-// flight while the program is built.
+// XOR-reduced in LDS.  Per wave, the absolute body targets for its (row, k)
+// pairs are built once into LDS ("program") and moved to SGPRs with
+// v_readfirstlane within the row.  X rows stream through a P-deep register
+// ring of buffer loads (rows past the wave's range are outside num_records and
+// read as zero); the first P are in flight while the program is built.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,6 +46,7 @@ namespace {
 constexpr int kBsRows = 8;     // output rows per wave
 constexpr int kBsBlock = 32;   // bytes per bit-sliced block
 constexpr int kBsWaveCols = 64 * kBsBlock;
+constexpr int kBsChunk = 8;    // input rows per program chunk (one VGPR of targets)
 
 // 8x8 bit-matrix transpose inside each byte lane of 8 dwords: afterwards
 // dword i holds bit i of all 32 bytes.  Self-inverse.
@@ -81,72 +85,50 @@ __global__ __launch_bounds__(256) void bitslice_kernel(uint8_t* __restrict__ X, 
   p[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
-// Writes the 256 body offsets (bytes from body 0) to offs; run once per device.
-__global__ __launch_bounds__(64) void gf_bs_export_kernel(uint32_t* offs) {
+// The bodies' only home: this kernel exports the absolute address of body
+// (0, 0) and every body's offset from it (out[i] for body i = copy * 256 + c,
+// out[1024] lo, out[1025] hi) and never runs them; gf_bs_kernel jumps here.
+__global__ __launch_bounds__(64) void gf_bs_export_kernel(uint32_t* out) {
   asm volatile(
       "s_branch .Lexp_%=\n\t"
       KODR_BS_BODIES
       ".Lexp_%=:\n\t"
-      KODR_BS_EXPORT("v24", "%[z]", "%[out]")
+      KODR_BS_EXPORT("v24", "%[z]", "v25", "%[out]")
       :
-      : [z] "v"(0u), [out] "s"(offs)
-      : "v24", "memory");
+      : [z] "v"(0u), [out] "s"(out)
+      : "v24", "v25", "s88", "s89", "memory");
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// The main loop (gen_bs_bodies.py).  The ring operands pin the 4 prefetched
-// rows to v[RING..RING+31], where the generated row code expects them.
-#define KODR_BS_ASM(LOOP, TAIL)                                                          \
-  asm volatile(                                                                          \
-      "s_mov_b32 s40, %[xlo]\n\t"                                                        \
-      "s_and_b32 s41, %[xhi], 0xffff\n\t"                                                \
-      "s_mov_b32 s42, %[nrec]\n\t"                                                       \
-      "s_mov_b32 s43, 0x00020000\n\t"                                                    \
-      "s_mov_b32 s44, %[roff]\n\t"                                                       \
-      "s_mov_b32 s45, %[ldx]\n\t"                                                        \
-      "s_getpc_b64 s[74:75]\n\t"                                                         \
-      ".Lpc_%=:\n\t"                                                                     \
-      "s_add_u32 s50, s74, .Lbs_b0_%= - .Lpc_%=\n\t"                                     \
-      "s_addc_u32 s51, s75, 0\n\t"                                                       \
-      KODR_BS_PROLOGUE                                                                   \
-      "s_mov_b32 s72, %[ngrp]\n\t"                                                       \
-      "s_cmp_eq_u32 s72, 0\n\t"                                                          \
-      "s_cbranch_scc1 .Ltail_%=\n\t"                                                     \
-      ".Lloop_%=:\n\t"                                                                   \
-      LOOP                                                                               \
-      "s_sub_u32 s72, s72, 1\n\t"                                                        \
-      "s_cmp_lg_u32 s72, 0\n\t"                                                          \
-      "s_cbranch_scc1 .Lloop_%=\n\t"                                                     \
-      ".Ltail_%=:\n\t"                                                                   \
-      TAIL                                                                               \
-      KODR_BS_REDUCE /* this wave's 64 accumulator planes into the LDS sums */           \
-      "s_waitcnt lgkmcnt(0)\n\t"                                                         \
-      "s_branch .Lend_%=\n\t"                                                            \
-      KODR_BS_BODIES                                                                     \
-      ".Lend_%=:\n\t"                                                                    \
-      : KODR_BS_RING_OPERANDS                                                            \
-      : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx), \
-        [ngrp] "s"(ngrp), [col] "v"(col), [lds] "v"((uint32_t)lane * 4u), [pl] "v"(pl)    \
-      : KODR_BS_CLOBBERS)
-
-
-// MODE (tuning builds only, -DKODR_TUNE_MODES): 1 = every program entry is the
-// empty body (dispatch without XOR work), 2 = as 1 without reading A, 3 = no
-// dispatch at all (row stream + table prep + reduction only), 4 = as 3 without
-// the row stream, 5 = no main loop (prologue, reduction and store only).
+// MODE (tuning builds only, -DKODR_TUNE_MODES): 3 = the row stream, table
+// prep and program reads without dispatching bodies, 4 = as 3 without the
+// row stream, 5 = no main loop (prologue, reduction and store only), 6 = the
+// full loop without the row stream (stale rows), 8 = s_memtime timeline,
+// 9 = register dump before the first jump.
 template <int KW, int MODE = 0>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
-    const uint32_t* __restrict__ offs) {
+    const uint32_t* __restrict__ tgt, uint32_t thi) {
   // LDS: [0, 16 KiB) per-row XOR sums [8 rows x 8 planes][64 lanes];
-  // [16, 17 KiB) the body offset table; then each wave's program, rpw x 8
-  // 16-bit body offsets (the bodies span < 64 KiB)
+  // [16, 17 KiB) the body target table (absolute lo words of copy 0; copy r
+  // is r * KODR_BS_COPY_BYTES further); then each wave's program: per input
+  // row the targets of output rows 0..7
   extern __shared__ uint32_t lds[];
+  uint64_t stamp[4] = {0, 0, 0, 0};  // MODE 8: s_memtime per phase (timeline)
+  if constexpr (MODE == 8) stamp[0] = __builtin_amdgcn_s_memtime();
+  if (ncols < 0) {  // bs_init's cross-check: where this kernel's code runs
+    const uint64_t pc = __builtin_amdgcn_s_getpc();
+    if (threadIdx.x == 0) {
+      reinterpret_cast<uint32_t*>(Y)[0] = (uint32_t)pc;
+      reinterpret_cast<uint32_t*>(Y)[1] = (uint32_t)(pc >> 32);
+    }
+    return;
+  }
   uint32_t* red = lds;
-  uint32_t* offs_l = lds + 64 * 64;
-  uint16_t* prog_l = reinterpret_cast<uint16_t*>(offs_l + 256);
+  uint32_t* tgt_l = lds + 64 * 64;
+  uint32_t* prog_l = tgt_l + 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware order: the nrg row groups of one column chunk go to blocks
   // b, b+8, ... (one XCD) and re-read that chunk from its L2.  Speed only.
@@ -155,32 +137,36 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const int cx = (b / (8 * nrg)) * 8 + (b & 7);
   if (cx >= ncx) return;
   const int m0 = rg * kBsRows, kb = w * rpw;
-  // this wave's input rows: [kb, kb + nr), nr a multiple of the ring depth P
-  // (rows >= K read zero)
-  const int kpad = (K + KODR_BS_P - 1) / KODR_BS_P * KODR_BS_P;
+  // this wave's input rows: [kb, kb + nr), nr a multiple of the 8-row
+  // program chunk (rows >= K read zero and have coefficient 0)
+  const int kpad = (K + kBsChunk - 1) / kBsChunk * kBsChunk;
   const int nr = __builtin_amdgcn_readfirstlane(max(0, min(rpw, kpad - kb)));
 
   // Prologue loads in retirement order (vmcnt counts in issue order): the
-  // offset table and this wave's first 512 coefficients, then the ring's first
-  // 4 rows, so the program build waits only for the former while the rows'
-  // HBM latency overlaps it (rows >= K are outside num_records: zeros).
+  // target table and this wave's first 512 coefficients, then the ring's
+  // first rows, so the program build waits only for the former while the
+  // rows' HBM latency overlaps it.
   const int ne = nr * kBsRows;
   auto coef = [&](int e) -> uint32_t {
     const int k = kb + (e >> 3), row = m0 + (e & 7);
-    return (MODE < 2 && e < ne && k < K && row < M) ? (uint32_t)A[(size_t)row * lda + k] : 0u;
+    return (e < ne && k < K && row < M) ? (uint32_t)A[(size_t)row * lda + k] : 0u;
   };
-  uint32_t ot[(256 + 63) / 64];
+  constexpr int kTgt = 256;
+  uint32_t ot[(kTgt + 63) / 64];
 #pragma unroll
-  for (int j = 0; j < (256 + 63) / 64; j++) {
+  for (int j = 0; j < (kTgt + 63) / 64; j++) {
     const int i = tid + j * 64 * KW;
-    ot[j] = i < 256 ? offs[i] : 0u;
+    ot[j] = i < kTgt ? tgt[i] : 0u;
   }
   uint32_t c[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
 
   const uint32_t col = (uint32_t)(cx * 64 + lane) * kBsBlock;
-  const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)K * (uint32_t)ldx);
+  // rows past this wave's range read zero, so the look-ahead loads of its
+  // last P rows move no data
+  const uint32_t kend = (uint32_t)max(0, min(K, kb + nr));
+  const uint32_t nrec = __builtin_amdgcn_readfirstlane(kend * (uint32_t)ldx);
   const uint32_t sldx = __builtin_amdgcn_readfirstlane((uint32_t)ldx);
   const uint32_t kboff = __builtin_amdgcn_readfirstlane((uint32_t)kb * (uint32_t)ldx);
   const __amdgpu_buffer_rsrc_t xr =
@@ -195,14 +181,15 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   }
 
 #pragma unroll
-  for (int j = 0; j < (256 + 63) / 64; j++) {
+  for (int j = 0; j < (kTgt + 63) / 64; j++) {
     const int i = tid + j * 64 * KW;
-    if (i < 256) offs_l[i] = ot[j];
+    if (i < kTgt) tgt_l[i] = ot[j];
   }
   for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
   __syncthreads();
-  // program: body offset for (row m0 + e%8, input row kb + e/8), in LDS
-  uint16_t* wp = prog_l + w * rpw * kBsRows;
+  // program: entry e = the target of (output row m0 + e%8, input row kb + e/8):
+  // body c in copy (e%8) & 3
+  uint32_t* wp = prog_l + w * rpw * kBsRows;
   for (int e0 = 0; e0 < ne; e0 += 64 * 8) {
     if (e0) {
 #pragma unroll
@@ -211,30 +198,54 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       const int e = e0 + j * 64 + lane;
-      if (e < ne) wp[e] = (uint16_t)offs_l[MODE == 0 ? c[j] : 0u];
+      if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)(e & 3) * KODR_BS_COPY_BYTES;
     }
   }
   __syncthreads();
 
-  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / KODR_BS_P - 1));
+  const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / kBsChunk));
   const uint64_t xa = reinterpret_cast<uint64_t>(X);
   const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
   const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
   const uint32_t roff = kboff + KODR_BS_P * sldx;  // the asm streams from row kb + P
-  const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp));  // LDS byte address
+  // this lane's program word in LDS (chunk lane 8j + m: row j, output row m)
+  const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp)) + (uint32_t)lane * 4u;
+  const uint32_t sthi = __builtin_amdgcn_readfirstlane(thi);
+  if constexpr (MODE == 8) stamp[1] = __builtin_amdgcn_s_memtime();
+#define KODR_BS_ASM(MAIN)                                                                           \
+  asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"                                       \
+               : KODR_BS_RING_OPERANDS                                                              \
+               : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx),  \
+                 [ngrp] "s"(ngrp), [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)lane * 4u),   \
+                 [pl] "v"(pl), [ydbg] "s"(Y)                                                        \
+               : KODR_BS_CLOBBERS)
   if (nr > 0 && MODE != 5) {
-    if constexpr (MODE == 3) {
-      KODR_BS_ASM(KODR_BS_LOOP_ND, KODR_BS_TAIL_ND);
+    if constexpr (MODE == 9) {
+      if (blockIdx.x == 0 && w == 0) {
+        KODR_BS_ASM(KODR_BS_DUMP);
+        uint32_t* yd = reinterpret_cast<uint32_t*>(Y) + 64;
+        if (lane == 0) {
+          yd[0] = pl;
+          for (int i = 0; i < 16; i++) yd[1 + i] = wp[i];
+          for (int i = 0; i < 8; i++) yd[17 + i] = tgt_l[i];
+          for (int i = 0; i < 4; i++) yd[25 + i] = tgt[i];
+          yd[29] = (uint32_t)ne;
+          yd[30] = (uint32_t)c[0];
+        }
+      }
+      return;
+    } else if constexpr (MODE == 3) {
+      KODR_BS_ASM(KODR_BS_MAIN_ND);
     } else if constexpr (MODE == 4) {
-      KODR_BS_ASM(KODR_BS_LOOP_NL, KODR_BS_TAIL_ND);
+      KODR_BS_ASM(KODR_BS_MAIN_NDNL);
     } else if constexpr (MODE == 6) {
-      KODR_BS_ASM(KODR_BS_LOOP_NL2, KODR_BS_TAIL_ND);
-    } else if constexpr (MODE == 7) {
-      KODR_BS_ASM(KODR_BS_LOOP_NL3, KODR_BS_TAIL_ND);
+      KODR_BS_ASM(KODR_BS_MAIN_NL);
     } else {
-      KODR_BS_ASM(KODR_BS_LOOP, KODR_BS_TAIL);
+      KODR_BS_ASM(KODR_BS_MAIN);
     }
   }
+#undef KODR_BS_ASM
+  if constexpr (MODE == 8) stamp[2] = __builtin_amdgcn_s_memtime();
   __syncthreads();
 
   // rows m0..m0+7 of this column chunk: planes -> bytes, store
@@ -255,53 +266,106 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       for (int i = 0; cc + i < ncols; i++) dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
     }
   }
+  if constexpr (MODE == 8) {  // timeline build: stamps past the M output rows (the caller sizes Y)
+    __syncthreads();
+    stamp[3] = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      uint64_t* t = reinterpret_cast<uint64_t*>(Y + (size_t)M * ldy) + ((size_t)blockIdx.x * KW + w) * 5;
+      for (int i = 0; i < 4; i++) t[i] = stamp[i];
+      t[4] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 struct BsDevice {
-  uint32_t* offs = nullptr;
-  bool ready = false;
+  uint32_t* tgt = nullptr;  // absolute lo words of the 256 bodies of copy 0
+  uint32_t thi = 0;         // their common hi word
+  uint32_t offs[256 * KODR_BS_NCOPY] = {};
+  bool ready = false, ok = false;
 };
 std::mutex g_bs_mu;
 BsDevice g_bs[64];
 
-hipError_t bs_offsets(int dev, const uint32_t** out) {
+// Once per device: export the bodies' addresses, check them against the
+// generator's layout and that all share one hi word (the kernel jumps to
+// hi:lo with a fixed hi).  ok = false leaves the bit-sliced path unused
+// (callers fall back to gf_gemm); the error return is for HIP failures.
+hipError_t bs_init(int dev, const BsDevice** out) {
   std::lock_guard<std::mutex> lk(g_bs_mu);
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   BsDevice& d = g_bs[dev];
   if (!d.ready) {
-    hipError_t e = hipMalloc((void**)&d.offs, 256 * sizeof(uint32_t));
+    constexpr int n = 256 * KODR_BS_NCOPY;
+    uint32_t* buf = nullptr;
+    hipError_t e = hipMalloc((void**)&buf, (n + 2) * sizeof(uint32_t));
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(gf_bs_export_kernel, dim3(1), dim3(64), 0, 0, d.offs);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
-    // the program stores offsets as 16 bits: the bodies must span < 64 KiB
-    uint32_t h[256];
-    if ((e = hipMemcpy(h, d.offs, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
-    for (int c = 1; c < 256; c++)
-      if (h[c] <= h[c - 1] || h[c] > 0xFFFFu) return hipErrorInvalidImage;
+    hipLaunchKernelGGL(gf_bs_export_kernel, dim3(1), dim3(64), 0, 0, buf);
+    if ((e = hipGetLastError()) == hipSuccess) e = hipDeviceSynchronize();
+    static uint32_t h[n + 2];
+    if (e == hipSuccess) e = hipMemcpy(h, buf, sizeof(h), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      (void)hipFree(buf);
+      return e;
+    }
+    const uint64_t base = (uint64_t)h[n] | ((uint64_t)h[n + 1] << 32);
+    // the bodies and gf_bs_kernel are in one code object: a base far from
+    // where gf_bs_kernel runs means the export is wrong, and jumping there
+    // would fault
+    hipLaunchKernelGGL((gf_bs_kernel<1, 0>), dim3(1), dim3(64), 0, 0, nullptr, 0, 0, 0, nullptr, 0,
+                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u);
+    if ((e = hipGetLastError()) == hipSuccess) e = hipDeviceSynchronize();
+    uint32_t kpc[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpy(kpc, buf, sizeof(kpc), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      (void)hipFree(buf);
+      return e;
+    }
+    const uint64_t kernel_pc = (uint64_t)kpc[0] | ((uint64_t)kpc[1] << 32);
+    const uint64_t dist = kernel_pc > base ? kernel_pc - base : base - kernel_pc;
+    bool ok = dist < ((uint64_t)64 << 20) && (base >> 32) == ((base + KODR_BS_CODE_BYTES) >> 32);
+    for (int i = 0; i < n; i++) {
+      d.offs[i] = h[i];
+      ok = ok && h[i] == kBsBodyOffsets[i] && h[i] == d.offs[i % 256] + (uint32_t)(i / 256) * KODR_BS_COPY_BYTES;
+      h[i] = (uint32_t)(base + h[i]);
+    }
+    if (ok) e = hipMemcpy(buf, h, 256 * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess || !ok) {
+      (void)hipFree(buf);
+      buf = nullptr;
+    }
+    if (e != hipSuccess) return e;
+    d.tgt = buf;
+    d.thi = (uint32_t)(base >> 32);
+    d.ok = ok;
     d.ready = true;
   }
-  *out = d.offs;
+  *out = &d;
   return hipSuccess;
 }
 
 template <int KW, int MODE = 0>
 hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, int ldx, uint8_t* Y,
-                     size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes,
-                     const uint32_t* offs, hipStream_t st) {
+                     size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes, const BsDevice* bd,
+                     hipStream_t st) {
   const int nb = (ncx + 7) / 8 * 8 * nrg;
   hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
-                     ldy, ncols, rpw, ncx, nrg, offs);
+                     ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi);
   return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t bs_body_offsets(int device, uint32_t* host_out) {
-  const uint32_t* offs = nullptr;
-  hipError_t e = bs_offsets(device, &offs);
+  const BsDevice* bd = nullptr;
+  hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;
-  return hipMemcpy(host_out, offs, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  for (int c = 0; c < 256; c++) host_out[c] = bd->offs[c];
+  return hipSuccess;
+}
+
+bool bs_ready(int device) {
+  const BsDevice* bd = nullptr;
+  return bs_init(device, &bd) == hipSuccess && bd->ok;
 }
 
 hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hipStream_t stream) {
@@ -323,7 +387,10 @@ constexpr int kBsWavesPerSimd = 512 / ((KODR_BS_VMAX + 7) / 8 * 8);
 constexpr int kBsKw[] = {1, 2, 3, 4, 6, 8, 16};
 constexpr size_t kLdsPerCu = 160 * 1024;
 
-size_t bs_lds_bytes(int kw, int rpw) { return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 2; }
+// row sums, the body target table, and KW programs of rpw rows x 8 targets
+size_t bs_lds_bytes(int kw, int rpw) {
+  return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4;
+}
 
 }  // namespace
 
@@ -332,7 +399,7 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
   p.nrg = (int)((M + kBsRows - 1) / kBsRows);
   const long tasks = (long)p.ncx * p.nrg;
-  constexpr long P = KODR_BS_P;
+  constexpr long P = kBsChunk;  // rows per wave: whole program chunks
   const long kpad = ((long)K + P - 1) / P * P;
   // cost model in row-units: rounds of resident waves x (rows per wave + the
   // per-wave fixed cost of program build, reduction and store, ~6 rows)
@@ -367,9 +434,10 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     return hipErrorInvalidValue;
   const BsPlan p = plan_gemm_bs(M, K, ncols);
   if (!p.ok) return hipErrorInvalidValue;
-  const uint32_t* offs = nullptr;
-  hipError_t e = bs_offsets(device, &offs);
+  const BsDevice* bd = nullptr;
+  hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;
+  if (!bd->ok) return hipErrorNotSupported;
   const int iM = (int)M, iK = (int)K, ild = (int)lda, ilx = (int)ldx, inc = (int)ncols;
   int mode = 0;
   (void)mode;
@@ -377,14 +445,13 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   if (const char* env = getenv("KODR_BS_MODE")) mode = atoi(env);
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
-  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, offs, stream)
+  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream)
 #ifdef KODR_TUNE_MODES
 #define KODR_BS_CASE(KW_)                                                                         \
   case KW_:                                                                                       \
-    return mode == 1 ? KODR_BS_CALL(KW_, 1) : mode == 2 ? KODR_BS_CALL(KW_, 2)                    \
-         : mode == 3 ? KODR_BS_CALL(KW_, 3) : mode == 4 ? KODR_BS_CALL(KW_, 4)                    \
-         : mode == 5 ? KODR_BS_CALL(KW_, 5) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
-         : mode == 7 ? KODR_BS_CALL(KW_, 7) : KODR_BS_CALL(KW_, 0);
+    return mode == 3 ? KODR_BS_CALL(KW_, 3) : mode == 5 ? KODR_BS_CALL(KW_, 5)                    \
+         : mode == 4 ? KODR_BS_CALL(KW_, 4) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
+         : mode == 8 ? KODR_BS_CALL(KW_, 8) : mode == 9 ? KODR_BS_CALL(KW_, 9) : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

@@ -36,8 +36,12 @@ hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t
 // becomes 8 bit planes (self-inverse).  ldx multiple of 32.
 hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hipStream_t stream);
 
-// byte offsets of the 256 coefficient bodies from body 0 (diagnostics)
+// byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);
+
+// true once the bodies' addresses were exported and checked on this device
+// (the bit-sliced path is usable); false sends callers to gf_gemm
+bool bs_ready(int device);
 
 struct BsPlan {
   int ncx = 0, nrg = 0, kw = 1, rpw = 8, blocks = 0;

@@ -34,6 +34,11 @@ def ring_shift(send, recv, group=None):
     if ws == 1:
         recv.copy_(send)
         return
+    if send.is_cuda and dist.get_backend(group) == "gloo":   # CPU-transport rehearsal
+        s, r = send.cpu(), recv.cpu()
+        ring_shift(s, r, group)
+        recv.copy_(r)
+        return
     ops = [dist.P2POp(dist.isend, send, (rank + 1) % ws, group),
            dist.P2POp(dist.irecv, recv, (rank - 1) % ws, group)]
     for r in dist.batch_isend_irecv(ops):
@@ -46,6 +51,8 @@ def max_over_ranks(value, device=None):
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() == "gloo":
+        device = None
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -53,12 +53,18 @@ def run(lines, regs, idx=0):
 
 
 def test_body_sizes_match_offsets():
-    off = 0
-    for c in range(256):
-        assert len(gen.body_ops(c)) <= 8
-        assert gen.body_bytes(c) == 8 * len(gen.body_ops(c)) + 4
-        off += gen.body_bytes(c)
-    assert off < 0xFFFF    # the LDS program stores 16-bit offsets
+    offs, total = gen.body_offsets()
+    assert len(offs) == 256 * gen.NCOPY
+    for r in range(gen.NCOPY):
+        for c in range(256):
+            assert len(gen.body_ops(c)) <= 8
+            assert gen.body_bytes(c) == 8 * len(gen.body_ops(c)) + 4
+            nxt = offs[r * 256 + c + 1] if r * 256 + c + 1 < len(offs) else total
+            assert nxt - offs[r * 256 + c] == gen.body_bytes(c)
+    # every copy is laid out identically, and all of them stay within what the
+    # instruction cache holds (tools/probe/dispatch.py: 4 copies fit, 8 thrash)
+    assert all(offs[r * 256 + c] - offs[r * 256] == offs[c] for r in range(gen.NCOPY) for c in range(256))
+    assert total < 72 * 1024
 
 
 def test_registers_fit_four_waves():
@@ -66,8 +72,8 @@ def test_registers_fit_four_waves():
     assert gen.TL0 % 2 == 0 and gen.TH0 % 2 == 0 and gen.RING % 2 == 0   # v_pk_mov pairs
     used = set(range(gen.ACC, gen.ACC + 64)) | set(range(gen.TL0, gen.TL0 + 15)) | \
         set(range(gen.TH0, gen.TH0 + 15)) | set(range(gen.RING, gen.RING + 8 * gen.P)) | \
-        set(range(gen.PR, gen.PR + 4)) | {gen.PL}
-    assert len(used) == 64 + 30 + 8 * gen.P + 5          # no overlaps
+        {gen.PG, gen.PGN, gen.PL}
+    assert len(used) == 64 + 30 + 8 * gen.P + 3          # no overlaps
 
 
 def test_every_coefficient_body_vs_oracle():
@@ -98,3 +104,147 @@ def test_bitslice_model_is_an_involution_and_plane_layout():
     blk[17] = 1 << 5
     planes = bitslice_np(blk).view(np.uint32)
     assert [i for i in range(8) if planes[i]] == [5]
+
+
+class _Wave:
+    """Model of the generated main loop + threaded bodies: every SALU, VALU,
+    LDS and buffer instruction the generator emits, with PC-level control flow
+    (s_setpc to absolute addresses, labels, branches), VGPR index mode, and
+    64-lane program chunks (v_readlane); data planes are modelled for one
+    lane.  Checks the dispatch plumbing (targets, stub, returns, M0, program
+    chunks) end to end on CPU, before any GPU run."""
+
+    BASE = 0x7F12_3456_0000
+    VEC = (gen.PG, gen.PGN, gen.PL)                # registers modelled per lane
+
+    def __init__(self, X, A, nr):
+        self.X, self.A, self.nr = X, A, nr          # X: nr x 32 bytes, A: 8 x nr
+        offs, _ = gen.body_offsets()
+        self.code, self.addr = [], {}
+        for r in range(gen.NCOPY):
+            for c in range(256):
+                self.addr[self.BASE + offs[r * 256 + c]] = len(self.code)
+                self.code += gen.body_lines(c, r)
+        self.main0 = len(self.code)
+        self.code += [ln.replace("_%=", "") for ln in gen.main_loop(True)] + ["END"]
+        self.labels = {ln[:-1]: i for i, ln in enumerate(self.code) if ln.endswith(":")}
+        for name, i in self.labels.items():          # main code at fake addresses
+            self.addr[0x1000_0000 + 4 * i] = i
+        self.s, self.v = {}, {}
+        self.m0, self.idx_on = 0, False
+        # LDS program: per row 8 absolute lo targets, body c in copy m & 3
+        self.lds = {}
+        pl = 0x400
+        for k in range(nr):
+            for m in range(8):
+                c = int(A[m, k])
+                self.lds[pl + 4 * (8 * k + m)] = (self.BASE + offs[(m & 3) * 256 + c]) & 0xFFFFFFFF
+        self.ops = {"xlo": 0, "xhi": 0, "nrec": nr * 32, "roff": gen.P * 32, "ldx": 32, "ngrp": nr // 8,
+                    "thi": self.BASE >> 32, "col": 0}
+        self.pl_lanes = [pl + 4 * lane for lane in range(64)]
+        for slot in range(gen.P):                      # the compiler's ring prologue
+            self._load_row(gen.RING + 8 * slot, slot * 32)
+
+    def _load_row(self, vb, off, half=None):
+        row = off // 32
+        planes = bitslice_np(self.X[row]).view(np.uint32) if row < self.nr else np.zeros(8, np.uint32)
+        for i in range(8):
+            if half is None or i // 4 == half:
+                self.v[vb + i] = int(planes[i])
+
+    def val(self, tok):
+        if tok.startswith("%["):
+            return self.ops[tok[2:-1]]
+        if tok.startswith("s"):
+            return self.s[int(tok[1:])]
+        return int(tok, 0)
+
+    def run(self):
+        pc, steps = self.main0, 0
+        while self.code[pc] != "END":
+            steps += 1
+            assert steps < 400000
+            ln = self.code[pc]
+            pc += 1
+            if ln.endswith(":"):
+                continue
+            op, _, rest = ln.partition(" ")
+            a = [t.strip() for t in rest.split(",")]
+            r = [int(x) for x in re.findall(r"v\[?(\d+)", ln)]
+            if op == "s_getpc_b64":
+                self.s[gen.GPC], self.s[gen.GPC + 1] = 0x1000_0000, 0
+            elif op == "s_add_u32" and "- .Lpc" in ln:
+                lab = a[2].split(" - ")[0]
+                self.s[int(a[0][1:])] = 0x1000_0000 + 4 * self.labels[lab]
+            elif op == "s_addc_u32":
+                self.s[int(a[0][1:])] = 0
+            elif op == "s_mov_b32":
+                self.s[int(a[0][1:])] = self.val(a[1])
+            elif op == "s_and_b32":
+                self.s[int(a[0][1:])] = self.val(a[1]) & self.val(a[2])
+            elif op == "s_add_u32" and a[0] == "m0":
+                assert self.idx_on
+                self.m0 += self.val(a[2])
+            elif op == "s_add_u32":
+                self.s[int(a[0][1:])] = self.val(a[1]) + self.val(a[2])
+            elif op == "s_sub_u32":
+                self.s[int(a[0][1:])] = self.val(a[1]) - self.val(a[2])
+            elif op == "s_cmp_lg_u32":
+                self.scc = self.val(a[0]) != self.val(a[1])
+            elif op == "s_cbranch_scc1":
+                if self.scc:
+                    pc = self.labels[a[0]]
+            elif op == "s_branch":
+                pc = self.labels[a[0]]
+            elif op == "s_mov_b64":
+                d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
+                self.s[d], self.s[d + 1] = self.s[sr], self.s[sr + 1]
+            elif op == "s_setpc_b64":
+                lo = int(re.findall(r"s\[(\d+):", ln)[0])
+                pc = self.addr[(self.s[lo + 1] << 32) | self.s[lo]]
+            elif op == "s_set_gpr_idx_on":
+                assert a[0] == "0"
+                self.idx_on, self.m0 = True, 0
+            elif op == "s_set_gpr_idx_off":
+                self.idx_on = False
+            elif op == "s_waitcnt":
+                continue
+            elif op == "v_mov_b32" and r[0] == gen.PL:
+                self.v[gen.PL] = list(self.pl_lanes)
+            elif op == "v_mov_b32" and r[0] in self.VEC:
+                self.v[r[0]] = list(self.v[r[1]])
+            elif op == "v_mov_b32":
+                self.v[r[0]] = self.val(a[1])
+            elif op == "v_readlane_b32":
+                assert not self.idx_on
+                self.s[int(a[0][1:])] = self.v[r[0]][int(a[2])]
+            elif op == "v_add_u32_e32":
+                assert r[0] == r[1] == gen.PL
+                self.v[gen.PL] = [x + int(a[1]) for x in self.v[gen.PL]]
+            elif op == "ds_read_b32":
+                off = int(ln.split("offset:")[1]) if "offset:" in ln else 0
+                self.v[r[0]] = [self.lds.get(x + off, 0xDEAD) for x in self.v[r[1]]]
+            elif op == "buffer_load_dwordx4":
+                half = 1 if "offset:16" in ln else 0
+                self._load_row(r[0] - 4 * half, self.s[44], half)
+            elif op in ("v_pk_mov_b32", "v_xor_b32_e32", "v_xor_b32_e64", "v_bitop3_b32"):
+                idx = self.m0 if self.idx_on else 0
+                run([ln], self.v, idx)
+            else:
+                raise AssertionError(ln)
+        return np.array([[self.v[gen.ACC + 8 * m + j] for j in range(8)] for m in range(8)], np.uint32)
+
+
+def test_threaded_dispatch_end_to_end_vs_oracle():
+    rng = np.random.default_rng(11)
+    for nr in (8, 16, 24):
+        X = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
+        A = rng.integers(0, 256, (8, nr), dtype=np.uint8)
+        A[0, 0], A[5, 1] = 0, 1                      # empty body, identity body
+        acc = _Wave(X, A, nr).run()
+        for m in range(8):
+            got = bitslice_np(acc[m].view(np.uint8).copy())
+            exp = np.zeros(32, np.uint8)
+            for k in range(nr):
+                exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
+            assert np.array_equal(got, exp), (nr, m)

@@ -26,7 +26,7 @@ for B in Bs:
     dV, dO = ctx.alloc(V.nbytes), ctx.alloc(B * L)
     ctx.h2d(dV, V)
     line = []
-    for mode in (0, 1, 3, 4, 5, 6, 7):
+    for mode in [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,3,5").split(",")]:
         os.environ["KODR_BS_MODE"] = str(mode)
         for i in range(3):
             errors.check(L_.rlnc_gf_matmul_bs_device(ctx.handle, dV, k, B, k, gens[i % G], L, dO, L, L))

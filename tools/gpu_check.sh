@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 STAGE="${1:-all}"
 run() { echo "== $*" >&2; "$@"; }
 if [[ "$STAGE" == all || "$STAGE" == tests ]]; then
-  run timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
+  run timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { tail -40 "$OUT/pytest_gpu.log"; exit 1; }
   tail -3 "$OUT/pytest_gpu.log"
   run timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
   cat "$OUT/smoke.log"

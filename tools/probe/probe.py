@@ -38,3 +38,7 @@ print(f"read_stream HOT {us:7.2f} us {S/us/1e3:7.1f} GB/s")
 # large stream: all 512 MiB at once
 us = timeit(lambda i: p.probe_read(ctypes.c_void_p(buf), ctypes.c_size_t(G * S), ctypes.c_void_p(out), 8192, 256, st), 20)
 print(f"read_stream 512MiB {us:7.2f} us {G*S/us/1e3:7.1f} GB/s")
+# launch floor: the same kernel with nothing to read
+for blocks in (256, 2048):
+    us = timeit(lambda i: p.probe_read(ctypes.c_void_p(buf), ctypes.c_size_t(0), ctypes.c_void_p(out), blocks, 256, st))
+    print(f"empty launch blocks={blocks} {us:7.2f} us")
