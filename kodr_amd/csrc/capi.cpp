@@ -896,8 +896,17 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
     vecs = d->hvecs.data();
     vpitch = k;
   }
-  // coefficient side, one row at a time, exactly as repeated AddPiece calls
+  // coefficient side, one row at a time, exactly as repeated AddPiece calls.
+  // Rows from pinned host memory start their DMA first, so the PCIe copy
+  // overlaps the elimination; rows past the ones accepted land beyond the
+  // received range and are never read.
   const size_t row0 = d->core.received();
+  const bool early = !dev && d->ctx && kodr_amd::Staging::is_pinned(rows);
+  if (early) {
+    TRY(dec_reserve_rows(d, row0 + count, row0));
+    HIPC(hipMemcpy2DAsync(d->recv.p + row0 * d->pitch, d->pitch, rows + k, pitch, d->L, count,
+                          hipMemcpyHostToDevice, d->ctx->stream));
+  }
   int st = RLNC_OK;
   size_t n = 0;
   for (; n < count; n++) {
@@ -909,7 +918,10 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   }
   if (n) d->decoded_ready = false;
   // data side: the accepted pieces are consecutive received rows -> one 2D copy
-  TRY(dec_store_pieces(d, row0, rows + k, pitch, n, dev));
+  if (early)
+    HIPC(hipStreamSynchronize(d->ctx->stream));  // the caller may reuse rows on return
+  else
+    TRY(dec_store_pieces(d, row0, rows + k, pitch, n, dev));
   *consumed = n;
   return st;
 }

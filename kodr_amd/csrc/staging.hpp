@@ -99,18 +99,6 @@ class Staging {
     return hipSuccess;
   }
 
-  void release() {
-    for (int b = 0; b < 2; b++) {
-      if (pending_[b]) (void)hipEventSynchronize(ev_[b]);
-      if (ev_[b]) (void)hipEventDestroy(ev_[b]);
-      if (buf_[b]) (void)hipHostFree(buf_[b]);
-      ev_[b] = nullptr;
-      buf_[b] = nullptr;
-      pending_[b] = false;
-    }
-  }
-
- private:
   // page-locked host memory (hipHostMalloc or hipHostRegister, e.g. through
   // rlnc_host_register) needs no bounce buffer.  An unknown pointer makes
   // hipPointerGetAttributes fail; clear that error so it is not reported by
@@ -124,6 +112,18 @@ class Staging {
     return a.type == hipMemoryTypeHost;
   }
 
+  void release() {
+    for (int b = 0; b < 2; b++) {
+      if (pending_[b]) (void)hipEventSynchronize(ev_[b]);
+      if (ev_[b]) (void)hipEventDestroy(ev_[b]);
+      if (buf_[b]) (void)hipHostFree(buf_[b]);
+      ev_[b] = nullptr;
+      buf_[b] = nullptr;
+      pending_[b] = false;
+    }
+  }
+
+ private:
   hipError_t ensure() {
     if (buf_[0]) return hipSuccess;
     for (int b = 0; b < 2; b++) {

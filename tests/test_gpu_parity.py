@@ -338,6 +338,14 @@ def test_batch_add_random_batches_vs_oracle(gpu_ctx, k, L):
         if mode == 1:
             gpu_ctx.h2d(dbuf, rows)
             st, got_n = _add_rows(d, ctypes.c_void_p(dbuf), n, pitch, True, L)
+        elif it % 2:  # page-locked rows: the DMA starts before the elimination
+            pinned = _page_aligned(rows.shape)
+            pinned[:] = rows
+            gpu_ctx.register(pinned)
+            try:
+                st, got_n = _add_rows(d, ptr(pinned), n, pitch, False, L)
+            finally:
+                gpu_ctx.unregister(pinned)
         else:
             st, got_n = _add_rows(d, ptr(rows), n, pitch, False, L)
         assert (st, got_n) == (exp_st, exp_n)
