@@ -227,10 +227,15 @@ int rlnc_gf_matmul_device(rlnc_ctx* ctx, const uint8_t* d_A, size_t lda, size_t 
  * [0, rows) x [0, round_up(ncols, 32)) becomes 8 bit planes, plane i = bit i
  * of the block's 32 bytes.  Self-inverse.  ldx multiple of 32.  Async. */
 int rlnc_bitslice_device(rlnc_ctx* ctx, uint8_t* d_X, size_t ldx, size_t rows, size_t ncols);
-/* Y = A (x) X like rlnc_gf_matmul_device, with X (K rows, pitch ldx, multiple
- * of 32, K*ldx < 2^32) in bit-sliced layout; Y in plain bytes.  Async. */
-/* diagnostics: byte offsets of the bit-sliced kernel's 256 coefficient bodies */
+/* diagnostics: byte offsets of the bit-sliced kernel's 256 coefficient bodies
+ * (first copy) from body 0; also runs the one-time check that enables the
+ * bit-sliced path on this device */
 int rlnc_bs_body_offsets(rlnc_ctx* ctx, uint32_t* out256);
+/* Y = A (x) X like rlnc_gf_matmul_device, with X (K rows, pitch ldx, multiple
+ * of 32, K*ldx < 2^32) in bit-sliced layout; Y in plain bytes.  Async.
+ * Returns a HIP error ("operation not supported") if the bit-sliced path
+ * failed its one-time check on this device (the engine's own callers then
+ * use rlnc_gf_matmul_device's kernel instead). */
 int rlnc_gf_matmul_bs_device(rlnc_ctx* ctx, const uint8_t* d_A, size_t lda, size_t M, size_t K,
                              const uint8_t* d_Xbs, size_t ldx, uint8_t* d_Y, size_t ldy, size_t ncols);
 
