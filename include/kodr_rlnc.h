@@ -71,6 +71,14 @@ int rlnc_ctx_synchronize(rlnc_ctx* ctx);
 void* rlnc_ctx_stream(rlnc_ctx* ctx);            /* the hipStream_t in use */
 int rlnc_random_bytes(uint8_t* out, size_t n);   /* getrandom(2): crypto/rand stand-in */
 
+/* The engine's own device buffers (generations, received rows, twins) come
+ * from a per-device caching pool: a destroyed encoder/decoder returns them
+ * for the next one instead of paying hipFree (~175 us per 32 MiB buffer).
+ * Reuse is ordered on the owning streams.  At most KODR_POOL_BYTES (default
+ * 8 GiB) stays cached per device; trim releases down to keep_bytes. */
+int rlnc_device_pool_trim(int device, size_t keep_bytes);
+size_t rlnc_device_pool_cached(int device);
+
 /* device memory helpers (plumbing for device-resident callers and benches) */
 int rlnc_dev_alloc(rlnc_ctx* ctx, size_t bytes, void** dptr);
 int rlnc_dev_free(rlnc_ctx* ctx, void* dptr);

@@ -29,6 +29,8 @@ SIGNATURES = {
     "rlnc_ctx_synchronize": (_int, [_vp]),
     "rlnc_ctx_stream": (_vp, [_vp]),
     "rlnc_random_bytes": (_int, [_u8p, _sz]),
+    "rlnc_device_pool_trim": (_int, [_int, _sz]),
+    "rlnc_device_pool_cached": (_sz, [_int]),
     "rlnc_dev_alloc": (_int, [_vp, _sz, _vpp]),
     "rlnc_dev_free": (_int, [_vp, _vp]),
     "rlnc_memcpy_h2d": (_int, [_vp, _vp, _vp, _sz]),

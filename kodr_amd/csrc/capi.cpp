@@ -18,6 +18,7 @@
 #include "../../include/kodr_rlnc.h"
 #include "decoder_core.hpp"
 #include "gf_kernels.hpp"
+#include "pool.hpp"
 #include "staging.hpp"
 
 using kodr_amd::DecoderCore;
@@ -41,21 +42,25 @@ constexpr size_t kPitchAlign = 256;
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 constexpr size_t kMaxDescBytes = (size_t)1 << 31;  // 32-bit buffer offsets in gf_gemm
 
-// Device buffer that only grows.
+// Device buffer that only grows, from the device's caching pool (pool.hpp),
+// ordered on the owner's stream (bind before the first reserve).
 struct DevBuf {
   uint8_t* p = nullptr;
   size_t cap = 0;
+  int dev = 0;
+  hipStream_t st = nullptr;
+  void bind(int device, hipStream_t stream) {
+    dev = device;
+    st = stream;
+  }
   int reserve(size_t bytes) {
     if (bytes <= cap) return RLNC_OK;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    HIPC(hipMalloc((void**)&p, bytes));
-    cap = bytes;
+    release();
+    HIPC(kodr_amd::DevicePool::get(dev).alloc(bytes, st, &p, &cap));
     return RLNC_OK;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) kodr_amd::DevicePool::get(dev).free(p, cap, st);
     p = nullptr;
     cap = 0;
   }
@@ -216,6 +221,7 @@ int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** ou
   rlnc_encoder* e = new (std::nothrow) rlnc_encoder;
   if (!e) return RLNC_ERR_OUT_OF_MEMORY;
   e->ctx = ctx;
+  for (DevBuf* b : {&e->pieces, &e->pieces_bs, &e->vecs, &e->out}) b->bind(ctx->device, ctx->stream);
   e->kind = kind;
   (void)rlnc_random_bytes(reinterpret_cast<uint8_t*>(&e->seed), sizeof(e->seed));
   e->k = k;
@@ -333,6 +339,19 @@ int rlnc_random_bytes(uint8_t* out, size_t n) {
     got += (size_t)r;
   }
   return RLNC_OK;
+}
+
+int rlnc_device_pool_trim(int device, size_t keep_bytes) {
+  int n = 0;
+  TRY(rlnc_device_count(&n));
+  if (device < 0 || device >= n) return RLNC_ERR_NO_DEVICE;
+  HIPC(hipSetDevice(device));
+  kodr_amd::DevicePool::get(device).trim(keep_bytes);
+  return RLNC_OK;
+}
+
+size_t rlnc_device_pool_cached(int device) {
+  return device < 0 ? 0 : kodr_amd::DevicePool::get(device).cached();
 }
 
 int rlnc_dev_alloc(rlnc_ctx* ctx, size_t bytes, void** dptr) {
@@ -600,6 +619,7 @@ static int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_re
   rlnc_recoder* r = new (std::nothrow) rlnc_recoder;
   if (!r) return RLNC_ERR_OUT_OF_MEMORY;
   r->ctx = ctx;
+  for (DevBuf* b : {&r->flat, &r->flat_bs, &r->r, &r->out}) b->bind(ctx->device, ctx->stream);
   r->n = n;
   r->k = k;
   r->clen = clen;
@@ -704,6 +724,9 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
   rlnc_decoder* d = new (std::nothrow) rlnc_decoder(k);
   if (!d) return RLNC_ERR_OUT_OF_MEMORY;
   d->ctx = ctx;
+  if (ctx)
+    for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch, &d->srcs})
+      b->bind(ctx->device, ctx->stream);
   *out = d;
   return RLNC_OK;
 }
@@ -732,15 +755,14 @@ int dec_reserve_rows(rlnc_decoder* d, size_t need, size_t have) {
   if (need <= d->recv_rows) return RLNC_OK;
   size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, need);
   if (nrows * d->pitch >= kMaxDescBytes) nrows = std::max(need, kMaxDescBytes / d->pitch - 1);
-  uint8_t* np = nullptr;
-  HIPC(hipMalloc((void**)&np, nrows * d->pitch));
-  HIPC(hipMemsetAsync(np, 0, nrows * d->pitch, d->ctx->stream));
+  DevBuf nb;
+  nb.bind(d->ctx->device, d->ctx->stream);
+  TRY(nb.reserve(nrows * d->pitch));
+  HIPC(hipMemsetAsync(nb.p, 0, nrows * d->pitch, d->ctx->stream));
   if (d->recv.p && have)
-    HIPC(hipMemcpyAsync(np, d->recv.p, have * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
-  HIPC(hipStreamSynchronize(d->ctx->stream));
-  d->recv.release();
-  d->recv.p = np;
-  d->recv.cap = nrows * d->pitch;
+    HIPC(hipMemcpyAsync(nb.p, d->recv.p, have * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
+  d->recv.release();  // back to the pool, reusable once the stream passes the copy
+  d->recv = nb;
   d->recv_rows = nrows;
   return RLNC_OK;
 }
@@ -790,7 +812,6 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
       !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
-    HIPC(hipStreamSynchronize(ctx->stream));
     TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
     d->bs_rows = 0;
   }

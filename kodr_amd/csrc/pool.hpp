@@ -1,0 +1,128 @@
+// pool.hpp -- per-device caching allocator for the engine's own buffers.
+//
+// hipFree of a 32 MiB buffer costs ~175 us on MI355X (profiles/r01/alloc.log)
+// and a decoder for 32 MiB/256 owns five such buffers, so a service that
+// decodes one generation after another would spend more time freeing than
+// decoding.  Freed blocks are kept instead, keyed by size, and handed to the
+// next request that fits (at most 2x oversized).  Reuse is stream-ordered: a
+// freed block carries an event recorded on the stream that last used it, and
+// a request from another stream makes its stream wait on that event (no host
+// synchronisation).  Blocks beyond the cache cap (KODR_POOL_BYTES, default
+// 8 GiB per device) are really freed, oldest first.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <list>
+#include <mutex>
+
+namespace kodr_amd {
+
+class DevicePool {
+ public:
+  static DevicePool& get(int device) {
+    static DevicePool pools[64];
+    return pools[device & 63];
+  }
+
+  // size rounded up to the block granularity; *cap receives the block size
+  hipError_t alloc(size_t bytes, hipStream_t stream, uint8_t** out, size_t* cap) {
+    const size_t need = round(bytes);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto best = free_.end();
+      for (auto it = free_.begin(); it != free_.end(); ++it)
+        if (it->size >= need && it->size <= 2 * need && (best == free_.end() || it->size < best->size)) best = it;
+      if (best != free_.end()) {
+        Block b = *best;
+        free_.erase(best);
+        cached_ -= b.size;
+        hipError_t e = hipSuccess;
+        if (b.stream != stream) e = hipStreamWaitEvent(stream, b.ev, 0);
+        events_.push_back(b.ev);
+        if (e != hipSuccess) return e;
+        *out = b.p;
+        *cap = b.size;
+        return hipSuccess;
+      }
+    }
+    hipError_t e = hipMalloc((void**)out, need);
+    if (e != hipSuccess) {  // give the cache back to the driver and retry once
+      trim(0);
+      (void)hipGetLastError();
+      e = hipMalloc((void**)out, need);
+    }
+    if (e == hipSuccess) *cap = need;
+    return e;
+  }
+
+  // p (cap bytes, from alloc) is no longer needed once `stream` reaches here
+  void free(uint8_t* p, size_t cap, hipStream_t stream) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    hipEvent_t ev = nullptr;
+    if (!events_.empty()) {
+      ev = events_.back();
+      events_.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      ev = nullptr;
+    }
+    if (!ev || hipEventRecord(ev, stream) != hipSuccess) {  // cannot order reuse: free for real
+      if (ev) events_.push_back(ev);
+      (void)hipStreamSynchronize(stream);
+      (void)hipFree(p);
+      return;
+    }
+    free_.push_front(Block{p, cap, stream, ev});
+    cached_ += cap;
+    while (cached_ > limit() && !free_.empty()) release_oldest();
+  }
+
+  // free cached blocks until at most `keep` bytes remain
+  void trim(size_t keep) {
+    std::lock_guard<std::mutex> lk(mu_);
+    while (cached_ > keep && !free_.empty()) release_oldest();
+  }
+
+  size_t cached() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return cached_;
+  }
+
+ private:
+  struct Block {
+    uint8_t* p;
+    size_t size;
+    hipStream_t stream;
+    hipEvent_t ev;
+  };
+
+  static size_t round(size_t b) {
+    const size_t g = b >= ((size_t)1 << 20) ? ((size_t)2 << 20) : ((size_t)64 << 10);
+    return (std::max<size_t>(b, 1) + g - 1) / g * g;
+  }
+  static size_t limit() {
+    static const size_t lim = [] {
+      const char* s = getenv("KODR_POOL_BYTES");
+      return s ? (size_t)strtoull(s, nullptr, 10) : ((size_t)8 << 30);
+    }();
+    return lim;
+  }
+  void release_oldest() {  // mu_ held
+    Block b = free_.back();
+    free_.pop_back();
+    cached_ -= b.size;
+    (void)hipEventSynchronize(b.ev);
+    (void)hipFree(b.p);
+    events_.push_back(b.ev);
+  }
+
+  std::mutex mu_;
+  std::list<Block> free_;  // most recently freed first
+  std::list<hipEvent_t> events_;
+  size_t cached_ = 0;
+};
+
+}  // namespace kodr_amd

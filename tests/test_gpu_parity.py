@@ -560,3 +560,30 @@ def test_gf_matmul_bs_vs_oracle(gpu_ctx, M, K, n):
     finally:
         for p in (dA, dX, dY):
             gpu_ctx.free(p)
+
+
+def test_device_pool_reuse_across_generations_and_streams(gpu_ctx):
+    """Encoders/decoders created one after another (and on two streams) reuse
+    pooled device buffers: every generation still decodes bit-exactly, and the
+    pool holds the freed buffers until trimmed."""
+    import kodr_amd.device as dev
+    L_ = _lib.lib()
+    other = dev.Context(0)   # a second stream: reuse across streams is event-ordered
+    rng = np.random.default_rng(33)
+    for it in range(6):
+        ctx = gpu_ctx if it % 2 == 0 else other
+        k, L = (32, 4096) if it < 3 else (16, 8192 + 32 * it)
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        e = Enc(ctx, P)
+        V, out = e.code(rng.integers(0, 256, (k + 2, k), dtype=np.uint8))
+        assert np.array_equal(out[:, k:], oracle.encode(P, V))
+        d = Dec(ctx, k)
+        st, n = _add_rows(d, ptr(out), out.shape[0], k + L, False)
+        assert st in (0, 3) and n >= k
+        st, allp = d.get_all()
+        assert st == 0 and np.array_equal(allp, P)
+        del e, d
+    assert L_.rlnc_device_pool_cached(0) > 0
+    errors.check(L_.rlnc_device_pool_trim(0, 0))
+    assert L_.rlnc_device_pool_cached(0) == 0
+    other.close()
