@@ -268,6 +268,57 @@ def run_relay(ctx, L_, errors, enc, k, L, rng, torch, dist, kdist):
     return res
 
 
+def two_streams(L_, errors, k, L, rng, batches=(1, 32), gens=16, steps=200):
+    """Independent generations encoded from two contexts (two HIP streams)
+    at once, steps alternating between them: the launch gap and the ramp of
+    one stream's kernel overlap the other's.  Wall time over the steps, both
+    streams drained; not the headline (per-kernel durations overlap)."""
+    import ctypes
+    import numpy as np
+    from kodr_amd import device as kdev
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    ctxs = [kdev.Context(0), kdev.Context(0)]
+    encs = [[], []]
+    for g in range(gens):
+        data = rng.integers(0, 256, k * L, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        errors.check(L_.rlnc_encoder_create(ctxs[g % 2].handle, 0, data.ctypes.data_as(u8p), k, L, ctypes.byref(h)))
+        encs[g % 2].append(h)
+    res = {}
+    for b in batches:
+        V = rng.integers(0, 256, (b, k), dtype=np.uint8)
+        bufs = []
+        for c in ctxs:
+            dv, do = c.alloc(V.nbytes), c.alloc(b * L)
+            c.h2d(dv, V)
+            bufs.append((dv, do))
+
+        def step(i):
+            s = i & 1
+            errors.check(L_.rlnc_encoder_coded_pieces_device(encs[s][(i >> 1) % len(encs[s])], bufs[s][0], b,
+                                                             bufs[s][1], L))
+        for i in range(20):
+            step(i)
+        for c in ctxs:
+            c.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(i)
+        for c in ctxs:
+            c.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        res[str(b)] = {"us_per_pass": round(dt * 1e6, 2), "coded_MBps": round(b * setbytes(k, L) / dt / 1e6, 1),
+                       "generation_read_GBps": round(k * L / dt / 1e9, 1)}
+        for c, (dv, do) in zip(ctxs, bufs):
+            c.free(dv)
+            c.free(do)
+    for c, es in zip(ctxs, encs):
+        for h in es:
+            L_.rlnc_encoder_destroy(h)
+        c.close()
+    return res
+
+
 def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     """Secondary measurements (not the headline): MALL-hot encode, full
     decode of 32 MiB/256 from device-resident pieces, host-path encode."""
@@ -351,14 +402,21 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     ctx.free(dWire)
     ctx.free(dDec)
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
+    out["encode_two_streams"] = two_streams(L_, errors, k, L, rng)
     out["host_path"] = host_roundtrip(ctx, L_, errors, k, L, rng)
     out["host_path_registered"] = host_roundtrip(ctx, L_, errors, k, L, rng, pinned=True)
     return out
 
 
-VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9      # integer VALU lane-ops/s (MI355X_MICROARCH.md)
-LANE_OPS_PER_MAC_PERM = 4.5 / 4            # gf_gemm_kernel: 3 v_perm + 1.5 v_bitop3 per coefficient x 4 bytes
-LANE_OPS_PER_MAC_BS = 18.0 / 32            # gf_bs_kernel: 18 XOR3 (average body) per coefficient x 32 bytes
+# Issue ceiling of the apply kernels: 1024 SIMDs at 2.4 GHz issuing one wave
+# instruction per ~2.35 cycles with 4 waves per SIMD (profiles/r01/dispatch_probe.log),
+# times the GF MACs each instruction carries: gf_bs_kernel issues ~15 per
+# coefficient per 2 KiB wave slice (8 XOR3, table share, v_readlane, SALU;
+# DESIGN.md), gf_gemm_kernel ~5 per coefficient per 256 B (3 v_perm + 1.5 XOR3
+# + selector share).
+ISSUE_PER_S = 1024 * 2.4e9 / 2.35
+MACS_PER_INST_BS = 2048 / 15
+MACS_PER_INST_PERM = 256 / 5
 
 
 def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
@@ -389,9 +447,9 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
     macs = best["gf_rows"] * best["received"] * L
     best["apply_gf_macs"] = macs
     best["apply_gf_macs_per_s"] = float(f"{macs / best['get_s']:.4g}")
-    per = LANE_OPS_PER_MAC_BS if best["gf_rows"] >= 16 else LANE_OPS_PER_MAC_PERM
+    mpi = MACS_PER_INST_BS if best["gf_rows"] >= 16 else MACS_PER_INST_PERM
     best["apply_kernel"] = "gf_bs_kernel" if best["gf_rows"] >= 16 else "gf_gemm_kernel"
-    best["valu_ceiling_macs_per_s"] = float(f"{VALU_LANE_OPS / per:.4g}")
+    best["issue_ceiling_macs_per_s"] = float(f"{ISSUE_PER_S * mpi:.4g}")
     return best
 
 

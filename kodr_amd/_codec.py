@@ -105,9 +105,10 @@ class _Encoder:
 class _Recoder:
     """full/recoder.go."""
 
-    def __init__(self, handle, ctx, rng=None, batch=16):
+    def __init__(self, handle, ctx, k, rng=None, batch=16):
         self._h = handle
         self._ctx = ctx
+        self._k = k          # pieces coded together: the vector part of a wire row
         self._rng = rng
         self._batch = max(1, int(batch))
         self._queue = deque()
@@ -139,7 +140,7 @@ class _Recoder:
                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out.reshape(count, clen)
 
-    def CodedPiece(self, k=None):
+    def CodedPiece(self):
         """full/recoder.go:27-46 -> CodedPiece(Vector = r x C, Piece = sum r_i P_i)."""
         if not self._queue:
             n = self.PieceCount()

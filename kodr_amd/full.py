@@ -56,9 +56,7 @@ def NewFullRLNCRecoderWithFlattenData(data, pieceCount, piecesCodedTogether, ctx
     arr, p = u8(bytes(data))
     errors.check(lib().rlnc_recoder_create(ctx.handle, p, len(data), pieceCount, piecesCodedTogether,
                                            ctypes.byref(h)))
-    rec = FullRLNCRecoder(h, ctx, rng=rng, batch=batch)
-    rec._k = piecesCodedTogether
-    return rec
+    return FullRLNCRecoder(h, ctx, piecesCodedTogether, rng=rng, batch=batch)
 
 
 def NewFullRLNCDecoder(pieceCount, ctx=None):

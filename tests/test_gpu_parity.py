@@ -587,3 +587,105 @@ def test_device_pool_reuse_across_generations_and_streams(gpu_ctx):
     errors.check(L_.rlnc_device_pool_trim(0, 0))
     assert L_.rlnc_device_pool_cached(0) == 0
     other.close()
+
+
+def test_c1_round_trip_vs_oracle(gpu_ctx):
+    """BASELINE config 1's shape (1 MiB / 16 pieces) on the engine: every coded
+    piece vs the oracle, and the decoder's counters after every AddPiece."""
+    rng = np.random.default_rng(0xC1)
+    k, L = 16, 65536
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    V, out = e.code(rng.integers(0, 256, (k + 4, k), dtype=np.uint8))
+    assert np.array_equal(out[:, k:], oracle.encode(P, V))
+    d, ref = Dec(gpu_ctx, k), oracle.Decoder(k)
+    for row in out:
+        st = d.add(row[:k], row[k:])
+        assert st == ref.add(row[:k], row[k:])
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+        if st == ERR["ErrAllUsefulPiecesReceived"]:
+            break
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+
+
+def test_c5_generations_encode_relay_recode_one_gpu(gpu_ctx):
+    """BASELINE config 5 on one GPU: 8 generations of 32 MiB / 256, each encoded
+    into device wire rows with device-drawn vectors, handed to the next
+    "rank" (a device copy standing in for the RCCL ring shift), recoded there
+    from device memory, checked against the oracle and decoded."""
+    L_ = _lib.lib()
+    k, L, G = 256, 131072, 8
+    clen = k + L
+    pitch = (clen + 255) // 256 * 256
+    rng = np.random.default_rng(0xC5)
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    encs = [Enc(gpu_ctx, P) for P in gens]
+    wire = [gpu_ctx.alloc(k * pitch) for _ in range(G)]
+    recv, out = gpu_ctx.alloc(k * pitch), gpu_ctx.alloc((k + 2) * pitch)
+    R = rng.integers(0, 256, (k + 2, k), dtype=np.uint8)
+    dR = gpu_ctx.alloc(R.nbytes)
+    gpu_ctx.h2d(dR, R)
+    try:
+        for g in range(G):
+            errors.check(L_.rlnc_encoder_coded_wire_device(encs[g].h, k, wire[g], pitch))
+        for g in range(G):
+            src = (g - 1) % G                     # rank g receives rank g-1's pieces
+            errors.check(L_.rlnc_memcpy_d2d_async(gpu_ctx.handle, recv, wire[src], k * pitch))
+            rh = ctypes.c_void_p()
+            errors.check(L_.rlnc_recoder_create_device(gpu_ctx.handle, recv, k, clen, pitch, k, ctypes.byref(rh)))
+            errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, k + 2, out, pitch))
+            gpu_ctx.synchronize()
+            L_.rlnc_recoder_destroy(rh)
+            rows = np.ascontiguousarray(gpu_ctx.d2h(out, (k + 2) * pitch).reshape(k + 2, pitch)[:, :clen])
+            held = np.ascontiguousarray(gpu_ctx.d2h(recv, k * pitch).reshape(k, pitch)[:, :clen])
+            assert np.array_equal(held[:, k:], oracle.encode(gens[src], held[:, :k]))
+            assert np.array_equal(rows[:2], oracle.recode(held, k, R[:2]))
+            d = Dec(gpu_ctx, k)
+            st, n = _add_rows(d, ptr(rows), k + 2, clen, False)
+            assert st in (0, 3) and n >= k
+            st, dec = d.get_all()
+            assert st == 0 and np.array_equal(dec, gens[src]), g
+    finally:
+        gpu_ctx.synchronize()
+        for p in wire + [recv, out, dR]:
+            gpu_ctx.free(p)
+
+
+def test_contexts_on_threads_run_concurrently(gpu_ctx):
+    """Three host threads, each with its own context (stream), encode and
+    decode different generations at the same time through the C ABI (ctypes
+    releases the GIL): every result bit-exact vs the oracle."""
+    import threading
+
+    import kodr_amd.device as dev
+    errs = []
+
+    def worker(seed):
+        try:
+            ctx = dev.Context(0)
+            rng = np.random.default_rng(seed)
+            for it in range(4):
+                k, L = 64, 32768 + 32 * seed
+                P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+                e = Enc(ctx, P)
+                V, out = e.code(rng.integers(0, 256, (k + 1, k), dtype=np.uint8))
+                if not np.array_equal(out[:3, k:], oracle.encode(P, V[:3])):
+                    errs.append(("encode", seed, it))
+                d = Dec(ctx, k)
+                st, n = _add_rows(d, ptr(out), out.shape[0], k + L, False)
+                st, dec = d.get_all()
+                if st != 0 or not np.array_equal(dec, P):
+                    errs.append(("decode", seed, it))
+                del e, d
+            ctx.close()
+        except Exception as ex:  # reported below, in the main thread
+            errs.append(repr(ex))
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in (1, 2, 3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not any(t.is_alive() for t in ts)
+    assert not errs, errs
