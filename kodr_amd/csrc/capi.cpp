@@ -195,8 +195,14 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
 }
 
 // Below this many output rows the perm-table kernel (gf_gemm) wins: the
-// bit-sliced launch has a higher fixed cost (profiles/r01/bs_bringup.log).
-constexpr size_t kBsMinRows = 16;
+// bit-sliced kernel runs one 8-row group however few rows are real, and with
+// 1-2 waves per SIMD its 2-row load ring leaves it latency-bound (~13 us for
+// B = 1 at 32 MiB/256 against 9 us; B = 8: 17-19 against 16 us; B = 10: 20
+// against 28 us; profiles/r01/bs_min_rows.log).
+constexpr size_t kBsMinRows = 9;
+// The decoder builds its twin per materialization (one more pass over the
+// received rows), so the bit-sliced kernel must save more than that pass.
+constexpr size_t kBsMinRowsDecode = 16;
 
 // Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
@@ -207,8 +213,7 @@ int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {
     TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
-    HIPC(hipMemcpyAsync(twin.p, plain, K * ldx, hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(kodr_amd::bitslice_rows(twin.p, ldx, K, ncols, ctx->stream));
+    HIPC(kodr_amd::bitslice_rows(plain, twin.p, ldx, K, ncols, ctx->stream));
     twin_valid = true;
   }
   return gemm_bs(ctx, dA, lda, M, K, twin.p, ldx, dY, ldy, ncols);
@@ -808,7 +813,11 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
 int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t ldy) {
   const size_t recv = d->core.received();
   rlnc_ctx* ctx = d->ctx;
-  if (M < kBsMinRows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
+  size_t min_rows = kBsMinRowsDecode;
+#ifdef KODR_TUNE_MODES
+  if (const char* env = getenv("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
+#endif
+  if (M < min_rows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
       !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
@@ -817,9 +826,8 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   }
   if (d->bs_rows < recv) {
     const size_t n = recv - d->bs_rows;
-    HIPC(hipMemcpyAsync(d->recv_bs.p + d->bs_rows * d->pitch, d->recv.p + d->bs_rows * d->pitch, n * d->pitch,
-                        hipMemcpyDeviceToDevice, ctx->stream));
-    HIPC(kodr_amd::bitslice_rows(d->recv_bs.p + d->bs_rows * d->pitch, d->pitch, n, d->L, ctx->stream));
+    HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
+                                 d->pitch, n, d->L, ctx->stream));
     d->bs_rows = recv;
   }
   return gemm_bs(ctx, dA, recv, M, recv, d->recv_bs.p, d->pitch, dY, ldy, d->L);
@@ -1025,7 +1033,7 @@ int rlnc_decoder_transform(const rlnc_decoder* d, uint8_t* out) {
 int rlnc_bitslice_device(rlnc_ctx* ctx, uint8_t* dX, size_t ldx, size_t rows, size_t ncols) {
   if (!ctx || (rows && ncols && !dX)) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(ctx));
-  HIPC(kodr_amd::bitslice_rows(dX, ldx, rows, ncols, ctx->stream));
+  HIPC(kodr_amd::bitslice_rows(dX, dX, ldx, rows, ncols, ctx->stream));
   return RLNC_OK;
 }
 

@@ -72,13 +72,16 @@ __device__ __forceinline__ void bitslice32(uint32_t (&d)[8]) {
   }
 }
 
-__global__ __launch_bounds__(256) void bitslice_kernel(uint8_t* __restrict__ X, size_t ldx, int rows,
+// src may equal dst (in place): each thread reads its block before writing it
+__global__ __launch_bounds__(256) void bitslice_kernel(const uint8_t* src, uint8_t* dst, size_t ldx, int rows,
                                                       int nblk) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const int r = (int)(i / (size_t)nblk), b = (int)(i % (size_t)nblk);
   if (r >= rows) return;
-  uint4* p = reinterpret_cast<uint4*>(X + (size_t)r * ldx + (size_t)b * kBsBlock);
-  const uint4 a = p[0], c = p[1];
+  const size_t off = (size_t)r * ldx + (size_t)b * kBsBlock;
+  const uint4* q = reinterpret_cast<const uint4*>(src + off);
+  uint4* p = reinterpret_cast<uint4*>(dst + off);
+  const uint4 a = q[0], c = q[1];
   uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
   bitslice32(d);
   p[0] = make_uint4(d[0], d[1], d[2], d[3]);
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"                                       \
                : KODR_BS_RING_OPERANDS                                                              \
                : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx),  \
-                 [ngrp] "s"(ngrp), [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)lane * 4u),   \
+                 [ngrp] "s"(ngrp), [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)reinterpret_cast<uintptr_t>(red) + (uint32_t)lane * 4u),   \
                  [pl] "v"(pl), [ydbg] "s"(Y)                                                        \
                : KODR_BS_CLOBBERS)
   if (nr > 0 && MODE != 5) {
@@ -368,14 +371,15 @@ bool bs_ready(int device) {
   return bs_init(device, &bd) == hipSuccess && bd->ok;
 }
 
-hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hipStream_t stream) {
+hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,
+                         hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;
   if (ldx % kBsBlock || ldx < (ncols + kBsBlock - 1) / kBsBlock * kBsBlock) return hipErrorInvalidValue;
   const size_t nblk = (ncols + kBsBlock - 1) / kBsBlock;
   const size_t total = rows * nblk;
   if (rows > 0x7fffffff || nblk > 0x7fffffff) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bitslice_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, dX, ldx,
-                     (int)rows, (int)nblk);
+  hipLaunchKernelGGL(bitslice_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src, dst,
+                     ldx, (int)rows, (int)nblk);
   return hipGetLastError();
 }
 

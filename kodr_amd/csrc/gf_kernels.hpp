@@ -32,9 +32,12 @@ hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t
                         size_t n_sys, size_t sys_first, hipStream_t stream);
 
 // ---- bit-sliced path (gf_bs.hip) ----
-// In place: every 32-byte block of rows [0, rows) x [0, round_up(ncols, 32))
-// becomes 8 bit planes (self-inverse).  ldx multiple of 32.
-hipError_t bitslice_rows(uint8_t* dX, size_t ldx, size_t rows, size_t ncols, hipStream_t stream);
+// dst = src with every 32-byte block of rows [0, rows) x [0, round_up(ncols,
+// 32)) turned into 8 bit planes (self-inverse); src == dst works in place.
+// Both use pitch ldx, a multiple of 32; dst's bytes past those blocks are not
+// written.
+hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,
+                         hipStream_t stream);
 
 // byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);

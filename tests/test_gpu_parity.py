@@ -530,7 +530,10 @@ def test_bitslice_layout(gpu_ctx):
 
 
 @pytest.mark.parametrize("M,K,n", [(1, 1, 32), (8, 8, 2048), (3, 5, 77), (16, 40, 5000), (17, 300, 4096),
-                                   (32, 256, 8192), (40, 7, 3000), (64, 256, 6149), (256, 258, 4096)])
+                                   (32, 256, 8192), (40, 7, 3000), (64, 256, 6149), (256, 258, 4096),
+                                   # shapes whose plan splits K across workgroups
+                                   (1, 256, 65536), (8, 256, 131072), (12, 128, 131072 - 96),
+                                   (16, 256, 131072)])
 def test_gf_matmul_bs_vs_oracle(gpu_ctx, M, K, n):
     """Bit-sliced kernel: bit-exact vs the oracle, with zero coefficients,
     lda > K, ragged columns and a canary row beyond the output."""
@@ -613,37 +616,42 @@ def test_c5_generations_encode_relay_recode_one_gpu(gpu_ctx):
     """BASELINE config 5 on one GPU: 8 generations of 32 MiB / 256, each encoded
     into device wire rows with device-drawn vectors, handed to the next
     "rank" (a device copy standing in for the RCCL ring shift), recoded there
-    from device memory, checked against the oracle and decoded."""
+    from device memory, checked against the oracle and decoded.  Each rank
+    sends n = k + 4 pieces: k random vectors over GF(256) are singular with
+    probability ~1/255, and the device vector stream is seeded at random."""
     L_ = _lib.lib()
     k, L, G = 256, 131072, 8
+    n = k + 4
     clen = k + L
     pitch = (clen + 255) // 256 * 256
     rng = np.random.default_rng(0xC5)
     gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
     encs = [Enc(gpu_ctx, P) for P in gens]
-    wire = [gpu_ctx.alloc(k * pitch) for _ in range(G)]
-    recv, out = gpu_ctx.alloc(k * pitch), gpu_ctx.alloc((k + 2) * pitch)
-    R = rng.integers(0, 256, (k + 2, k), dtype=np.uint8)
+    wire = [gpu_ctx.alloc(n * pitch) for _ in range(G)]
+    recv, out = gpu_ctx.alloc(n * pitch), gpu_ctx.alloc((k + 2) * pitch)
+    R = rng.integers(0, 256, (k + 2, n), dtype=np.uint8)
     dR = gpu_ctx.alloc(R.nbytes)
     gpu_ctx.h2d(dR, R)
     try:
         for g in range(G):
-            errors.check(L_.rlnc_encoder_coded_wire_device(encs[g].h, k, wire[g], pitch))
+            errors.check(L_.rlnc_encoder_coded_wire_device(encs[g].h, n, wire[g], pitch))
         for g in range(G):
             src = (g - 1) % G                     # rank g receives rank g-1's pieces
-            errors.check(L_.rlnc_memcpy_d2d_async(gpu_ctx.handle, recv, wire[src], k * pitch))
+            errors.check(L_.rlnc_memcpy_d2d_async(gpu_ctx.handle, recv, wire[src], n * pitch))
             rh = ctypes.c_void_p()
-            errors.check(L_.rlnc_recoder_create_device(gpu_ctx.handle, recv, k, clen, pitch, k, ctypes.byref(rh)))
+            errors.check(L_.rlnc_recoder_create_device(gpu_ctx.handle, recv, n, clen, pitch, k, ctypes.byref(rh)))
             errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, k + 2, out, pitch))
             gpu_ctx.synchronize()
             L_.rlnc_recoder_destroy(rh)
             rows = np.ascontiguousarray(gpu_ctx.d2h(out, (k + 2) * pitch).reshape(k + 2, pitch)[:, :clen])
-            held = np.ascontiguousarray(gpu_ctx.d2h(recv, k * pitch).reshape(k, pitch)[:, :clen])
+            held = np.ascontiguousarray(gpu_ctx.d2h(recv, n * pitch).reshape(n, pitch)[:, :clen])
             assert np.array_equal(held[:, k:], oracle.encode(gens[src], held[:, :k]))
             assert np.array_equal(rows[:2], oracle.recode(held, k, R[:2]))
+            # every row's vector and first data block (column separability)
+            assert np.array_equal(rows[:, :k + 64], oracle.recode(np.ascontiguousarray(held[:, :k + 64]), k, R)), g
             d = Dec(gpu_ctx, k)
-            st, n = _add_rows(d, ptr(rows), k + 2, clen, False)
-            assert st in (0, 3) and n >= k
+            st, used = _add_rows(d, ptr(rows), k + 2, clen, False)
+            assert st in (0, 3) and used >= k
             st, dec = d.get_all()
             assert st == 0 and np.array_equal(dec, gens[src]), g
     finally:

@@ -87,7 +87,7 @@ for g in range(G):
     errors.check(L_.rlnc_bitslice_device(ctx.handle, db, L, k, L))
     gens.append((d, db))
 e0, e1 = ctx.event(), ctx.event()
-for B in (1, 8, 16, 32, 64, 256):
+for B in [int(b) for b in os.environ.get("KODR_BS_CHECK_B", "1,8,16,32,64,256").split(",")]:
     V = rng.integers(0, 256, (B, k), dtype=np.uint8)
     dV, dO = ctx.alloc(V.nbytes), ctx.alloc(B * L)
     ctx.h2d(dV, V)
