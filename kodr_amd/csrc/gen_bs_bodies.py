@@ -149,14 +149,25 @@ def table_lines(slot):
     return out
 
 
-def row_lines(j, dispatch=True, loads=True):
+# Wave priority of input row j of a chunk.  Without it the SIMD's arbiter
+# favours the oldest wave and the 4 waves of a SIMD finish far apart (18-35 k
+# cycles, profiles/r01/bs_timeline.log), so the last rows of a launch run at
+# low occupancy.  Rotating the priority with the row index lets the waves
+# overtake each other: -5 % per B = 32 launch, -6 % at B = 64 (measured against
+# 5 other patterns, profiles/r01/bs_prio.log).
+def ROW_PRIO(j):
+    return j % 4
+
+
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
     trip sits inside a row."""
     slot = j % P
     h = lambda i: T0 + 2 * i  # noqa: E731
-    t = [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
+    t = [f"s_setprio {prio(j)}"] if prio else []
+    t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
     t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)]
     t += table_lines(slot)
     b = RING + 8 * slot
@@ -208,7 +219,7 @@ def prologue_lines(dispatch=True):
     return pro
 
 
-def main_loop(dispatch=True, loads=True):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
@@ -218,10 +229,12 @@ def main_loop(dispatch=True, loads=True):
         t += ["s_branch .Lloop_%="] + stub_lines()
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads)
+        t += row_lines(j, dispatch, loads, prio)
     t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
           f"v_add_u32_e32 v{PL}, 256, v{PL}"]
     t += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_lg_u32 s{CNT}, 0", "s_cbranch_scc1 .Lloop_%="]
+    if prio:
+        t += ["s_setprio 0"]
     return t
 
 
@@ -239,6 +252,8 @@ def dump_lines():
     t += ["s_waitcnt vmcnt(0)"]
     t += [".Lstub_%=:"] + [f".Lret{j}_%=:" for j in range(8)]   # never jumped to
     return t
+
+
 
 
 def emit(name, lines):
@@ -299,6 +314,8 @@ def main():
     out += emit("KODR_BS_MAIN_ND", main_loop(False))
     out += emit("KODR_BS_MAIN_NL", main_loop(True, False))
     out += emit("KODR_BS_MAIN_NDNL", main_loop(False, False))
+    # tuning: the loop without the priority rotation (MODE 10)
+    out += emit("KODR_BS_MAIN_NOPRIO", main_loop(True, True, None))
     out += emit("KODR_BS_DUMP", dump_lines())
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)

@@ -227,6 +227,8 @@ class _Wave:
             elif op == "buffer_load_dwordx4":
                 half = 1 if "offset:16" in ln else 0
                 self._load_row(r[0] - 4 * half, self.s[44], half)
+            elif op == "s_setprio":  # scheduling only
+                assert 0 <= int(a[0]) <= 3
             elif op in ("v_pk_mov_b32", "v_xor_b32_e32", "v_xor_b32_e64", "v_bitop3_b32"):
                 idx = self.m0 if self.idx_on else 0
                 run([ln], self.v, idx)

@@ -23,6 +23,6 @@ fi
 if [[ "$STAGE" == all || "$STAGE" == prof ]]; then
   cd /tmp
   run timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python3 "$R/bench.py" --no-cpu-baseline --steps 200 > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { tail -30 "$OUT/prof.err"; exit 1; }
+      python3 "$R/bench.py" --no-cpu-baseline --no-extras --steps 200 > "$OUT/prof_bench.json" 2> "$OUT/prof.err" || { tail -30 "$OUT/prof.err"; exit 1; }
   find "$OUT/prof" -name "*stats*" | head
 fi
