@@ -255,7 +255,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, k, L),
-                         "kernel": "gf_bs_kernel" if B >= 16 else "gf_gemm_kernel",
+                         "kernel": "gf_bs_kernel" if B >= 9 else "gf_gemm_kernel",  # capi.cpp kBsMinRows
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "compulsory_hbm_bytes_per_launch": compulsory,
                          "compulsory_hbm_GBps": round(compulsory / t_launch / 1e9, 1),
@@ -536,6 +536,7 @@ def c4_decode(ctx, L_, errors, rng):
     dAll = ctx.alloc(n * W)
     errors.check(L_.rlnc_encoder_coded_wire_device(eh, n, dAll, W))
     rows = ctx.d2h(dAll, n * W).reshape(n, W)
+    res_enc = c4_encode(ctx, L_, errors, data, k, L)
     lost = set(rng.choice(k, k // 10, replace=False).tolist())
     keep = [i for i in range(k) if i not in lost] + list(range(k, n))
     kept = np.ascontiguousarray(rows[keep])
@@ -543,7 +544,7 @@ def c4_decode(ctx, L_, errors, rng):
     dKept, dCoded, dDec = ctx.alloc(kept.nbytes), ctx.alloc(coded.nbytes), ctx.alloc(k * L)
     ctx.h2d(dKept, kept)
     ctx.h2d(dCoded, coded)
-    res = {"lost_systematic": len(lost)}
+    res = {"encode": res_enc, "lost_systematic": len(lost)}
     res["systematic"] = time_decode(ctx, L_, errors, dKept, kept.shape[0], W, k, L, dDec)
     ok = bool(np.array_equal(ctx.d2h(dDec, k * L), data))
     res["full_coded_only"] = time_decode(ctx, L_, errors, dCoded, coded.shape[0], W, k, L, dDec)
@@ -554,6 +555,47 @@ def c4_decode(ctx, L_, errors, rng):
         ctx.free(p)
     L_.rlnc_encoder_destroy(eh)
     return res
+
+
+def c4_encode(ctx, L_, errors, data, k, L, B=32, iters=40):
+    """Systematic encode at BASELINE config 4 (16 MiB/128), device-resident
+    wire rows with device-drawn vectors: the first k pieces are e_i ++ P_i
+    copies (systematic/encoder.go:83-96), later ones coded, B per call.
+    kodr's SetBytes per piece: S + (k+L) (benches/systematic/encoder_test.go:44)."""
+    import ctypes
+    from kodr_amd import device as kdev
+    W = k + L
+    unit = k * L + W
+    dW = ctx.alloc(k * W)
+    e0, e1 = ctx.event(), ctx.event()
+    t_sys = []
+    for rep in range(3):
+        eh = ctypes.c_void_p()
+        errors.check(L_.rlnc_encoder_create(ctx.handle, 1, data.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), k,
+                                            L, ctypes.byref(eh)))
+        ctx.synchronize()
+        ctx.record(e0)
+        errors.check(L_.rlnc_encoder_coded_wire_device(eh, k, dW, W))   # the k systematic pieces
+        ctx.record(e1)
+        ctx.synchronize()
+        t_sys.append(kdev.Context.elapsed_ms(e0, e1) / 1e3)
+        if rep < 2:
+            L_.rlnc_encoder_destroy(eh)
+    for i in range(3):
+        errors.check(L_.rlnc_encoder_coded_wire_device(eh, B, dW, W))
+    ctx.record(e0)
+    for i in range(iters):
+        errors.check(L_.rlnc_encoder_coded_wire_device(eh, B, dW, W))
+    ctx.record(e1)
+    t_cod = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters
+    L_.rlnc_encoder_destroy(eh)
+    ctx.free(dW)
+    ts = min(t_sys)
+    return {"systematic_k_pieces_us": round(ts * 1e6, 2), "systematic_MBps": round(k * unit / ts / 1e6, 1),
+            "coded_B": B, "coded_us_per_call": round(t_cod * 1e6, 2),
+            "coded_MBps": round(B * unit / t_cod / 1e6, 1),
+            "first_2k_pieces_MBps": round(2 * k * unit / (ts + k / B * t_cod) / 1e6, 1),
+            "unit_bytes": unit}
 
 
 def _page_aligned(np, n):

@@ -159,7 +159,7 @@ def ROW_PRIO(j):
     return j % 4
 
 
-def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO):
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
@@ -178,8 +178,12 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO):
               "s_add_u32 s44, s44, s45"]
     t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)]
     if dispatch:
-        t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{STUB}:{STUB + 1}]",
-              f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]",
+        if half_prio:  # this row's own stub, which sets the second half's priority
+            t += [f"s_add_u32 s{h(4)}, s{GPC}, .Lstub{j}_%= - .Lpc_%=",
+                  f"s_addc_u32 s{h(4) + 1}, s{GPC + 1}, 0"]
+        else:
+            t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{STUB}:{STUB + 1}]"]
+        t += [f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]",
               "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
               f"s_setpc_b64 s[{h(0)}:{h(0) + 1}]",
               f".Lret{j}_%=:",
@@ -187,12 +191,12 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO):
     return t
 
 
-def stub_lines():
+def stub_lines(label="stub", prio=None):
     """Between the two halves of a row: rows 4..7 reuse copies 0..3 at M0
     index 32, with targets T[1..3] from the second half's registers and T[4]
     the row's return address."""
     h = lambda i: T0 + 2 * i  # noqa: E731
-    t = [".Lstub_%=:", "s_add_u32 m0, m0, 32"]
+    t = [f".L{label}_%=:"] + ([f"s_setprio {prio}"] if prio is not None else []) + ["s_add_u32 m0, m0, 32"]
     t += [f"s_mov_b64 s[{h(m)}:{h(m) + 1}], s[{H2 + 2 * m}:{H2 + 2 * m + 1}]" for m in (1, 2, 3)]
     t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{RT}:{RT + 1}]", f"s_setpc_b64 s[{H2}:{H2 + 1}]"]
     return t
@@ -219,7 +223,7 @@ def prologue_lines(dispatch=True):
     return pro
 
 
-def main_loop(dispatch=True, loads=True, prio=ROW_PRIO):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
@@ -227,9 +231,12 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO):
     t = prologue_lines(dispatch)
     if dispatch:
         t += ["s_branch .Lloop_%="] + stub_lines()
+        if half_prio:
+            for j in range(8):
+                t += stub_lines(f"stub{j}", half_prio(j))
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads, prio)
+        t += row_lines(j, dispatch, loads, prio, half_prio)
     t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
           f"v_add_u32_e32 v{PL}, 256, v{PL}"]
     t += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_lg_u32 s{CNT}, 0", "s_cbranch_scc1 .Lloop_%="]
@@ -316,6 +323,8 @@ def main():
     out += emit("KODR_BS_MAIN_NDNL", main_loop(False, False))
     # tuning: the loop without the priority rotation (MODE 10)
     out += emit("KODR_BS_MAIN_NOPRIO", main_loop(True, True, None))
+    out += emit("KODR_BS_MAIN_HALF", main_loop(True, True, ROW_PRIO, lambda j: (j + 2) % 4))
+    out += emit("KODR_BS_MAIN_HALF2", main_loop(True, True, lambda j: (2 * j) % 4, lambda j: (2 * j + 1) % 4))
     out += emit("KODR_BS_DUMP", dump_lines())
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)

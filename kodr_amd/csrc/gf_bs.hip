@@ -243,6 +243,10 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       KODR_BS_ASM(KODR_BS_MAIN_NDNL);
     } else if constexpr (MODE == 10) {
       KODR_BS_ASM(KODR_BS_MAIN_NOPRIO);
+    } else if constexpr (MODE == 11) {
+      KODR_BS_ASM(KODR_BS_MAIN_HALF);
+    } else if constexpr (MODE == 12) {
+      KODR_BS_ASM(KODR_BS_MAIN_HALF2);
     } else if constexpr (MODE == 6) {
       KODR_BS_ASM(KODR_BS_MAIN_NL);
     } else {
@@ -458,7 +462,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     return mode == 3 ? KODR_BS_CALL(KW_, 3) : mode == 5 ? KODR_BS_CALL(KW_, 5)                    \
          : mode == 4 ? KODR_BS_CALL(KW_, 4) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
          : mode == 8 ? KODR_BS_CALL(KW_, 8) : mode == 9 ? KODR_BS_CALL(KW_, 9)                    \
-         : mode == 10 ? KODR_BS_CALL(KW_, 10) : KODR_BS_CALL(KW_, 0);
+         : mode == 10 ? KODR_BS_CALL(KW_, 10) : mode == 11 ? KODR_BS_CALL(KW_, 11)                \
+         : mode == 12 ? KODR_BS_CALL(KW_, 12) : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

@@ -7,6 +7,7 @@ import re
 import sys
 
 import numpy as np
+import pytest
 
 import oracle
 
@@ -117,7 +118,7 @@ class _Wave:
     BASE = 0x7F12_3456_0000
     VEC = (gen.PG, gen.PGN, gen.PL)                # registers modelled per lane
 
-    def __init__(self, X, A, nr):
+    def __init__(self, X, A, nr, loop=None):
         self.X, self.A, self.nr = X, A, nr          # X: nr x 32 bytes, A: 8 x nr
         offs, _ = gen.body_offsets()
         self.code, self.addr = [], {}
@@ -126,7 +127,8 @@ class _Wave:
                 self.addr[self.BASE + offs[r * 256 + c]] = len(self.code)
                 self.code += gen.body_lines(c, r)
         self.main0 = len(self.code)
-        self.code += [ln.replace("_%=", "") for ln in gen.main_loop(True)] + ["END"]
+        loop = gen.main_loop(True) if loop is None else loop
+        self.code += [ln.replace("_%=", "") for ln in loop] + ["END"]
         self.labels = {ln[:-1]: i for i, ln in enumerate(self.code) if ln.endswith(":")}
         for name, i in self.labels.items():          # main code at fake addresses
             self.addr[0x1000_0000 + 4 * i] = i
@@ -237,13 +239,21 @@ class _Wave:
         return np.array([[self.v[gen.ACC + 8 * m + j] for j in range(8)] for m in range(8)], np.uint32)
 
 
-def test_threaded_dispatch_end_to_end_vs_oracle():
+# the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-12)
+LOOPS = {"main": lambda: gen.main_loop(True),
+         "noprio": lambda: gen.main_loop(True, True, None),
+         "half": lambda: gen.main_loop(True, True, gen.ROW_PRIO, lambda j: (j + 2) % 4),
+         "half2": lambda: gen.main_loop(True, True, lambda j: 2 * j % 4, lambda j: (2 * j + 1) % 4)}
+
+
+@pytest.mark.parametrize("variant", sorted(LOOPS))
+def test_threaded_dispatch_end_to_end_vs_oracle(variant):
     rng = np.random.default_rng(11)
     for nr in (8, 16, 24):
         X = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
         A = rng.integers(0, 256, (8, nr), dtype=np.uint8)
         A[0, 0], A[5, 1] = 0, 1                      # empty body, identity body
-        acc = _Wave(X, A, nr).run()
+        acc = _Wave(X, A, nr, LOOPS[variant]()).run()
         for m in range(8):
             got = bitslice_np(acc[m].view(np.uint8).copy())
             exp = np.zeros(32, np.uint8)
