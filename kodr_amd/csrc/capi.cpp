@@ -602,15 +602,24 @@ int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wir
   size_t n_sys = 0;
   if (e->kind == RLNC_SYSTEMATIC && e->sys_next < k) n_sys = std::min(count, k - e->sys_next);
   HIPC(kodr_amd::fill_vectors(d_wire, wire_pitch, count, k, e->seed, e->drawn, n_sys, e->sys_next, st));
-  // the vectors are read in place as the coefficient matrix (lda = wire_pitch)
-  if ((k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0) {
-    TRY(gemm_resident(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch,
-                      d_wire + k, wire_pitch, L));
+  // the systematic pieces are the pieces themselves (e_id x P = P_id): one
+  // strided copy of rows sys_next.., no GF product
+  if (n_sys)
+    HIPC(hipMemcpy2DAsync(d_wire + k, wire_pitch, e->pieces.p + e->sys_next * e->pitch, e->pitch, L, n_sys,
+                          hipMemcpyDeviceToDevice, st));
+  // the coded rows' vectors are read in place as the coefficient matrix
+  // (lda = wire_pitch)
+  const size_t nc = count - n_sys;
+  uint8_t* w0 = d_wire + n_sys * wire_pitch;
+  if (!nc) {
+  } else if ((k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0) {
+    TRY(gemm_resident(e->ctx, w0, wire_pitch, nc, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch, w0 + k,
+                      wire_pitch, L));
   } else {  // piece columns not 16-byte aligned: compute aside, then one strided copy
-    TRY(e->out.reserve(count * e->pitch));
-    TRY(gemm_resident(e->ctx, d_wire, wire_pitch, count, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch,
-                      e->out.p, e->pitch, L));
-    HIPC(hipMemcpy2DAsync(d_wire + k, wire_pitch, e->out.p, e->pitch, L, count, hipMemcpyDeviceToDevice, st));
+    TRY(e->out.reserve(nc * e->pitch));
+    TRY(gemm_resident(e->ctx, w0, wire_pitch, nc, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch, e->out.p,
+                      e->pitch, L));
+    HIPC(hipMemcpy2DAsync(w0 + k, wire_pitch, e->out.p, e->pitch, L, nc, hipMemcpyDeviceToDevice, st));
   }
   e->sys_next += n_sys;
   e->drawn += count;
