@@ -442,8 +442,17 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
     return hipErrorInvalidValue;
-  const BsPlan p = plan_gemm_bs(M, K, ncols);
+  BsPlan p = plan_gemm_bs(M, K, ncols);
   if (!p.ok) return hipErrorInvalidValue;
+#ifdef KODR_TUNE_MODES
+  if (const char* env = getenv("KODR_BS_KW")) {  // force the waves per workgroup
+    const int kw = atoi(env);
+    const long kpad = ((long)K + kBsChunk - 1) / kBsChunk * kBsChunk;
+    p.kw = kw;
+    p.rpw = (int)(((kpad + kw - 1) / kw + kBsChunk - 1) / kBsChunk * kBsChunk);
+    p.lds_bytes = bs_lds_bytes(kw, p.rpw);
+  }
+#endif
   const BsDevice* bd = nullptr;
   hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;
