@@ -503,16 +503,18 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):
         gf, cp = ctypes.c_size_t(), ctypes.c_size_t()
         errors.check(L_.rlnc_decoder_apply_stats(dh, ctypes.byref(gf), ctypes.byref(cp)))
         decoded = bool(L_.rlnc_decoder_is_decoded(dh))
+        bs = bool(L_.rlnc_decoder_last_apply_bitsliced(dh))
         recv = L_.rlnc_decoder_received(dh)
         L_.rlnc_decoder_destroy(dh)
         if best is None or t2 - t0 < best["s"]:
             best = {"s": round(t2 - t0, 6), "add_s": round(t1 - t0, 6), "get_s": round(t2 - t1, 6),
-                    "gf_rows": gf.value, "copy_rows": cp.value, "received": recv, "decoded": decoded}
+                    "gf_rows": gf.value, "copy_rows": cp.value, "received": recv, "decoded": decoded, "bs": bs}
     macs = best["gf_rows"] * best["received"] * L
     best["apply_gf_macs"] = macs
     best["apply_gf_macs_per_s"] = float(f"{macs / best['get_s']:.4g}")
-    mpi = MACS_PER_INST_BS if best["gf_rows"] >= 16 else MACS_PER_INST_PERM
-    best["apply_kernel"] = "gf_bs_kernel" if best["gf_rows"] >= 16 else "gf_gemm_kernel"
+    bs = best.pop("bs")
+    mpi = MACS_PER_INST_BS if bs else MACS_PER_INST_PERM
+    best["apply_kernel"] = "gf_bs_kernel" if bs else "gf_gemm_kernel"
     best["issue_ceiling_macs_per_s"] = float(f"{ISSUE_PER_S * mpi:.4g}")
     return best
 

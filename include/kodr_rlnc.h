@@ -223,6 +223,9 @@ int rlnc_decoder_coefficients(const rlnc_decoder* dec, uint8_t* out);
 /* rows of the last data-side materialization (GetPiece/GetPieces) that went
  * through the GF kernel vs were plain copies of received systematic pieces */
 int rlnc_decoder_apply_stats(const rlnc_decoder* dec, size_t* gf_rows, size_t* copy_rows);
+/* 1 if the last materialization's GF product ran on the bit-sliced kernel
+ * (gf_bs_kernel), 0 for the v_perm kernel or no GF rows (diagnostics) */
+int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* dec);
 int rlnc_decoder_transform(const rlnc_decoder* dec, uint8_t* out);
 
 /* ---- raw kernel entry: Y = A (x) X over GF(2^8) ------------------------ */

@@ -85,6 +85,7 @@ SIGNATURES = {
     "rlnc_decoder_get_pieces_device": (_int, [_vp, _vp, _sz]),
     "rlnc_decoder_coefficients": (_int, [_vp, _u8p]),
     "rlnc_decoder_apply_stats": (_int, [_vp, _szp, _szp]),
+    "rlnc_decoder_last_apply_bitsliced": (_int, [_vp]),
     "rlnc_decoder_transform": (_int, [_vp, _u8p]),
     "rlnc_gf_matmul_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
     "rlnc_bitslice_device": (_int, [_vp, _vp, _sz, _sz, _sz]),

@@ -129,8 +129,9 @@ struct rlnc_decoder {
   std::vector<uint8_t> hvecs;  // coding vectors of a device batch
   std::vector<uint8_t> hTc;    // transform rows that need GF work
   std::vector<const uint8_t*> hsrc;  // per output row: source row of the gather
-  DevBuf scratch, srcs;        // GF rows before the gather; device copy of hsrc
+  DevBuf scratch;              // GF rows before the gather
   size_t last_gf_rows = 0, last_copy_rows = 0;
+  bool last_bs = false;         // the last GF product ran on the bit-sliced kernel
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -200,9 +201,14 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
 // B = 1 at 32 MiB/256 against 9 us; B = 8: 17-19 against 16 us; B = 10: 20
 // against 28 us; profiles/r01/bs_min_rows.log).
 constexpr size_t kBsMinRows = 9;
-// The decoder builds its twin per materialization (one more pass over the
-// received rows), so the bit-sliced kernel must save more than that pass.
+// The decoder builds its twin per materialization (one pass over the rows
+// received since the last one).  From 16 rows the bit-sliced kernel always
+// wins; from 9 rows it wins when that pass is short: 12 GF rows at 16 MiB/128
+// take 28 us on gf_gemm, 10 us + 9 us of twin on the bit-sliced path, while at
+// 32 MiB/256 a fresh twin costs 15 us and gf_gemm keeps the edge
+// (profiles/r01/dec_get.log).
 constexpr size_t kBsMinRowsDecode = 16;
+constexpr size_t kBsTwinBudget = 16u << 20;  // bytes of new twin rows worth building for 9..15 rows
 
 // Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
@@ -739,7 +745,7 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
   if (!d) return RLNC_ERR_OUT_OF_MEMORY;
   d->ctx = ctx;
   if (ctx)
-    for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch, &d->srcs})
+    for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch})
       b->bind(ctx->device, ctx->stream);
   *out = d;
   return RLNC_OK;
@@ -756,7 +762,6 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   d->decoded.release();
   d->rowbuf.release();
   d->scratch.release();
-  d->srcs.release();
   d->recv_bs.release();
   delete d;
   return RLNC_OK;
@@ -822,13 +827,16 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
 int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t ldy) {
   const size_t recv = d->core.received();
   rlnc_ctx* ctx = d->ctx;
-  size_t min_rows = kBsMinRowsDecode;
+  const size_t twin_ok = d->recv_bs.cap >= d->recv_rows * d->pitch ? std::min(d->bs_rows, recv) : 0;
+  size_t min_rows = (recv - twin_ok) * d->pitch <= kBsTwinBudget ? kBsMinRows : kBsMinRowsDecode;
 #ifdef KODR_TUNE_MODES
   if (const char* env = getenv("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
 #endif
+  d->last_bs = false;
   if (M < min_rows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
       !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
+  d->last_bs = true;
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
     TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
     d->bs_rows = 0;
@@ -872,23 +880,24 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
     HIPC(d->ctx->stage.h2d(d->tmat.p, recv, trows, recv, recv, rows, st));
     return dec_gemm(d, d->tmat.p, rows, dst, dpitch);
   }
-  if (m) {
-    d->hTc.resize(m * recv);
-    TRY(d->scratch.reserve(m * d->pitch));
-    for (size_t i = 0, t = 0; i < rows; i++)
-      if (!d->hsrc[i]) {
-        memcpy(d->hTc.data() + t * recv, trows + i * recv, recv);
-        d->hsrc[i] = d->scratch.p + t * d->pitch;
-        t++;
-      }
-    TRY(d->tmat.reserve(m * recv));
-    HIPC(d->ctx->stage.h2d(d->tmat.p, recv, d->hTc.data(), recv, recv, m, st));
-    TRY(dec_gemm(d, d->tmat.p, m, d->scratch.p, d->pitch));
-  }
-  const size_t tb = rows * sizeof(uint8_t*);
-  TRY(d->srcs.reserve(tb));
-  HIPC(d->ctx->stage.h2d(d->srcs.p, tb, reinterpret_cast<const uint8_t*>(d->hsrc.data()), tb, tb, 1, st));
-  HIPC(kodr_amd::gather_rows(reinterpret_cast<const uint8_t* const*>(d->srcs.p), dst, dpitch, rows, d->L, st));
+  // one upload ahead of both kernels: [the m GF rows of T | the gather's
+  // source-row table].  A small H2D costs ~15-20 us of DMA latency, so a
+  // second one between the kernels would stall the stream.
+  const size_t tbytes = (m * recv + 15) / 16 * 16, pbytes = rows * sizeof(uint8_t*);
+  if (m) TRY(d->scratch.reserve(m * d->pitch));
+  d->hTc.resize(tbytes + pbytes);
+  for (size_t i = 0, t = 0; i < rows; i++)
+    if (!d->hsrc[i]) {
+      memcpy(d->hTc.data() + t * recv, trows + i * recv, recv);
+      d->hsrc[i] = d->scratch.p + t * d->pitch;
+      t++;
+    }
+  memcpy(d->hTc.data() + tbytes, d->hsrc.data(), pbytes);
+  TRY(d->tmat.reserve(tbytes + pbytes));
+  HIPC(d->ctx->stage.h2d(d->tmat.p, tbytes + pbytes, d->hTc.data(), tbytes + pbytes, tbytes + pbytes, 1, st));
+  if (m) TRY(dec_gemm(d, d->tmat.p, m, d->scratch.p, d->pitch));
+  HIPC(kodr_amd::gather_rows(reinterpret_cast<const uint8_t* const*>(d->tmat.p + tbytes), dst, dpitch, rows, d->L,
+                             st));
   return RLNC_OK;
 }
 
@@ -1025,6 +1034,8 @@ int rlnc_decoder_apply_stats(const rlnc_decoder* d, size_t* gf_rows, size_t* cop
   *copy_rows = d->last_copy_rows;
   return RLNC_OK;
 }
+
+int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* d) { return d && d->last_bs ? 1 : 0; }
 
 int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;

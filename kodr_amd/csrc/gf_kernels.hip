@@ -314,6 +314,33 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* const* 
 
 }  // namespace
 
+namespace {
+
+// dst (pitch dpitch) = width x rows bytes read straight from host-mapped
+// pinned memory (contiguous rows).  Small uploads only: a kernel's reads over
+// PCIe start with the dispatch, where a DMA engine's copy is followed by a
+// ~11 us cross-engine wait before the next kernel (profiles/r01/upload.log).
+__global__ __launch_bounds__(256) void upload_small_kernel(const uint8_t* __restrict__ src,
+                                                          uint8_t* __restrict__ dst, size_t dpitch,
+                                                          int width, int total) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int r = i / width, c = i - r * width;
+  dst[(size_t)r * dpitch + c] = src[i];
+}
+
+}  // namespace
+
+hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, size_t width, size_t rows,
+                        hipStream_t stream) {
+  if (!width || !rows) return hipSuccess;
+  const size_t total = width * rows;
+  if (total > kUploadSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(upload_small_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src_mapped,
+                     dst, dpitch, (int)width, (int)total);
+  return hipGetLastError();
+}
+
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;

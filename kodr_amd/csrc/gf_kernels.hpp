@@ -21,6 +21,13 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
                    const GemmConfig* force = nullptr);
 
+// dst (pitch dpitch) = width x rows contiguous bytes of host-mapped pinned
+// memory (a device pointer of a hipHostMalloc buffer), copied by a kernel
+// rather than a DMA engine.  width x rows <= kUploadSmallMax.
+constexpr size_t kUploadSmallMax = 64 * 1024;
+hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, size_t width, size_t rows,
+                        hipStream_t stream);
+
 // dY row r = the first ncols bytes of device row d_src[r] (d_src: device array
 // of rows pointers, 16-byte aligned).  rows <= 65535.
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,

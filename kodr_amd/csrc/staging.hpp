@@ -11,6 +11,8 @@
 
 #include <algorithm>
 
+#include "gf_kernels.hpp"
+
 namespace kodr_amd {
 
 class Staging {
@@ -28,6 +30,16 @@ class Staging {
     }
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
+    if (width * height <= kUploadSmallMax) {  // coefficients, row tables: a kernel reads the pinned chunk
+      const int b = next_;
+      next_ ^= 1;
+      if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+      pack(buf_[b], width, src, spitch, width, height);
+      if ((e = upload_small(dev_[b], dst, dpitch, width, height, s)) != hipSuccess) return e;
+      if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
+      pending_[b] = true;
+      return hipSuccess;
+    }
     if (width > kChunk) {  // rows wider than a chunk: each row as chunk-wide segments
       for (size_t r = 0; r < height; r++) {
         const size_t full = width / kChunk, tail = width - full * kChunk;
@@ -119,6 +131,7 @@ class Staging {
       if (buf_[b]) (void)hipHostFree(buf_[b]);
       ev_[b] = nullptr;
       buf_[b] = nullptr;
+      dev_[b] = nullptr;
       pending_[b] = false;
     }
   }
@@ -129,6 +142,7 @@ class Staging {
     for (int b = 0; b < 2; b++) {
       hipError_t e = hipHostMalloc((void**)&buf_[b], kChunk, hipHostMallocDefault);
       if (e != hipSuccess) return e;
+      if ((e = hipHostGetDevicePointer((void**)&dev_[b], buf_[b], 0)) != hipSuccess) return e;
       if ((e = hipEventCreateWithFlags(&ev_[b], hipEventDisableTiming)) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -142,6 +156,7 @@ class Staging {
   }
 
   uint8_t* buf_[2] = {nullptr, nullptr};
+  uint8_t* dev_[2] = {nullptr, nullptr};  // the same chunks as the device sees them
   hipEvent_t ev_[2] = {nullptr, nullptr};
   bool pending_[2] = {false, false};
   int next_ = 0;

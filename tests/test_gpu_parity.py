@@ -697,3 +697,28 @@ def test_contexts_on_threads_run_concurrently(gpu_ctx):
         t.join(120)
     assert not any(t.is_alive() for t in ts)
     assert not errs, errs
+
+
+@pytest.mark.parametrize("k,lost,bs", [(128, 12, True), (256, 12, False), (256, 20, True), (64, 5, False)])
+def test_decoder_kernel_choice_and_result(gpu_ctx, k, lost, bs):
+    """Systematic decode with `lost` pieces replaced by coded ones: the GF
+    rows run on the bit-sliced kernel from 16 rows, or from 9 rows when the
+    twin to build is at most 16 MiB (capi.cpp dec_gemm); bytes equal P
+    either way."""
+    L = 131072
+    rng = np.random.default_rng(k + lost)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P, SYSTEMATIC)
+    errors.check(_lib.lib().rlnc_encoder_seed(e.h, 9))
+    W = _wire_device(gpu_ctx, e, k + lost + 4, k + L)
+    drop = set(rng.choice(k, lost, replace=False).tolist())
+    rows = np.ascontiguousarray(W[[i for i in range(k) if i not in drop] + list(range(k, W.shape[0]))])
+    d = Dec(gpu_ctx, k)
+    st, used = _add_rows(d, ptr(rows), rows.shape[0], k + L, False)
+    assert st in (0, 3) and used >= k
+    st, dec = d.get_all()
+    assert st == 0 and np.array_equal(dec, P)
+    gf_rows, copy_rows = ctypes.c_size_t(), ctypes.c_size_t()
+    errors.check(_lib.lib().rlnc_decoder_apply_stats(d.h, ctypes.byref(gf_rows), ctypes.byref(copy_rows)))
+    assert (gf_rows.value, copy_rows.value) == (lost, k - lost)
+    assert bool(_lib.lib().rlnc_decoder_last_apply_bitsliced(d.h)) == bs
