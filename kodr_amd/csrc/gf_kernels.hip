@@ -329,7 +329,27 @@ __global__ __launch_bounds__(256) void upload_small_kernel(const uint8_t* __rest
   dst[(size_t)r * dpitch + c] = src[i];
 }
 
+// the reverse: dst (host-mapped pinned, contiguous rows) = width x rows bytes
+// of device memory at pitch spitch
+__global__ __launch_bounds__(256) void download_small_kernel(const uint8_t* __restrict__ src, size_t spitch,
+                                                            uint8_t* __restrict__ dst, int width, int total) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int r = i / width, c = i - r * width;
+  dst[i] = src[(size_t)r * spitch + c];
+}
+
 }  // namespace
+
+hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped, size_t width, size_t rows,
+                          hipStream_t stream) {
+  if (!width || !rows) return hipSuccess;
+  const size_t total = width * rows;
+  if (total > kUploadSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(download_small_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src,
+                     spitch, dst_mapped, (int)width, (int)total);
+  return hipGetLastError();
+}
 
 hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, size_t width, size_t rows,
                         hipStream_t stream) {

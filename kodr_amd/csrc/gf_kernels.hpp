@@ -27,6 +27,10 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
 constexpr size_t kUploadSmallMax = 64 * 1024;
 hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, size_t width, size_t rows,
                         hipStream_t stream);
+// the reverse: width x rows bytes of device memory (pitch spitch) into
+// host-mapped pinned memory, contiguous rows
+hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped, size_t width, size_t rows,
+                          hipStream_t stream);
 
 // dY row r = the first ncols bytes of device row d_src[r] (d_src: device array
 // of rows pointers, 16-byte aligned).  rows <= 65535.

@@ -4,6 +4,10 @@
 // one chunk overlap the CPU copy of the next, instead of the driver's slow
 // pageable path.  Host pointers are never retained: h2d returns once the
 // bytes are in pinned memory, d2h once they are in the caller's buffer.
+// Transfers of at most kUploadSmallMax bytes (coefficients, transforms, row
+// tables) are moved by a kernel that reads or writes the pinned chunk through
+// its device mapping: a DMA copy that small is all latency, and the next
+// kernel waits ~11 us more for the copy engine (profiles/r01/dec_get.log).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -74,6 +78,17 @@ class Staging {
     }
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
+    if (width * height <= kUploadSmallMax) {  // coding vectors of a batch: a kernel writes the pinned chunk
+      const int b = next_;
+      next_ ^= 1;
+      if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+      if ((e = download_small(src, spitch, dev_[b], width, height, s)) != hipSuccess) return e;
+      if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
+      if ((e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+      pending_[b] = false;
+      pack(dst, dpitch, buf_[b], width, width, height);
+      return hipSuccess;
+    }
     if (width > kChunk) {
       for (size_t r = 0; r < height; r++) {
         const size_t full = width / kChunk, tail = width - full * kChunk;
