@@ -26,6 +26,15 @@ st = ctypes.c_void_p(ctx.stream)
 def model(t, mode, nb, dyn, ncopy=8):
     x = [int(inp[(t * 8 + i) & 4095]) for i in range(8)]
     acc = [0] * 64
+    if mode == "W":  # 4 rows, two blocks per lane (the second = words rotated by one)
+        x2 = [x[(i + 1) % 8] for i in range(8)]
+        for m in range(4):
+            c = (5 * m + 3 + 232) % nb
+            for j in range(8):
+                a, b = planes(c, j)
+                acc[16 * m + j] ^= x[a - X] ^ x[b - X]
+                acc[16 * m + 8 + j] ^= x2[a - X] ^ x2[b - X]
+        return [acc[r] ^ acc[r + 16] ^ acc[r + 32] ^ acc[r + 48] for r in range(16)]
     for m0 in range(8):
         m = m0 % ncopy
         c = (5 * m0 + 3 + 232) % nb if mode == "T" else coef(m0, nb, 1 if dyn else None)

@@ -35,6 +35,15 @@ def body_xors(c, accbase):
     return out
 
 
+def body_xors_hi(c, accbase):
+    """The same body on the lane's second block (planes X+8..X+15)."""
+    out = []
+    for j in range(8):
+        a, b = planes(c, j)
+        out.append(f"v_bitop3_b32 v{accbase + j}, v{accbase + j}, v{a + 8}, v{b + 8} bitop3:0x96")
+    return out
+
+
 def coef(m, nb=NB, it=None):
     if it is None:
         return (5 * m + 3) % nb
@@ -96,8 +105,14 @@ __global__ __launch_bounds__(256) void {name}(uint32_t* out, const uint32_t* in,
 def kernel(name, mode, nb=NB, dyn=False, ncopy=8):
     L = []
     B = L.append
+    wide = mode == "W"
+    if wide:
+        mode = "T"
     for i in range(8):
         B(f"v_mov_b32 v{X + i}, %[x{i}]")
+    if wide:  # second 32-byte block of the lane: the same words rotated by one
+        for i in range(8):
+            B(f"v_mov_b32 v{X + 8 + i}, %[x{(i + 1) % 8}]")
     for r in range(ACC, ACC + 64):
         B(f"v_mov_b32 v{r}, 0")
     B("s_mov_b32 %[cnt], %[iters]")
@@ -144,12 +159,12 @@ def kernel(name, mode, nb=NB, dyn=False, ncopy=8):
     B(".Lloop_%=:")
     if mode == "T":
         R = ncopy
-        for ps in range(8 // R):
+        for ps in range((4 if wide else 8) // R):
             for r in range(R):
                 m = ps * R + r
                 B(f"s_add_u32 s{78 + m}, s{78 + m}, 232")
                 B(f"s_and_b32 s{78 + m}, s{78 + m}, {nb - 1}")
-                B(f"s_mul_i32 s92, s{78 + m}, 68")
+                B(f"s_mul_i32 s92, s{78 + m}, {132 if wide else 68}")  # body bytes: 8 or 16 XOR3 + s_setpc
                 B(f"s_add_u32 s{60 + 2 * r}, s92, s{34 + r}")
                 B(f"s_addc_u32 s{61 + 2 * r}, s91, 0")
             B(f"s_add_u32 s{60 + 2 * R}, s90, .Lret{ps}_%= - .Lpc_%=")
@@ -236,7 +251,11 @@ def kernel(name, mode, nb=NB, dyn=False, ncopy=8):
         for r in range(ncopy):
             for c in range(nb):
                 B(f".Lt{r}_{c}_%=:")
-                L.extend(body_xors(c, ACC + 8 * r))
+                if wide:
+                    L.extend(body_xors(c, ACC + 16 * r))
+                    L.extend(body_xors_hi(c, ACC + 16 * r + 8))
+                else:
+                    L.extend(body_xors(c, ACC + 8 * r))
                 B(f"s_setpc_b64 s[{62 + 2 * r}:{63 + 2 * r}]")
     if mode == "G":
         for c in range(nb):
@@ -256,7 +275,7 @@ def kernel(name, mode, nb=NB, dyn=False, ncopy=8):
         B(f"v_xor_b32 %[r{r}], v{ACC + r}, v{ACC + r + 48}")
     asm = "\\n\\t".join(L)
     outs = ", ".join(f'[r{r}] "=v"(res[{r}])' for r in range(16))
-    clob_v = ", ".join(f'"v{r}"' for r in range(ACC, X + 8))
+    clob_v = ", ".join(f'"v{r}"' for r in range(ACC, X + (16 if wide else 8)))
     clob_s = ", ".join(f'"s{r}"' for r in list(range(34, 50)) + list(range(60, 88)) + list(range(90, 100)))
     ins = ", ".join(f'[x{i}] "v"(xin[{i}])' for i in range(8))
     return f'''
@@ -282,7 +301,8 @@ GSIZE = 4 + 64 + 4 + 4
 VARIANTS = [("S", "S", NB, False), ("A", "A", NB, False), ("B", "B", NB, False), ("C", "C", NB, False),
             ("D", "D", NB, False), ("T16r8", "T", 16, True, 8), ("T256r8", "T", 256, True, 8),
             ("T256r4", "T", 256, True, 4), ("T16r4", "T", 16, True, 4), ("T128r8", "T", 128, True, 8),
-            ("T64r8", "T", 64, True, 8), ("bank_ok", "BANK", 0, False), ("bank_conflict", "BANK", 1, False)]
+            ("T64r8", "T", 64, True, 8), ("bank_ok", "BANK", 0, False), ("bank_conflict", "BANK", 1, False),
+            ("W256r4", "W", 256, True, 4), ("W16r4", "W", 16, True, 4)]
 
 
 def main():
