@@ -722,3 +722,31 @@ def test_decoder_kernel_choice_and_result(gpu_ctx, k, lost, bs):
     errors.check(_lib.lib().rlnc_decoder_apply_stats(d.h, ctypes.byref(gf_rows), ctypes.byref(copy_rows)))
     assert (gf_rows.value, copy_rows.value) == (lost, k - lost)
     assert bool(_lib.lib().rlnc_decoder_last_apply_bitsliced(d.h)) == bs
+
+
+@pytest.mark.parametrize("count", [255, 256, 257])
+def test_host_vectors_across_small_upload_limit(gpu_ctx, count):
+    """count x k coefficient bytes around the 64 KiB limit where staging
+    switches from the upload kernel to a DMA copy (staging.hpp): the coded
+    pieces match the oracle on both sides, and a device batch decode whose
+    vectors come back through the small-download kernel decodes."""
+    k, L = 256, 96
+    rng = np.random.default_rng(count)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    e = Enc(gpu_ctx, P)
+    V, out = e.code(rng.integers(0, 256, (count, k), dtype=np.uint8))
+    assert np.array_equal(out[:, :k], V)
+    assert np.array_equal(out[:, k:], oracle.encode(P, V))
+    rows = np.ascontiguousarray(out)
+    d_rows = gpu_ctx.alloc(rows.nbytes)
+    try:
+        gpu_ctx.h2d(d_rows, rows)
+        d = Dec(gpu_ctx, k)
+        st, used = _add_rows(d, ctypes.c_void_p(d_rows), count, k + L, True)
+        ref = oracle.Decoder(k)
+        for r in rows[:used]:
+            ref.add(r[:k], r[k:])
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+    finally:
+        gpu_ctx.synchronize()
+        gpu_ctx.free(d_rows)
