@@ -617,11 +617,11 @@ int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wir
   // (lda = wire_pitch)
   const size_t nc = count - n_sys;
   uint8_t* w0 = d_wire + n_sys * wire_pitch;
-  if (!nc) {
-  } else if ((k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0) {
+  const bool aligned = (k % 16) == 0 && (wire_pitch % 16) == 0 && ((uintptr_t)d_wire % 16) == 0;
+  if (nc && aligned) {
     TRY(gemm_resident(e->ctx, w0, wire_pitch, nc, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch, w0 + k,
                       wire_pitch, L));
-  } else {  // piece columns not 16-byte aligned: compute aside, then one strided copy
+  } else if (nc) {  // piece columns not 16-byte aligned: compute aside, then one strided copy
     TRY(e->out.reserve(nc * e->pitch));
     TRY(gemm_resident(e->ctx, w0, wire_pitch, nc, k, e->pieces.p, e->pieces_bs, e->bs_valid, e->pitch, e->out.p,
                       e->pitch, L));
