@@ -954,15 +954,8 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
     HIPC(hipMemcpy2DAsync(d->recv.p + row0 * d->pitch, d->pitch, rows + k, pitch, d->L, count,
                           hipMemcpyHostToDevice, d->ctx->stream));
   }
-  int st = RLNC_OK;
   size_t n = 0;
-  for (; n < count; n++) {
-    if (d->core.is_decoded()) {
-      st = RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;
-      break;
-    }
-    if ((st = d->core.add(vecs + n * vpitch)) != RLNC_OK) break;
-  }
+  const int st = d->core.add_many(vecs, vpitch, count, &n);  // == count calls of AddPiece
   if (n) d->decoded_ready = false;
   // data side: the accepted pieces are consecutive received rows -> one 2D copy
   if (early)

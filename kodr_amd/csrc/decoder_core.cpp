@@ -66,6 +66,99 @@ int DecoderCore::add(const uint8_t* vec) {
   return 0;
 }
 
+int DecoderCore::add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* used) {
+  size_t i = 0;
+  int st = 0;
+  while (i < n) {
+    if (is_decoded()) {
+      st = 3;  // full/decoder.go:52-54
+      break;
+    }
+    const size_t np = std::min(std::min<size_t>(4, n - i), k_ - rows_.size());
+    if (all_clean_ && received_ >= 1 && np >= 2) {
+      const size_t c = add_panel(vecs + i * pitch, pitch, np);
+      i += c;
+      if (c == np) continue;
+      // row i is not a diagonal pivot: it takes the literal path below
+    }
+    if ((st = add(vecs + i * pitch)) != 0) break;
+    i++;
+  }
+  *used = i;
+  return st;
+}
+
+// np new rows on a state of r diagonal pivots [I_r | X] (all_clean_), as np
+// successive rref_clean() calls would add them.  While every new row keeps a
+// non-zero diagonal the end state is the reduced row echelon form of
+// [coefficients | identity over received rows] with pivots in columns
+// 0..r+np-1, which is unique, so the order of the row operations is free:
+//  1. each new row drops its columns < r against the old pivots (one pass
+//     over the old rows for all new rows);
+//  2. the new rows are eliminated among themselves in arrival order; the
+//     first whose diagonal is then 0 ends the panel (it and those after it go
+//     through add() as usual, from their original vectors);
+//  3. the old rows drop the c accepted pivot columns (one rank-c pass).
+// Returns c, the rows accepted.
+size_t DecoderCore::add_panel(const uint8_t* vecs, size_t pitch, size_t np) {
+  const hostgf::Tables& t = T();
+  const size_t r = rows_.size(), m0 = received_;
+  ensure_tcap(m0 + np);
+  const size_t width = k_ + m0 + np;
+  uint8_t* pr[4];
+  for (size_t p = 0; p < np; p++) {
+    pr[p] = free_.back();
+    free_.pop_back();
+    memcpy(pr[p], vecs + p * pitch, k_);
+    memset(pr[p] + k_, 0, tcap_);
+    pr[p][k_ + m0 + p] = 1;  // T row = e_(received index)
+  }
+  uint8_t* vp[4];
+  if (r) {
+    qbuf_.resize(np * r);
+    ptrs_.resize(r);
+    for (size_t p = 0; p < np; p++) {
+      memcpy(qbuf_.data() + p * r, pr[p], r);
+      vp[p] = pr[p] + r;
+    }
+    for (size_t i = 0; i < r; i++) ptrs_[i] = rows_[i] + r;
+    hostgf::accumulate_multi(vp, np, ptrs_.data(), qbuf_.data(), r, r, width - r);
+    for (size_t p = 0; p < np; p++) memset(pr[p], 0, r);
+  }
+  size_t c = np;
+  for (size_t p = 0; p < np; p++) {
+    for (size_t q = 0; q < p; q++) {
+      const uint8_t f = pr[p][r + q];
+      if (f) hostgf::axpy(pr[p] + r + q, pr[q] + r + q, width - r - q, f);
+    }
+    const uint8_t d = pr[p][r + p];
+    if (!d) {
+      c = p;
+      break;
+    }
+    if (d != 1) hostgf::scale(pr[p] + r + p, width - r - p, t.inv(d));
+    for (size_t q = 0; q < p; q++) {
+      const uint8_t f = pr[q][r + p];
+      if (f) hostgf::axpy(pr[q] + r + p, pr[p] + r + p, width - r - p, f);
+    }
+  }
+  if (c && r) {
+    qbuf_.resize(r * c);
+    for (size_t j = 0; j < r; j++)
+      for (size_t p = 0; p < c; p++) qbuf_[j * c + p] = rows_[j][r + p];
+    for (size_t p = 0; p < c; p++) vp[p] = pr[p] + r;
+    hostgf::rank_multi(ptrs_.data(), qbuf_.data(), r, vp, c, width - r);
+  }
+  for (size_t p = np; p-- > c;) free_.push_back(pr[p]);
+  for (size_t p = 0; p < c; p++) {
+    rows_.push_back(pr[p]);
+    clean_[r + p] = 1;
+  }
+  received_ += c;
+  useful_ = rows_.size();
+  return c;
+}
+
 // Rref (:178-182) on a state whose rows 0..R-2 are the output of the previous
 // Rref and row R-1 is the new piece.
 void DecoderCore::rref() {

@@ -28,6 +28,11 @@ class DecoderCore {
   // received piece number received(); returns 0 or kodr's
   // ErrAllUsefulPiecesReceived (3).
   int add(const uint8_t* vec);
+  // the same as n calls of add() on rows vecs + i * pitch, stopping at the
+  // first call that does not return 0; *used = rows accepted.  Runs of rows
+  // that stay diagonal pivots are eliminated 4 at a time (one pass over the
+  // existing rows per 4 new ones); the result is the same state.
+  int add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* used);
 
   bool is_decoded() const { return useful_ >= k_; }   // full/decoder.go:32-34
   size_t required() const { return k_ - useful_; }    // full/decoder.go:38-40
@@ -49,6 +54,7 @@ class DecoderCore {
  private:
   void rref();
   void rref_clean();
+  size_t add_panel(const uint8_t* vecs, size_t pitch, size_t np);
   void update_clean();
   void ensure_tcap(size_t need);
   void axpy_row(size_t dst, size_t src, uint8_t q, size_t from);

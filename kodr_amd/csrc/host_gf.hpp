@@ -212,6 +212,87 @@ __attribute__((target("avx512f,avx512bw,gfni"))) inline void rank1_gfni512(
 }
 #endif
 
+#if defined(__x86_64__)
+// v[p][0..n) ^= XOR_i q[p * ldq + i] * rows[i][0..n) for p < P: every block of
+// a source row is loaded once for all P outputs (256 B of each output in
+// registers at a time)
+template <int P>
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void accumulate_multi_gfni512(
+    uint8_t* const* v, const uint8_t* const* rows, const uint8_t* q, size_t ldq, size_t nrows, size_t n) {
+  const Tables& t = T();
+  for (size_t i0 = 0; i0 < n; i0 += 256) {
+    __mmask64 km[4];
+    for (int b = 0; b < 4; b++) {
+      const size_t o = i0 + (size_t)b * 64;
+      km[b] = o >= n ? (__mmask64)0 : (__mmask64)(~0ULL >> (64 - (n - o < 64 ? n - o : 64)));
+    }
+    __m512i acc[P][4];
+#pragma GCC unroll 4
+    for (int p = 0; p < P; p++)
+#pragma GCC unroll 4
+      for (int b = 0; b < 4; b++) acc[p][b] = _mm512_maskz_loadu_epi8(km[b], v[p] + i0 + b * 64);
+    for (size_t r = 0; r < nrows; r++) {
+      const uint8_t* src = rows[r] + i0;
+      __m512i x[4];
+#pragma GCC unroll 4
+      for (int b = 0; b < 4; b++) x[b] = _mm512_maskz_loadu_epi8(km[b], src + b * 64);
+#pragma GCC unroll 4
+      for (int p = 0; p < P; p++) {
+        const uint8_t c = q[p * ldq + r];
+        if (!c) continue;
+        const __m512i A = _mm512_set1_epi64((long long)t.affine[c]);
+#pragma GCC unroll 4
+        for (int b = 0; b < 4; b++) acc[p][b] = _mm512_xor_si512(acc[p][b], _mm512_gf2p8affine_epi64_epi8(x[b], A, 0));
+      }
+    }
+#pragma GCC unroll 4
+    for (int p = 0; p < P; p++)
+#pragma GCC unroll 4
+      for (int b = 0; b < 4; b++) _mm512_mask_storeu_epi8(v[p] + i0 + b * 64, km[b], acc[p][b]);
+  }
+}
+
+// rows[j][0..n) ^= XOR_p q[j * P + p] * v[p][0..n) for every j (rank-P
+// update): each destination block is loaded and stored once for all P sources
+template <int P>
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void rank_multi_gfni512(
+    uint8_t* const* rows, const uint8_t* q, size_t nrows, const uint8_t* const* v, size_t n) {
+  const Tables& t = T();
+  for (size_t i0 = 0; i0 < n; i0 += 256) {
+    __mmask64 km[4];
+    for (int b = 0; b < 4; b++) {
+      const size_t o = i0 + (size_t)b * 64;
+      km[b] = o >= n ? (__mmask64)0 : (__mmask64)(~0ULL >> (64 - (n - o < 64 ? n - o : 64)));
+    }
+    __m512i vb[P][4];
+#pragma GCC unroll 4
+    for (int p = 0; p < P; p++)
+#pragma GCC unroll 4
+      for (int b = 0; b < 4; b++) vb[p][b] = _mm512_maskz_loadu_epi8(km[b], v[p] + i0 + b * 64);
+    for (size_t j = 0; j < nrows; j++) {
+      const uint8_t* qj = q + j * P;
+      bool any = false;
+      __m512i A[P];
+#pragma GCC unroll 4
+      for (int p = 0; p < P; p++) {
+        A[p] = _mm512_set1_epi64((long long)t.affine[qj[p]]);  // affine[0] = 0: a zero term
+        any = any || qj[p];
+      }
+      if (!any) continue;
+      uint8_t* dst = rows[j] + i0;
+#pragma GCC unroll 4
+      for (int b = 0; b < 4; b++) {
+        if (!km[b]) break;
+        __m512i d = _mm512_maskz_loadu_epi8(km[b], dst + b * 64);
+#pragma GCC unroll 4
+        for (int p = 0; p < P; p++) d = _mm512_xor_si512(d, _mm512_gf2p8affine_epi64_epi8(vb[p][b], A[p], 0));
+        _mm512_mask_storeu_epi8(dst + b * 64, km[b], d);
+      }
+    }
+  }
+}
+#endif
+
 // dst[0..n) ^= q * src[0..n)
 inline void axpy(uint8_t* dst, const uint8_t* src, size_t n, uint8_t q) {
   if (q == 0 || n == 0) return;
@@ -247,6 +328,39 @@ inline void rank1(uint8_t* const* rows, const uint8_t* q, size_t nrows, const ui
   if (have_gfni512()) return rank1_gfni512(rows, q, nrows, v, n);
 #endif
   for (size_t r = 0; r < nrows; r++) axpy(rows[r], v, n, q[r]);
+}
+
+// v[p][0..n) ^= XOR_i q[p * ldq + i] * rows[i][0..n), p < np (np <= 4)
+inline void accumulate_multi(uint8_t* const* v, size_t np, const uint8_t* const* rows, const uint8_t* q,
+                             size_t ldq, size_t nrows, size_t n) {
+#if defined(__x86_64__)
+  if (have_gfni512()) {
+    switch (np) {
+      case 1: return accumulate_multi_gfni512<1>(v, rows, q, ldq, nrows, n);
+      case 2: return accumulate_multi_gfni512<2>(v, rows, q, ldq, nrows, n);
+      case 3: return accumulate_multi_gfni512<3>(v, rows, q, ldq, nrows, n);
+      case 4: return accumulate_multi_gfni512<4>(v, rows, q, ldq, nrows, n);
+    }
+  }
+#endif
+  for (size_t p = 0; p < np; p++) accumulate(v[p], rows, q + p * ldq, nrows, n);
+}
+
+// rows[j][0..n) ^= XOR_p q[j * np + p] * v[p][0..n) for every j (np <= 4)
+inline void rank_multi(uint8_t* const* rows, const uint8_t* q, size_t nrows, const uint8_t* const* v, size_t np,
+                       size_t n) {
+#if defined(__x86_64__)
+  if (have_gfni512()) {
+    switch (np) {
+      case 1: return rank_multi_gfni512<1>(rows, q, nrows, v, n);
+      case 2: return rank_multi_gfni512<2>(rows, q, nrows, v, n);
+      case 3: return rank_multi_gfni512<3>(rows, q, nrows, v, n);
+      case 4: return rank_multi_gfni512<4>(rows, q, nrows, v, n);
+    }
+  }
+#endif
+  for (size_t j = 0; j < nrows; j++)
+    for (size_t p = 0; p < np; p++) axpy(rows[j], v[p], n, q[j * np + p]);
 }
 
 inline bool all_zero(const uint8_t* p, size_t n) {

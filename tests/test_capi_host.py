@@ -265,3 +265,61 @@ def test_core_fuzz_mixed_streams(seed):
         seen.append(v)
         stream.append((v, rng.integers(0, 256, L, dtype=np.uint8)))
     check_stream(k, stream)
+
+
+def _batch_vs_rows(k, R, cuts):
+    """rlnc_decoder_add_pieces over R (one row per received piece) split at
+    `cuts` == the same rows through rlnc_decoder_add_piece one by one (which
+    the tests above tie to the oracle): return codes, rows consumed, and the
+    coefficient and transform matrices byte for byte."""
+    L = _lib.lib()
+    seq, bat = CoreDecoder(k), CoreDecoder(k)
+    seq_st = []
+    for v in R:
+        seq_st.append(seq.add(v))
+        if seq_st[-1] != 0:
+            break
+    W = np.ascontiguousarray(np.concatenate([R, np.zeros((R.shape[0], 1), np.uint8)], axis=1))
+    pos = 0
+    for c1 in cuts:
+        if c1 <= pos:
+            continue
+        used = ctypes.c_size_t()
+        st = L.rlnc_decoder_add_pieces(bat.h, W[pos:].ctypes.data_as(_lib._u8p), c1 - pos, k + 1, 1, 0,
+                                       ctypes.byref(used))
+        exp_used = sum(1 for s in seq_st[pos:c1] if s == 0)
+        exp_st = seq_st[pos + exp_used] if exp_used < c1 - pos and pos + exp_used < len(seq_st) else 0
+        assert (st, used.value) == (exp_st, exp_used), (pos, c1)
+        pos += used.value
+        if st != 0:
+            break
+    assert seq.state() == bat.state()
+    assert np.array_equal(seq.coefficients(), bat.coefficients())
+    assert np.array_equal(seq.transform(), bat.transform())
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_batch_add_matches_row_by_row(seed):
+    # the batched path eliminates runs of clean rows 4 at a time
+    # (decoder_core.cpp add_panel); it must leave exactly the state of
+    # one-by-one AddPiece, including when a row of a run is not a pivot
+    rng = np.random.default_rng(9100 + seed)
+    k = int(rng.choice([2, 3, 5, 8, 16, 33, 64, 256]))
+    n = k + int(rng.integers(0, 6))
+    kind = seed % 5
+    if kind == 0:
+        R = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    elif kind == 1:
+        R = (rng.integers(0, 256, (n, k)) * (rng.random((n, k)) < 0.2)).astype(np.uint8)
+    elif kind == 2:  # systematic stream with losses, coded rows after
+        lost = set(rng.choice(k, max(1, k // 5), replace=False).tolist())
+        R = np.concatenate([np.eye(k, dtype=np.uint8)[[i for i in range(k) if i not in lost]],
+                            rng.integers(0, 256, (n, k), dtype=np.uint8)])[:n]
+    elif kind == 3:  # rank-deficient combinations, some zero rows
+        B = rng.integers(0, 256, (max(1, k // 2), k), dtype=np.uint8)
+        R = oracle.matmul(rng.integers(0, 256, (n, B.shape[0]), dtype=np.uint8), B)[1]
+        R[rng.random(n) < 0.1] = 0
+    else:  # tiny field: frequent zero diagonals inside a run
+        R = rng.integers(0, 3, (n, k), dtype=np.uint8)
+    cuts = sorted(set(rng.integers(1, n + 1, 3).tolist()) | {n})
+    _batch_vs_rows(k, np.ascontiguousarray(R), cuts)
