@@ -792,7 +792,7 @@ int dec_store_pieces(rlnc_decoder* d, size_t row0, const uint8_t* src, size_t sp
   TRY(dec_reserve_rows(d, row0 + n, row0));
   uint8_t* dst = d->recv.p + row0 * d->pitch;
   if (dev)
-    HIPC(hipMemcpy2DAsync(dst, d->pitch, src, spitch, d->L, n, hipMemcpyDeviceToDevice, d->ctx->stream));
+    HIPC(kodr_amd::copy_rows(src, spitch, dst, d->pitch, n, d->L, d->ctx->stream));
   else  // staged: the host buffer is only borrowed for the duration of the call
     HIPC(d->ctx->stage.h2d(dst, d->pitch, src, spitch, d->L, n, d->ctx->stream));
   return RLNC_OK;

@@ -361,6 +361,38 @@ hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, 
   return hipGetLastError();
 }
 
+namespace {
+
+// dst row r = bytes [0, ncols) of src row r (both device, any pitch): 16 B
+// per lane where both rows allow it, bytes otherwise
+__global__ __launch_bounds__(256) void copy_rows_kernel(const uint8_t* __restrict__ src, size_t spitch,
+                                                       uint8_t* __restrict__ dst, size_t dpitch, int ncols,
+                                                       int vec) {
+  const int r = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
+  if (c >= ncols) return;
+  const uint8_t* s = src + (size_t)r * spitch + c;
+  uint8_t* d = dst + (size_t)r * dpitch + c;
+  if (vec && c + kLaneBytes <= ncols) {
+    *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+  } else {
+    for (int i = 0; i < kLaneBytes && c + i < ncols; i++) d[i] = s[i];
+  }
+}
+
+}  // namespace
+
+hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
+                     hipStream_t stream) {
+  if (!rows || !ncols) return hipSuccess;
+  if (rows > 65535 || ncols > 0x7fffffff) return hipErrorInvalidValue;
+  const int vec = ((uintptr_t)src % 16 == 0 && (uintptr_t)dst % 16 == 0 && spitch % 16 == 0 && dpitch % 16 == 0);
+  const unsigned gx = (unsigned)((ncols + 256 * kLaneBytes - 1) / (256 * kLaneBytes));
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, src, spitch, dst, dpitch,
+                     (int)ncols, vec);
+  return hipGetLastError();
+}
+
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;

@@ -34,6 +34,12 @@ hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped
 
 // dY row r = the first ncols bytes of device row d_src[r] (d_src: device array
 // of rows pointers, 16-byte aligned).  rows <= 65535.
+// dst row r = the first ncols bytes of src row r, device to device, as a
+// kernel: a few rows cost a launch (~2 us of host time) instead of a
+// hipMemcpy2DAsync call.  rows <= 65535.
+hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
+                     hipStream_t stream);
+
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream);
 
