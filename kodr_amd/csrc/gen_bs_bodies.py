@@ -159,7 +159,7 @@ def ROW_PRIO(j):
     return j % 4
 
 
-def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
@@ -168,15 +168,15 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
     h = lambda i: T0 + 2 * i  # noqa: E731
     t = [f"s_setprio {prio(j)}"] if prio else []
     t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
-    t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)]
-    t += table_lines(slot)
+    t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
+    t += table_lines(slot) * (2 if "table" in twice else 1)
     b = RING + 8 * slot
     # the row P ahead into this slot (rows past the wave's range read zero)
     if loads:
         t += [f"buffer_load_dwordx4 v[{b}:{b + 3}], %[col], s[40:43], s44 offen",
               f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16",
               "s_add_u32 s44, s44, s45"]
-    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)]
+    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
     if dispatch:
         if half_prio:  # this row's own stub, which sets the second half's priority
             t += [f"s_add_u32 s{h(4)}, s{GPC}, .Lstub{j}_%= - .Lpc_%=",
@@ -223,7 +223,7 @@ def prologue_lines(dispatch=True):
     return pro
 
 
-def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
@@ -236,7 +236,7 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None):
                 t += stub_lines(f"stub{j}", half_prio(j))
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads, prio, half_prio)
+        t += row_lines(j, dispatch, loads, prio, half_prio, twice)
     t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
           f"v_add_u32_e32 v{PL}, 256, v{PL}"]
     t += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_lg_u32 s{CNT}, 0", "s_cbranch_scc1 .Lloop_%="]
@@ -324,7 +324,9 @@ def main():
     # tuning: the loop without the priority rotation (MODE 10)
     out += emit("KODR_BS_MAIN_NOPRIO", main_loop(True, True, None))
     out += emit("KODR_BS_MAIN_HALF", main_loop(True, True, ROW_PRIO, lambda j: (j + 2) % 4))
-    out += emit("KODR_BS_MAIN_HALF2", main_loop(True, True, lambda j: (2 * j) % 4, lambda j: (2 * j + 1) % 4))
+    # cost probes: the row's target reads or its tables issued twice (same result)
+    out += emit("KODR_BS_MAIN_2RL", main_loop(True, True, ROW_PRIO, None, ("readlane",)))
+    out += emit("KODR_BS_MAIN_2TB", main_loop(True, True, ROW_PRIO, None, ("table",)))
     out += emit("KODR_BS_DUMP", dump_lines())
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)

@@ -246,7 +246,9 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     } else if constexpr (MODE == 11) {
       KODR_BS_ASM(KODR_BS_MAIN_HALF);
     } else if constexpr (MODE == 12) {
-      KODR_BS_ASM(KODR_BS_MAIN_HALF2);
+      KODR_BS_ASM(KODR_BS_MAIN_2RL);
+    } else if constexpr (MODE == 13) {
+      KODR_BS_ASM(KODR_BS_MAIN_2TB);
     } else if constexpr (MODE == 6) {
       KODR_BS_ASM(KODR_BS_MAIN_NL);
     } else {
@@ -472,7 +474,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 4 ? KODR_BS_CALL(KW_, 4) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
          : mode == 8 ? KODR_BS_CALL(KW_, 8) : mode == 9 ? KODR_BS_CALL(KW_, 9)                    \
          : mode == 10 ? KODR_BS_CALL(KW_, 10) : mode == 11 ? KODR_BS_CALL(KW_, 11)                \
-         : mode == 12 ? KODR_BS_CALL(KW_, 12) : KODR_BS_CALL(KW_, 0);
+         : mode == 12 ? KODR_BS_CALL(KW_, 12) : mode == 13 ? KODR_BS_CALL(KW_, 13) : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

@@ -239,11 +239,12 @@ class _Wave:
         return np.array([[self.v[gen.ACC + 8 * m + j] for j in range(8)] for m in range(8)], np.uint32)
 
 
-# the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-12)
+# the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-13)
 LOOPS = {"main": lambda: gen.main_loop(True),
          "noprio": lambda: gen.main_loop(True, True, None),
          "half": lambda: gen.main_loop(True, True, gen.ROW_PRIO, lambda j: (j + 2) % 4),
-         "half2": lambda: gen.main_loop(True, True, lambda j: 2 * j % 4, lambda j: (2 * j + 1) % 4)}
+         "twice_readlane": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, ("readlane",)),
+         "twice_table": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, ("table",))}
 
 
 @pytest.mark.parametrize("variant", sorted(LOOPS))
