@@ -56,6 +56,8 @@ RT = 80
 RET = 82
 CNT = 98
 GPC = 56           # s_getpc scratch s[56:57]
+SP = 46            # scalar-load variant: program pointer s[46:47]
+SL = 48            # scalar-load variant: the next row's 8 targets s[48:55]
 # table slot of subset s (1..15): the singles 1, 2, 4, 8 first so that each
 # pair of them is one aligned v_pk_mov_b32, then the combinations in order
 SLOT = {1: 0, 2: 1, 4: 2, 8: 3}
@@ -159,7 +161,7 @@ def ROW_PRIO(j):
     return j % 4
 
 
-def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()):
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
@@ -167,8 +169,15 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
     slot = j % P
     h = lambda i: T0 + 2 * i  # noqa: E731
     t = [f"s_setprio {prio(j)}"] if prio else []
-    t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
-    t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
+    if sload:  # targets staged by the previous row's scalar load; fetch the next row's
+        t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(0)"]
+        t += [f"s_mov_b32 s{h(m)}, s{SL + m}" for m in range(4)]
+        t += [f"s_mov_b32 s{H2 + 2 * m}, s{SL + 4 + m}" for m in range(4)]
+        t += [f"s_load_dwordx8 s[{SL}:{SL + 7}], s[{SP}:{SP + 1}], 0x0",
+              f"s_add_u32 s{SP}, s{SP}, 32", f"s_addc_u32 s{SP + 1}, s{SP + 1}, 0"]
+    else:
+        t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
+        t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
     t += table_lines(slot) * (2 if "table" in twice else 1)
     b = RING + 8 * slot
     # the row P ahead into this slot (rows past the wave's range read zero)
@@ -176,7 +185,8 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
         t += [f"buffer_load_dwordx4 v[{b}:{b + 3}], %[col], s[40:43], s44 offen",
               f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16",
               "s_add_u32 s44, s44, s45"]
-    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
+    if not sload:
+        t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
     if dispatch:
         if half_prio:  # this row's own stub, which sets the second half's priority
             t += [f"s_add_u32 s{h(4)}, s{GPC}, .Lstub{j}_%= - .Lpc_%=",
@@ -202,7 +212,7 @@ def stub_lines(label="stub", prio=None):
     return t
 
 
-def prologue_lines(dispatch=True):
+def prologue_lines(dispatch=True, sload=False):
     """Descriptor, stub and per-row return addresses, target hi words, the
     first two program chunks, zeroed accumulators.  SGPRs: s[40:43] X
     descriptor (num_records = end of this wave's rows), s44 row offset,
@@ -216,19 +226,24 @@ def prologue_lines(dispatch=True):
                     f"s_addc_u32 s{reg + 1}, s{GPC + 1}, 0"]
     pro += [f"s_mov_b32 s{T0 + 2 * i + 1}, %[thi]" for i in range(4)]
     pro += [f"s_mov_b32 s{H2 + 2 * i + 1}, %[thi]" for i in range(4)]
-    pro += [f"v_mov_b32 v{PL}, %[pl]", f"ds_read_b32 v{PG}, v{PL}", f"ds_read_b32 v{PGN}, v{PL} offset:256",
-            f"v_add_u32_e32 v{PL}, 512, v{PL}"]
+    if sload:  # the wave's program in global memory, one 32-byte row of targets at a time
+        pro += [f"s_mov_b32 s{SP}, %[pglo]", f"s_mov_b32 s{SP + 1}, %[pghi]",
+                f"s_load_dwordx8 s[{SL}:{SL + 7}], s[{SP}:{SP + 1}], 0x0",
+                f"s_add_u32 s{SP}, s{SP}, 32", f"s_addc_u32 s{SP + 1}, s{SP + 1}, 0"]
+    else:
+        pro += [f"v_mov_b32 v{PL}, %[pl]", f"ds_read_b32 v{PG}, v{PL}", f"ds_read_b32 v{PGN}, v{PL} offset:256",
+                f"v_add_u32_e32 v{PL}, 512, v{PL}"]
     pro += [f"v_mov_b32 v{ACC + r}, 0" for r in range(64)]
     pro += [f"s_mov_b32 s{CNT}, %[ngrp]"]
     return pro
 
 
-def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
     into v[PG] and the one after is requested."""
-    t = prologue_lines(dispatch)
+    t = prologue_lines(dispatch, sload)
     if dispatch:
         t += ["s_branch .Lloop_%="] + stub_lines()
         if half_prio:
@@ -236,9 +251,10 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()
                 t += stub_lines(f"stub{j}", half_prio(j))
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads, prio, half_prio, twice)
-    t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
-          f"v_add_u32_e32 v{PL}, 256, v{PL}"]
+        t += row_lines(j, dispatch, loads, prio, half_prio, twice, sload)
+    if not sload:
+        t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
+              f"v_add_u32_e32 v{PL}, 256, v{PL}"]
     t += [f"s_sub_u32 s{CNT}, s{CNT}, 1", f"s_cmp_lg_u32 s{CNT}, 0", "s_cbranch_scc1 .Lloop_%="]
     if prio:
         t += ["s_setprio 0"]
@@ -327,6 +343,8 @@ def main():
     # cost probes: the row's target reads or its tables issued twice (same result)
     out += emit("KODR_BS_MAIN_2RL", main_loop(True, True, ROW_PRIO, None, ("readlane",)))
     out += emit("KODR_BS_MAIN_2TB", main_loop(True, True, ROW_PRIO, None, ("table",)))
+    # program through scalar loads instead of LDS + v_readlane (MODE 14)
+    out += emit("KODR_BS_MAIN_SLOAD", main_loop(True, True, ROW_PRIO, None, (), True))
     out += emit("KODR_BS_DUMP", dump_lines())
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)
@@ -335,6 +353,8 @@ def main():
     assert CNT <= 101 and GPC + 1 < T0
     clob += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
     out.append("#define KODR_BS_CLOBBERS " + ", ".join(clob) + ', "scc", "memory"')
+    out.append("#define KODR_BS_CLOBBERS_SLOAD " + ", ".join(clob + [f'"s{r}"' for r in range(SP, SL + 8)]) +
+               ', "scc", "memory"')
     out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "
                f"row prep {len(table_lines(0))} per row; {total} bytes of bodies")
     print("\n".join(out))

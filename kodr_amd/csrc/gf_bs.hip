@@ -109,6 +109,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // row stream, 5 = no main loop (prologue, reduction and store only), 6 = the
 // full loop without the row stream (stale rows), 8 = s_memtime timeline,
 // 9 = register dump before the first jump.
+#ifdef KODR_TUNE_MODES
+__device__ uint32_t* g_bs_prog = nullptr;  // MODE 14's program scratch (tuning builds only)
+#endif
+
 template <int KW, int MODE = 0>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
@@ -204,6 +208,17 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)(e & 3) * KODR_BS_COPY_BYTES;
     }
   }
+#ifdef KODR_TUNE_MODES
+  // MODE 14: the program also in global memory, read by the asm with scalar
+  // loads (the compiler waits for these stores with the ring loads before the asm)
+  uint32_t* progw = nullptr;
+  if constexpr (MODE == 14) {
+    progw = g_bs_prog + ((size_t)blockIdx.x * KW + w) * (size_t)rpw * kBsRows;
+    for (int e = lane; e < ne; e += 64) progw[e] = wp[e];
+  }
+#else
+  uint32_t* progw = nullptr;
+#endif
   __syncthreads();
 
   const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / kBsChunk));
@@ -215,13 +230,17 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp)) + (uint32_t)lane * 4u;
   const uint32_t sthi = __builtin_amdgcn_readfirstlane(thi);
   if constexpr (MODE == 8) stamp[1] = __builtin_amdgcn_s_memtime();
-#define KODR_BS_ASM(MAIN)                                                                           \
+  const uint64_t pga = reinterpret_cast<uint64_t>(progw);
+  const uint32_t pglo = __builtin_amdgcn_readfirstlane((uint32_t)pga);
+  const uint32_t pghi = __builtin_amdgcn_readfirstlane((uint32_t)(pga >> 32));
+#define KODR_BS_ASM2(MAIN, CLOB)                                                                    \
   asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"                                       \
                : KODR_BS_RING_OPERANDS                                                              \
                : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx),  \
                  [ngrp] "s"(ngrp), [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)reinterpret_cast<uintptr_t>(red) + (uint32_t)lane * 4u),   \
-                 [pl] "v"(pl), [ydbg] "s"(Y)                                                        \
-               : KODR_BS_CLOBBERS)
+                 [pl] "v"(pl), [ydbg] "s"(Y), [pglo] "s"(pglo), [pghi] "s"(pghi)                   \
+               : CLOB)
+#define KODR_BS_ASM(MAIN) KODR_BS_ASM2(MAIN, KODR_BS_CLOBBERS)
   if (nr > 0 && MODE != 5) {
     if constexpr (MODE == 9) {
       if (blockIdx.x == 0 && w == 0) {
@@ -249,6 +268,10 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       KODR_BS_ASM(KODR_BS_MAIN_2RL);
     } else if constexpr (MODE == 13) {
       KODR_BS_ASM(KODR_BS_MAIN_2TB);
+#ifdef KODR_TUNE_MODES
+    } else if constexpr (MODE == 14) {
+      KODR_BS_ASM2(KODR_BS_MAIN_SLOAD, KODR_BS_CLOBBERS_SLOAD);
+#endif
     } else if constexpr (MODE == 6) {
       KODR_BS_ASM(KODR_BS_MAIN_NL);
     } else {
@@ -256,6 +279,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     }
   }
 #undef KODR_BS_ASM
+#undef KODR_BS_ASM2
   if constexpr (MODE == 8) stamp[2] = __builtin_amdgcn_s_memtime();
   __syncthreads();
 
@@ -464,6 +488,16 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   (void)mode;
 #ifdef KODR_TUNE_MODES
   if (const char* env = getenv("KODR_BS_MODE")) mode = atoi(env);
+  if (mode == 14) {  // program scratch for the scalar-load variant, with look-ahead slack
+    static uint32_t* scratch = nullptr;
+    constexpr size_t kScratch = (size_t)64 << 20;
+    const size_t need = (size_t)p.blocks * p.kw * p.rpw * kBsRows * 4 + 256;
+    if (need > kScratch) return hipErrorInvalidValue;
+    if (!scratch) {
+      if ((e = hipMalloc((void**)&scratch, kScratch)) != hipSuccess) return e;
+      if ((e = hipMemcpyToSymbol(HIP_SYMBOL(g_bs_prog), &scratch, sizeof(scratch))) != hipSuccess) return e;
+    }
+  }
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
   bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream)
@@ -474,7 +508,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 4 ? KODR_BS_CALL(KW_, 4) : mode == 6 ? KODR_BS_CALL(KW_, 6)                    \
          : mode == 8 ? KODR_BS_CALL(KW_, 8) : mode == 9 ? KODR_BS_CALL(KW_, 9)                    \
          : mode == 10 ? KODR_BS_CALL(KW_, 10) : mode == 11 ? KODR_BS_CALL(KW_, 11)                \
-         : mode == 12 ? KODR_BS_CALL(KW_, 12) : mode == 13 ? KODR_BS_CALL(KW_, 13) : KODR_BS_CALL(KW_, 0);
+         : mode == 12 ? KODR_BS_CALL(KW_, 12) : mode == 13 ? KODR_BS_CALL(KW_, 13)                \
+         : mode == 14 ? KODR_BS_CALL(KW_, 14) : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

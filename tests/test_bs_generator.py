@@ -141,8 +141,11 @@ class _Wave:
             for m in range(8):
                 c = int(A[m, k])
                 self.lds[pl + 4 * (8 * k + m)] = (self.BASE + offs[(m & 3) * 256 + c]) & 0xFFFFFFFF
+        # the same program in global memory for the scalar-load variant (plus
+        # one row of look-ahead past the end, as the kernel's scratch has)
+        self.gmem = {0x2000_0000 + a - pl: v for a, v in self.lds.items()}
         self.ops = {"xlo": 0, "xhi": 0, "nrec": nr * 32, "roff": gen.P * 32, "ldx": 32, "ngrp": nr // 8,
-                    "thi": self.BASE >> 32, "col": 0}
+                    "thi": self.BASE >> 32, "col": 0, "pglo": 0x2000_0000, "pghi": 0}
         self.pl_lanes = [pl + 4 * lane for lane in range(64)]
         for slot in range(gen.P):                      # the compiler's ring prologue
             self._load_row(gen.RING + 8 * slot, slot * 32)
@@ -201,6 +204,11 @@ class _Wave:
             elif op == "s_mov_b64":
                 d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
                 self.s[d], self.s[d + 1] = self.s[sr], self.s[sr + 1]
+            elif op == "s_load_dwordx8":
+                d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
+                addr = (self.s[sr + 1] << 32) | self.s[sr]
+                for i in range(8):
+                    self.s[d + i] = self.gmem.get(addr + 4 * i, 0xDEAD)
             elif op == "s_setpc_b64":
                 lo = int(re.findall(r"s\[(\d+):", ln)[0])
                 pc = self.addr[(self.s[lo + 1] << 32) | self.s[lo]]
@@ -239,12 +247,13 @@ class _Wave:
         return np.array([[self.v[gen.ACC + 8 * m + j] for j in range(8)] for m in range(8)], np.uint32)
 
 
-# the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-13)
+# the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-14)
 LOOPS = {"main": lambda: gen.main_loop(True),
          "noprio": lambda: gen.main_loop(True, True, None),
          "half": lambda: gen.main_loop(True, True, gen.ROW_PRIO, lambda j: (j + 2) % 4),
          "twice_readlane": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, ("readlane",)),
-         "twice_table": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, ("table",))}
+         "twice_table": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, ("table",)),
+         "sload": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, (), True)}
 
 
 @pytest.mark.parametrize("variant", sorted(LOOPS))
