@@ -822,6 +822,22 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   return dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev);
 }
 
+// bit-sliced twin of the received rows: rows [bs_rows, received) added
+// (all of them again when the plain buffer has grown)
+int dec_extend_twin(rlnc_decoder* d) {
+  const size_t recv = d->core.received();
+  if (d->recv_bs.cap < d->recv_rows * d->pitch) {
+    TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
+    d->bs_rows = 0;
+  }
+  if (d->bs_rows < recv) {
+    HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
+                                 d->pitch, recv - d->bs_rows, d->L, d->ctx->stream));
+    d->bs_rows = recv;
+  }
+  return RLNC_OK;
+}
+
 // X = the received rows for a T x R product of M output rows: the plain rows
 // for small M, else the bit-sliced twin with rows [bs_rows, received) added.
 int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t ldy) {
@@ -837,16 +853,7 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
       !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   d->last_bs = true;
-  if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // the plain buffer grew: rebuild the twin
-    TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
-    d->bs_rows = 0;
-  }
-  if (d->bs_rows < recv) {
-    const size_t n = recv - d->bs_rows;
-    HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
-                                 d->pitch, n, d->L, ctx->stream));
-    d->bs_rows = recv;
-  }
+  TRY(dec_extend_twin(d));
   return gemm_bs(ctx, dA, recv, M, recv, d->recv_bs.p, d->pitch, dY, ldy, d->L);
 }
 
@@ -943,25 +950,43 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
     vecs = d->hvecs.data();
     vpitch = k;
   }
-  // coefficient side, one row at a time, exactly as repeated AddPiece calls.
-  // Rows from pinned host memory start their DMA first, so the PCIe copy
-  // overlaps the elimination; rows past the ones accepted land beyond the
-  // received range and are never read.
+  // Device rows and rows from pinned host memory are copied (and, for a large
+  // batch, bit-sliced into the decoder's twin) before the elimination, so the
+  // GPU work overlaps it; rows past the ones accepted land beyond the received
+  // range and are never read.
+  // The rows that can still be accepted before full rank (plus some slack for
+  // dependent ones) are copied first; the rest, if any are accepted, after.
   const size_t row0 = d->core.received();
-  const bool early = !dev && d->ctx && kodr_amd::Staging::is_pinned(rows);
-  if (early) {
-    TRY(dec_reserve_rows(d, row0 + count, row0));
-    HIPC(hipMemcpy2DAsync(d->recv.p + row0 * d->pitch, d->pitch, rows + k, pitch, d->L, count,
-                          hipMemcpyHostToDevice, d->ctx->stream));
+  const bool early = d->ctx && (dev || kodr_amd::Staging::is_pinned(rows));
+  const size_t pre = early ? std::min(count, d->core.required() + 16) : 0;
+  size_t twin_end = 0;
+  if (pre) {
+    TRY(dec_reserve_rows(d, row0 + pre, row0));
+    uint8_t* dst = d->recv.p + row0 * d->pitch;
+    if (dev)
+      HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
+    else
+      HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice, d->ctx->stream));
+    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0 && (row0 + pre) * d->pitch < ((size_t)1 << 32)) {
+      d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
+      if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
+        TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
+        d->bs_rows = 0;
+      }
+      HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
+                                   d->pitch, row0 + pre - d->bs_rows, d->L, d->ctx->stream));
+      twin_end = row0 + pre;
+    }
   }
+  // coefficient side, exactly as repeated AddPiece calls
   size_t n = 0;
-  const int st = d->core.add_many(vecs, vpitch, count, &n);  // == count calls of AddPiece
+  const int st = d->core.add_many(vecs, vpitch, count, &n);
   if (n) d->decoded_ready = false;
-  // data side: the accepted pieces are consecutive received rows -> one 2D copy
-  if (early)
-    HIPC(hipStreamSynchronize(d->ctx->stream));  // the caller may reuse rows on return
-  else
-    TRY(dec_store_pieces(d, row0, rows + k, pitch, n, dev));
+  if (twin_end) d->bs_rows = row0 + std::min(n, pre);  // only accepted rows' twin counts
+  // data side: accepted rows not copied yet (dependent rows past the slack,
+  // or the staged path) -> one 2D copy
+  if (n > pre) TRY(dec_store_pieces(d, row0 + pre, rows + pre * pitch + k, pitch, n - pre, dev));
+  if (early && !dev) HIPC(hipStreamSynchronize(d->ctx->stream));  // the caller may reuse rows on return
   *consumed = n;
   return st;
 }

@@ -750,3 +750,41 @@ def test_host_vectors_across_small_upload_limit(gpu_ctx, count):
     finally:
         gpu_ctx.synchronize()
         gpu_ctx.free(d_rows)
+
+
+@pytest.mark.parametrize("dev", [True, False])
+def test_batch_add_many_dependent_rows_past_the_precopy(gpu_ctx, dev):
+    """A batch whose accepted rows exceed what AddPieces copies ahead of the
+    elimination (required + 16): 40 rows spanning only 8 dimensions come
+    first, then independent ones; the late rows are copied after the
+    elimination and the decode still equals P (capi.cpp add_pieces)."""
+    k, L = 16, 4096
+    rng = np.random.default_rng(77 + dev)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    base = rng.integers(0, 256, (8, k), dtype=np.uint8)
+    V = np.concatenate([oracle.matmul(rng.integers(0, 256, (40, 8), dtype=np.uint8), base)[1],
+                        rng.integers(0, 256, (k + 4, k), dtype=np.uint8)])
+    rows = np.ascontiguousarray(np.concatenate([V, oracle.encode(P, V)], axis=1))
+    d, ref = Dec(gpu_ctx, k), oracle.Decoder(k)
+    if dev:
+        d_rows = gpu_ctx.alloc(rows.nbytes)
+        gpu_ctx.h2d(d_rows, rows)
+        st, used = _add_rows(d, ctypes.c_void_p(d_rows), rows.shape[0], k + L, True)
+    else:
+        hb = _page_aligned(rows.shape)
+        hb[:] = rows
+        gpu_ctx.register(hb)
+        st, used = _add_rows(d, ptr(hb), rows.shape[0], k + L, False)
+    try:
+        for r in rows[:used]:
+            ref.add(r[:k], r[k:])
+        assert used > 40 and st in (0, 3)
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+        st, dec = d.get_all()
+        assert st == 0 and np.array_equal(dec, P)
+    finally:
+        gpu_ctx.synchronize()
+        if dev:
+            gpu_ctx.free(d_rows)
+        else:
+            gpu_ctx.unregister(hb)
