@@ -197,7 +197,7 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
 
 // Below this many output rows the perm-table kernel (gf_gemm) wins: the
 // bit-sliced kernel runs one 8-row group however few rows are real, and with
-// 1-2 waves per SIMD its 2-row load ring leaves it latency-bound (~13 us for
+// 1-2 waves per SIMD its short load ring leaves it latency-bound (~13 us for
 // B = 1 at 32 MiB/256 against 9 us; B = 8: 17-19 against 16 us; B = 10: 20
 // against 28 us; profiles/r01/bs_min_rows.log).
 constexpr size_t kBsMinRows = 9;

@@ -40,7 +40,9 @@ ACC = 12           # 8 rows x 8 planes: v[12..75]; copy r owns v[12+8r .. 19+8r]
 TL0 = 76           # TL table, 15 registers v[76..90] (singles first, as aligned pairs)
 PL = 91            # LDS address of the next program quad
 TH0 = 92           # TH table v[92..106]
-P = int(os.environ.get("KODR_BS_P", "2"))   # ring depth (rows in flight per wave)
+# ring depth (rows in flight per wave): 1 measured 1.5-2.5 % faster than 2 at
+# B = 16-32 (profiles/r01/bs_ring.log), 3 drops to 3 waves per SIMD
+P = int(os.environ.get("KODR_BS_P", "1"))
 RING = 108         # P row slots x 8 planes: v[108..123]
 PG = RING + 8 * P  # program chunk: 8 rows x 8 targets, lane 8j + m (absolute lo words)
 PGN = PG + 1       # the next chunk, in flight from LDS
