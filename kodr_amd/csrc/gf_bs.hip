@@ -7,7 +7,7 @@
 // coefficient c is GF(2)-linear on the planes: out plane j = XOR of the input
 // planes i with bit j of c*2^i set (gf256.go:15-44, poly 0x11D).  Per input
 // row the wave tabulates the XORs of every subset of planes 0-3 and of planes
-// 4-7 (30 registers, 30 VALU shared by 8 output rows); then each output plane
+// 4-7 (30 registers, 26 VALU shared by 8 output rows); then each output plane
 // is one XOR3, at most 8 instructions per coefficient per 32 bytes, against 36
 // for the 3x v_perm lookup formulation of gf_gemm_kernel.
 //
@@ -24,9 +24,11 @@
 // range of at most rpw input rows; the KW waves of a workgroup split K and are
 // XOR-reduced in LDS.  Per wave, the absolute body targets for its (row, k)
 // pairs are built once into LDS ("program") and moved to SGPRs with
-// v_readfirstlane within the row.  X rows stream through a P-deep register
-// ring of buffer loads (rows past the wave's range are outside num_records and
-// read as zero); the first P are in flight while the program is built.
+// v_readlane within the row.  X rows stream through a P-deep register ring of
+// buffer loads (rows past the wave's range are outside num_records and read
+// as zero); the first P are in flight while the program is built.  Each input
+// row starts with s_setprio (row mod 4) so the 4 waves of a SIMD take turns
+// instead of finishing oldest-first.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
