@@ -106,14 +106,15 @@ def body_lines(c, r=0):
         a = ACC + 8 * r + j
         if lo and hi:
             out.append(f"v_bitop3_b32 v{a}, v{a}, v{tl(lo)}, v{th(hi)} bitop3:0x96")
-        else:
-            out.append(f"v_xor_b32_e64 v{a}, v{a}, v{tl(lo) if lo else th(hi)}")
+        else:  # one table entry: a 4-byte VOP2 XOR (index mode applies to src0 and vdst)
+            out.append(f"v_xor_b32_e32 v{a}, v{a}, v{tl(lo) if lo else th(hi)}")
     out.append(f"s_setpc_b64 s[{T0 + 2 * (r + 1)}:{T0 + 2 * (r + 1) + 1}]")
     return out
 
 
 def body_bytes(c):
-    return 8 * len(body_ops(c)) + 4      # VOP3 = 8 bytes, s_setpc_b64 = 4
+    # v_bitop3 (VOP3) 8 bytes, v_xor_b32_e32 (VOP2) 4, s_setpc_b64 4
+    return sum(8 if lo and hi else 4 for _j, lo, hi in body_ops(c)) + 4
 
 
 def body_offsets():

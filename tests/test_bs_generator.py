@@ -37,10 +37,11 @@ def run(lines, regs, idx=0):
             assert ln.endswith("op_sel:[0,1]")
             regs[r[0]] = regs[r[1]]          # lo <- a.lo
             regs[r[0] + 1] = regs[r[2] + 1]  # hi <- b.hi
-        elif op == "v_xor_b32_e32":
-            regs[r[0]] = regs[r[1]] ^ regs[r[2]]
-        elif op == "v_xor_b32_e64":   # body: acc (indexed) ^= table
-            regs[r[0] + idx] = regs[r[1] + idx] ^ regs[r[2]]
+        elif op in ("v_xor_b32_e32", "v_xor_b32_e64"):
+            if r[0] < gen.TL0:        # body: acc (indexed) ^= table entry
+                regs[r[0] + idx] = regs[r[1] + idx] ^ regs[r[2]]
+            else:                     # table build
+                regs[r[0]] = regs[r[1]] ^ regs[r[2]]
         elif op == "v_bitop3_b32":
             assert ln.endswith("bitop3:0x96")
             if r[0] < gen.TL0:        # body: acc (indexed) ^= a ^ b
@@ -59,7 +60,9 @@ def test_body_sizes_match_offsets():
     for r in range(gen.NCOPY):
         for c in range(256):
             assert len(gen.body_ops(c)) <= 8
-            assert gen.body_bytes(c) == 8 * len(gen.body_ops(c)) + 4
+            # an XOR3 is VOP3 (8 bytes), a single-entry XOR VOP2 (4), s_setpc 4
+            assert gen.body_bytes(c) == sum(8 if lo and hi else 4 for _j, lo, hi in gen.body_ops(c)) + 4
+            assert sum(8 if ln.startswith("v_bitop3") else 4 for ln in gen.body_lines(c, r)) == gen.body_bytes(c)
             nxt = offs[r * 256 + c + 1] if r * 256 + c + 1 < len(offs) else total
             assert nxt - offs[r * 256 + c] == gen.body_bytes(c)
     # every copy is laid out identically, and all of them stay within what the
