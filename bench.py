@@ -5,7 +5,8 @@ pieces (BASELINE.json configs[1]) on MI355X, device-resident, coded MB/s.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--gens G]
 
 One step = one pass of the hot path: B coded pieces of one resident generation
-(one gf_gemm launch: B coding vectors x the k x L generation).  The G
+(one kernel launch: B coding vectors x the k x L generation; gf_bs_kernel
+for B >= 9, gf_gemm_kernel below).  The G
 generations rotate so that consecutive steps stream from HBM, not from the
 256 MiB Infinity Cache.  Metric accounting is kodr's own: each coded piece is
 worth SetBytes = S + padding + (k + L) bytes (benches/full/encoder_test.go:53),
@@ -15,7 +16,7 @@ Multi-GPU (torchrun, one process per GPU): generations are independent, so
 every rank encodes its own G generations with no data-path collective (weak
 scaling); value = all ranks' coded bytes / max-over-ranks time.
 
-The JSON line also carries the roofline of the dominant kernel (gf_gemm,
+The JSON line also carries the roofline of the dominant kernel (gf_bs_kernel,
 timed with HIP events on the stream it runs on) and a CPU baseline: the
 kodr-equivalent scalar restatement (oracle/, one core) timed on a bounded
 sample of the same workload on this host.
@@ -259,10 +260,12 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "compulsory_hbm_bytes_per_launch": compulsory,
                          "compulsory_hbm_GBps": round(compulsory / t_launch / 1e9, 1),
+                         "compulsory_hbm_frac": round(compulsory / t_launch / 1e9 / HBM_PEAK_GBS, 4),
                          "avg_launch_us": round(t_launch * 1e6, 3),
                          "note": "B coded pieces per launch share one read of the generation; "
                                  "achieved counts kodr's SetBytes per piece (SURVEY 8d), so frac > 1 "
-                                 "means HBM reuse, see traffic"},
+                                 "means HBM reuse, see traffic; at B >= 9 the launch is bound by "
+                                 "instruction issue, not HBM (compulsory_hbm_frac, DESIGN.md Roofline)"},
             "cpu_baseline": cpu,
             "wall_s": round(wall, 4),
         }
