@@ -40,7 +40,7 @@ int hip_fail(hipError_t e, const char* what) {
 
 constexpr size_t kPitchAlign = 256;
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-constexpr size_t kMaxDescBytes = (size_t)1 << 31;  // 32-bit buffer offsets in gf_gemm
+constexpr size_t kMaxDescBytes = (size_t)1 << 31;  // gf_gemm's signed 32-bit buffer offsets: X rows per launch
 
 // Device buffer that only grows, from the device's caching pool (pool.hpp),
 // ordered on the owner's stream (bind before the first reserve).
@@ -169,30 +169,77 @@ int split_size(size_t len, size_t size, size_t* count, size_t* pad) {
   return RLNC_OK;
 }
 
+// The kernels address X through 32-bit buffer offsets (signed in gf_gemm,
+// unsigned in gf_bs) and gf_bs keeps each wave's program of (row, coefficient)
+// targets in LDS, so one launch takes at most kc rows of X.  A taller X (a
+// generation past 2 GiB, sized for 288 GB of HBM) is split into row chunks:
+// the first chunk's product goes to Y, each later one to a scratch block that
+// is XORed into Y (byte j of Y needs only byte j of every row, data.go:20-28).
+template <class F>
+int gemm_k_chunked(rlnc_ctx* ctx, const uint8_t* dA, size_t M, size_t K, const uint8_t* dX, size_t ldx,
+                   uint8_t* dY, size_t ldy, size_t ncols, size_t kc, F launch) {
+  if (K <= kc) return launch(dA, K, dX, dY);
+  DevBuf part;
+  part.bind(ctx->device, ctx->stream);
+  int s = part.reserve(M * ldy);
+  for (size_t k0 = 0; s == RLNC_OK && k0 < K; k0 += kc) {
+    const size_t kn = std::min(kc, K - k0);
+    s = launch(dA + k0, kn, dX + k0 * ldx, k0 ? part.p : dY);
+    for (size_t m0 = 0; k0 && s == RLNC_OK && m0 < M; m0 += 65535) {
+      const hipError_t e = kodr_amd::xor_rows(part.p + m0 * ldy, ldy, dY + m0 * ldy, ldy,
+                                              std::min<size_t>(65535, M - m0), ncols, ctx->stream);
+      if (e != hipSuccess) s = hip_fail(e, "xor_rows");
+    }
+  }
+  part.release();
+  return s;
+}
+
+// rows of X per gf_gemm launch
+size_t gemm_chunk_rows(size_t ldx) { return ldx ? (kMaxDescBytes - 1) / ldx : 0; }
+
+// rows of X per gf_bs launch for M output rows (0: the bit-sliced path cannot run)
+size_t bs_chunk_rows(size_t M, size_t K, size_t ldx, size_t ncols) {
+  if (!ldx || ldx > 0x7fffffff) return 0;
+  size_t kc = std::min<size_t>(K, (((size_t)1 << 32) - 1) / ldx);
+  if (kc > 8) kc = kc / 8 * 8;
+  while (kc && !kodr_amd::plan_gemm_bs(M, kc, ncols).ok) kc = kc > 8 ? kc / 2 / 8 * 8 : 0;
+  return kc;
+}
+
 int gemm(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
          size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (K * ldx >= kMaxDescBytes || (ldx % 16) || (ldy % 16) || ldx < ncols || ldy < ncols) {
-    g_last_error = "gf_gemm: unsupported layout (pitch must be a multiple of 16, K*pitch < 2^31)";
+  const size_t kc = gemm_chunk_rows(ldx);
+  if (kc == 0 || (ldx % 16) || (ldy % 16) || ldx < ncols || ldy < ncols || ldx > 0x7fffffff) {
+    g_last_error = "gf_gemm: unsupported layout (pitch a multiple of 16 and below 2^31)";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
-  HIPC(kodr_amd::gf_gemm(dA, lda, M, K, dX, ldx, dY, ldy, ncols, ctx->stream));
-  return RLNC_OK;
+  return gemm_k_chunked(ctx, dA, M, K, dX, ldx, dY, ldy, ncols, kc,
+                        [&](const uint8_t* a, size_t kn, const uint8_t* x, uint8_t* y) {
+                          HIPC(kodr_amd::gf_gemm(a, lda, M, kn, x, ldx, y, ldy, ncols, ctx->stream));
+                          return (int)RLNC_OK;
+                        });
 }
 
 // Y = A (x) X over a bit-sliced X (kodr_amd::bitslice_rows), plain Y
 int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
             size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (K * ldx >= ((size_t)1 << 32) || (ldx % 32) || (ldy % 16) || ldx < ncols || ldy < ncols) {
-    g_last_error = "gf_gemm_bs: unsupported layout (pitch multiple of 32, K*pitch < 2^32)";
+  if ((ldx % 32) || (ldy % 16) || ldx < ncols || ldy < ncols) {
+    g_last_error = "gf_gemm_bs: unsupported layout (pitch a multiple of 32)";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
   if (M == 0 || ncols == 0) return RLNC_OK;
-  if (!kodr_amd::plan_gemm_bs(M, K, ncols).ok) {
-    g_last_error = "gf_gemm_bs: K too large for the LDS program";
+  const size_t kc = bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols);
+  if (kc == 0) {
+    g_last_error = "gf_gemm_bs: no launch plan for this shape";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
-  HIPC(kodr_amd::gf_gemm_bs(dA, lda, M, K, dX, ldx, dY, ldy, ncols, ctx->device, ctx->stream));
-  return RLNC_OK;
+  return gemm_k_chunked(ctx, dA, M, K, dX, ldx, dY, ldy, ncols, kc,
+                        [&](const uint8_t* a, size_t kn, const uint8_t* x, uint8_t* y) {
+                          HIPC(kodr_amd::gf_gemm_bs(a, lda, M, kn, x, ldx, y, ldy, ncols, ctx->device,
+                                                    ctx->stream));
+                          return (int)RLNC_OK;
+                        });
 }
 
 // Below this many output rows the perm-table kernel (gf_gemm) wins: the
@@ -214,7 +261,7 @@ constexpr size_t kBsTwinBudget = 16u << 20;  // bytes of new twin rows worth bui
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (M < kBsMinRows || (ldx % 32) || K * ldx >= ((size_t)1 << 32) || !kodr_amd::plan_gemm_bs(M, K, ncols).ok ||
+  if (M < kBsMinRows || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
       !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {
@@ -238,9 +285,9 @@ int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** ou
   e->k = k;
   e->L = L;
   e->pitch = round_up(L, kPitchAlign);
-  if (k * e->pitch >= kMaxDescBytes) {
+  if (e->pitch >= kMaxDescBytes) {
     delete e;
-    g_last_error = "generation larger than 2 GiB";
+    g_last_error = "piece size of 2 GiB or more";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
   int s = e->pieces.reserve(k * e->pitch);
@@ -644,7 +691,7 @@ static int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_re
   r->k = k;
   r->clen = clen;
   r->pitch = round_up(clen, kPitchAlign);
-  if (n * r->pitch >= kMaxDescBytes) {
+  if (r->pitch >= kMaxDescBytes) {
     delete r;
     return RLNC_ERR_INVALID_ARGUMENT;
   }
@@ -773,7 +820,6 @@ namespace {
 int dec_reserve_rows(rlnc_decoder* d, size_t need, size_t have) {
   if (need <= d->recv_rows) return RLNC_OK;
   size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, need);
-  if (nrows * d->pitch >= kMaxDescBytes) nrows = std::max(need, kMaxDescBytes / d->pitch - 1);
   DevBuf nb;
   nb.bind(d->ctx->device, d->ctx->stream);
   TRY(nb.reserve(nrows * d->pitch));
@@ -849,8 +895,8 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   if (const char* env = getenv("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
 #endif
   d->last_bs = false;
-  if (M < min_rows || (d->pitch % 32) || recv * d->pitch >= ((size_t)1 << 32) ||
-      !kodr_amd::plan_gemm_bs(M, recv, d->L).ok || !kodr_amd::bs_ready(ctx->device))
+  if (M < min_rows || (d->pitch % 32) || !bs_chunk_rows(M, std::max<size_t>(recv, 1), d->pitch, d->L) ||
+      !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   d->last_bs = true;
   TRY(dec_extend_twin(d));
@@ -967,7 +1013,7 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
       HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
     else
       HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice, d->ctx->stream));
-    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0 && (row0 + pre) * d->pitch < ((size_t)1 << 32)) {
+    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0) {
       d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
       if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
         TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));

@@ -393,6 +393,43 @@ hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpi
   return hipGetLastError();
 }
 
+namespace {
+
+// dst row r ^= src row r over [0, ncols) (16-byte aligned rows and pitches)
+__global__ __launch_bounds__(256) void xor_rows_kernel(const uint8_t* __restrict__ src, size_t spitch,
+                                                      uint8_t* __restrict__ dst, size_t dpitch, int ncols) {
+  const int r = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
+  if (c >= ncols) return;
+  const uint8_t* s = src + (size_t)r * spitch + c;
+  uint8_t* d = dst + (size_t)r * dpitch + c;
+  if (c + kLaneBytes <= ncols) {
+    const uint4 a = *reinterpret_cast<const uint4*>(s);
+    uint4 b = *reinterpret_cast<const uint4*>(d);
+    b.x ^= a.x;
+    b.y ^= a.y;
+    b.z ^= a.z;
+    b.w ^= a.w;
+    *reinterpret_cast<uint4*>(d) = b;
+  } else {
+    for (int i = 0; c + i < ncols; i++) d[i] ^= s[i];
+  }
+}
+
+}  // namespace
+
+hipError_t xor_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
+                    hipStream_t stream) {
+  if (!rows || !ncols) return hipSuccess;
+  if (rows > 65535 || ncols > 0x7fffffff || (uintptr_t)src % 16 || (uintptr_t)dst % 16 || spitch % 16 ||
+      dpitch % 16)
+    return hipErrorInvalidValue;
+  const unsigned gx = (unsigned)((ncols + 256 * kLaneBytes - 1) / (256 * kLaneBytes));
+  hipLaunchKernelGGL(xor_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, src, spitch, dst, dpitch,
+                     (int)ncols);
+  return hipGetLastError();
+}
+
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;

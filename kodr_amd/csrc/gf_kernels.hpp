@@ -40,6 +40,12 @@ hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped
 hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
                      hipStream_t stream);
 
+// dst row r ^= src row r over [0, ncols): folds the partial products of a
+// K-split GEMM (generations past the kernels' 32-bit buffer offsets).  Rows and
+// pitches 16-byte aligned, rows <= 65535.
+hipError_t xor_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
+                    hipStream_t stream);
+
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream);
 

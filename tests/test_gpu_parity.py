@@ -788,3 +788,64 @@ def test_batch_add_many_dependent_rows_past_the_precopy(gpu_ctx, dev):
             gpu_ctx.free(d_rows)
         else:
             gpu_ctx.unregister(hb)
+
+
+def test_generation_past_4_gib(gpu_ctx):
+    # A 5 GiB generation (40 pieces of 128 MiB): past the kernels' 32-bit
+    # buffer offsets, so gf_gemm (B = 1) runs it in 3 row chunks and gf_bs
+    # (B >= 9, decode) in 2, with the partial products XORed together
+    # (capi.cpp gemm_k_chunked).  Column windows at the start, the middle
+    # (unaligned) and the ragged end are checked against the oracle; the
+    # round trip through the decoder is checked on the same windows.
+    L_ = _lib.lib()
+    k, L = 40, 128 << 20
+    rng = np.random.default_rng(11)
+    wins = [(0, 4096), (L // 2 + 96, 4096), (L - 4000, 4000)]
+    keep = {o: np.empty((k, w), np.uint8) for o, w in wins}
+    dP = gpu_ctx.alloc(k * L)
+    eh = ctypes.c_void_p()
+    try:
+        for r in range(k):
+            row = np.frombuffer(rng.bytes(L), np.uint8)
+            gpu_ctx.h2d(dP + r * L, row)
+            for o, w in wins:
+                keep[o][r] = row[o:o + w]
+        del row
+        errors.check(L_.rlnc_encoder_create_device(gpu_ctx.handle, FULL, dP, k, L, L, ctypes.byref(eh)))
+    finally:
+        gpu_ctx.free(dP)
+    n = k + 8
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    dV, dOut, dDec = gpu_ctx.alloc(V.nbytes), gpu_ctx.alloc(n * L), gpu_ctx.alloc(k * L)
+    dh = ctypes.c_void_p()
+    try:
+        gpu_ctx.h2d(dV, V)
+        # B = 1 (gf_gemm, row-chunked), then the rest in one call (gf_bs, row-chunked)
+        errors.check(L_.rlnc_encoder_coded_pieces_device(eh, dV, 1, dOut, L))
+        errors.check(L_.rlnc_encoder_coded_pieces_device(eh, dV + k, n - 1, dOut + L, L))
+        gpu_ctx.synchronize()
+        for o, w in wins:
+            ref = oracle.encode(keep[o], V)
+            for i in list(range(0, n, 5)) + [n - 1]:
+                got = gpu_ctx.d2h(dOut + i * L + o, w)
+                assert np.array_equal(got, ref[i]), f"coded piece {i}, columns [{o}, {o + w})"
+        errors.check(L_.rlnc_decoder_create(gpu_ctx.handle, k, ctypes.byref(dh)))
+        for i in range(n):
+            v = np.ascontiguousarray(V[i])
+            st = L_.rlnc_decoder_add_piece_device(dh, ptr(v), k, dOut + i * L, L)
+            if st == ERR["ErrAllUsefulPiecesReceived"]:
+                break
+            assert st == 0
+        assert L_.rlnc_decoder_is_decoded(dh)
+        errors.check(L_.rlnc_decoder_get_pieces_device(dh, dDec, L))
+        gpu_ctx.synchronize()
+        for o, w in wins:
+            for r in range(k):
+                assert np.array_equal(gpu_ctx.d2h(dDec + r * L + o, w), keep[o][r]), f"decoded piece {r}"
+    finally:
+        if dh.value:
+            L_.rlnc_decoder_destroy(dh)
+        L_.rlnc_encoder_destroy(eh)
+        for p in (dV, dOut, dDec):
+            gpu_ctx.free(p)
+        L_.rlnc_device_pool_trim(0, 0)
