@@ -179,6 +179,10 @@ template <class F>
 int gemm_k_chunked(rlnc_ctx* ctx, const uint8_t* dA, size_t M, size_t K, const uint8_t* dX, size_t ldx,
                    uint8_t* dY, size_t ldy, size_t ncols, size_t kc, F launch) {
   if (K <= kc) return launch(dA, K, dX, dY);
+  // equal chunks (whole 8-row program chunks where kc allows): 256 rows of
+  // 16 MiB split 128 + 128, not 248 + 8
+  const size_t nch = (K + kc - 1) / kc;
+  kc = std::min(kc, ((K + nch - 1) / nch + 7) / 8 * 8);
   DevBuf part;
   part.bind(ctx->device, ctx->stream);
   int s = part.reserve(M * ldy);

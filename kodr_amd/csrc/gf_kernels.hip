@@ -485,7 +485,15 @@ namespace {
 // Every tile stages K-chunks of 256 rows; for K > 256 the tables are
 // double-buffered (2 x 256 x MT x 20 B of LDS), which rules out MT = 16.
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
-  (void)ncols;
+  // Few rows of X: the K-splitting tiles below give each of their 16 waves 16
+  // rows, so with K < 256 most waves of a workgroup idle.  One wave per
+  // workgroup running all K rows wastes nothing; it needs many column chunks
+  // to fill the chip, which wide rows (or K <= 16, where the wide tiles have a
+  // single busy wave anyway) provide.
+  if (M <= 8 && (K <= 16 || (K < 256 && ncols >= ((size_t)2 << 20)))) {
+    const int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
+    return {mt, 1, 2, 8};
+  }
   if (K > 256 && M > 8 && M <= 16) return {8, 16, 2, 2};
   if (M <= 1) return {1, 16, 2, 0};
   if (M <= 2) return {2, 16, 2, 0};
@@ -529,6 +537,10 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
 #define KODR_TRY(MT_, KW_, S_, RC_, P_)                                               \
   if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))             \
     return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  KODR_TRY(1, 1, 2, 16, 8)
+  KODR_TRY(2, 1, 2, 16, 8)
+  KODR_TRY(4, 1, 2, 16, 8)
+  KODR_TRY(8, 1, 2, 16, 8)
   KODR_TRY(1, 16, 4, 16, 4)
   KODR_TRY(1, 16, 2, 16, 8)
   KODR_TRY(1, 16, 1, 16, 8)
