@@ -485,13 +485,18 @@ namespace {
 // Every tile stages K-chunks of 256 rows; for K > 256 the tables are
 // double-buffered (2 x 256 x MT x 20 B of LDS), which rules out MT = 16.
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
-  // Few rows of X: the K-splitting tiles below give each of their 16 waves 16
+  // Few rows of X: the K-splitting tiles below give each of their waves 16-32
   // rows, so with K < 256 most waves of a workgroup idle.  One wave per
   // workgroup running all K rows wastes nothing; it needs many column chunks
-  // to fill the chip, which wide rows (or K <= 16, where the wide tiles have a
-  // single busy wave anyway) provide.
-  if (M <= 8 && (K <= 16 || (K < 256 && ncols >= ((size_t)2 << 20)))) {
-    const int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
+  // (512 B each) to fill the chip, which rows of 256 KiB or more (or K <= 16,
+  // where the wide tiles have a single busy wave anyway) provide, and the
+  // output rows are split over row tiles until there are >= 1024 workgroups.
+  // Measured 1.1-6.7x faster for K = 32-128, L = 256 KiB-4 MiB, M = 1-8
+  // (tools/sweep_fewrows.sh, profiles/r01/sweep_fewrows.log).
+  const size_t nxc = (ncols + 511) / 512;
+  if (M <= 8 && K < 256 && (K <= 16 || nxc >= 512)) {
+    int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
+    while (mt > 1 && nxc * ((M + mt - 1) / mt) < 1024) mt /= 2;
     return {mt, 1, 2, 8};
   }
   if (K > 256 && M > 8 && M <= 16) return {8, 16, 2, 2};

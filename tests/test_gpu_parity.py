@@ -147,6 +147,31 @@ def test_gf_matmul_vs_oracle(gpu_ctx, M, K):
         assert (Y[:, ncols:] == 0xA5).all(), "wrote past ncols"
 
 
+@pytest.mark.parametrize("M,K,ncols", [(1, 32, 262144 + 48), (3, 64, 262144), (8, 100, (1 << 20) + 16),
+                                       (5, 17, 300000 + 3), (2, 255, 262144), (8, 16, 65536 + 5)])
+def test_gf_matmul_few_rows_wide_vs_oracle(gpu_ctx, M, K, ncols):
+    # the one-wave gf_gemm tiles (K < 256 with rows of >= 256 KiB, or K <= 16),
+    # split over row tiles: bit-exact, and nothing written past ncols
+    rng = np.random.default_rng(M * 7919 + K)
+    ld = (ncols + 255) // 256 * 256
+    A = rng.integers(0, 256, (M, K), dtype=np.uint8)
+    X = np.zeros((K, ld), np.uint8)
+    X[:, :ncols] = rng.integers(0, 256, (K, ncols), dtype=np.uint8)
+    dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(X.nbytes), gpu_ctx.alloc(M * ld)
+    try:
+        gpu_ctx.h2d(dA, A)
+        gpu_ctx.h2d(dX, X)
+        gpu_ctx.h2d(dY, np.full(M * ld, 0xA5, np.uint8))
+        errors.check(_lib.lib().rlnc_gf_matmul_device(gpu_ctx.handle, dA, K, M, K, dX, ld, dY, ld, ncols))
+        Y = gpu_ctx.d2h(dY, M * ld).reshape(M, ld)
+    finally:
+        for p in (dA, dX, dY):
+            gpu_ctx.free(p)
+    st, ref = oracle.matmul(A, X[:, :ncols])
+    assert np.array_equal(Y[:, :ncols], ref), (M, K, ncols)
+    assert (Y[:, ncols:] == 0xA5).all(), "wrote past ncols"
+
+
 def test_c2_encode_batch_full_compare(gpu_ctx):
     # BASELINE config 2: 32 MiB / 256 pieces, 8 coded pieces compared in full
     rng = np.random.default_rng(0x6B6F6472)
