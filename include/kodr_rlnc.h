@@ -121,7 +121,10 @@ int rlnc_encoder_create_with_piece_count(rlnc_ctx* ctx, int kind, const uint8_t*
 int rlnc_encoder_create_with_piece_size(rlnc_ctx* ctx, int kind, const uint8_t* data,
                                         size_t data_len, size_t piece_size, rlnc_encoder** out);
 /* NewFullRLNCEncoder(pieces) (full/encoder.go:76-78) / NewSystematicRLNCEncoder
- * (systematic/encoder.go:115-117): k pieces of L bytes, row-major contiguous */
+ * (systematic/encoder.go:115-117): k pieces of L bytes, row-major contiguous.
+ * Size: a generation may exceed 4 GiB (products run in row chunks); a single
+ * piece (its 256-byte row pitch) must stay below 2 GiB, else
+ * RLNC_ERR_INVALID_ARGUMENT.  The same holds for recoders and decoders. */
 int rlnc_encoder_create(rlnc_ctx* ctx, int kind, const uint8_t* pieces, size_t piece_count,
                         size_t piece_size, rlnc_encoder** out);
 /* the same from a device buffer (k rows, row pitch `pitch` bytes), copied D2D */
