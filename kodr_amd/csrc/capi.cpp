@@ -173,29 +173,17 @@ int split_size(size_t len, size_t size, size_t* count, size_t* pad) {
 // unsigned in gf_bs) and gf_bs keeps each wave's program of (row, coefficient)
 // targets in LDS, so one launch takes at most kc rows of X.  A taller X (a
 // generation past 2 GiB, sized for 288 GB of HBM) is split into row chunks:
-// the first chunk's product goes to Y, each later one to a scratch block that
-// is XORed into Y (byte j of Y needs only byte j of every row, data.go:20-28).
+// the first chunk's launch writes Y, each later one XORs its product into Y in
+// its store (byte j of Y needs only byte j of every row, data.go:20-28).
 template <class F>
-int gemm_k_chunked(rlnc_ctx* ctx, const uint8_t* dA, size_t M, size_t K, const uint8_t* dX, size_t ldx,
-                   uint8_t* dY, size_t ldy, size_t ncols, size_t kc, F launch) {
-  if (K <= kc) return launch(dA, K, dX, dY);
+int gemm_k_chunked(size_t K, size_t kc, F launch) {
+  if (K <= kc) return launch(0, K, false);
   // equal chunks (whole 8-row program chunks where kc allows): 256 rows of
   // 16 MiB split 128 + 128, not 248 + 8
   const size_t nch = (K + kc - 1) / kc;
   kc = std::min(kc, ((K + nch - 1) / nch + 7) / 8 * 8);
-  DevBuf part;
-  part.bind(ctx->device, ctx->stream);
-  int s = part.reserve(M * ldy);
-  for (size_t k0 = 0; s == RLNC_OK && k0 < K; k0 += kc) {
-    const size_t kn = std::min(kc, K - k0);
-    s = launch(dA + k0, kn, dX + k0 * ldx, k0 ? part.p : dY);
-    for (size_t m0 = 0; k0 && s == RLNC_OK && m0 < M; m0 += 65535) {
-      const hipError_t e = kodr_amd::xor_rows(part.p + m0 * ldy, ldy, dY + m0 * ldy, ldy,
-                                              std::min<size_t>(65535, M - m0), ncols, ctx->stream);
-      if (e != hipSuccess) s = hip_fail(e, "xor_rows");
-    }
-  }
-  part.release();
+  int s = RLNC_OK;
+  for (size_t k0 = 0; s == RLNC_OK && k0 < K; k0 += kc) s = launch(k0, std::min(kc, K - k0), k0 > 0);
   return s;
 }
 
@@ -218,11 +206,10 @@ int gemm(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const
     g_last_error = "gf_gemm: unsupported layout (pitch a multiple of 16 and below 2^31)";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
-  return gemm_k_chunked(ctx, dA, M, K, dX, ldx, dY, ldy, ncols, kc,
-                        [&](const uint8_t* a, size_t kn, const uint8_t* x, uint8_t* y) {
-                          HIPC(kodr_amd::gf_gemm(a, lda, M, kn, x, ldx, y, ldy, ncols, ctx->stream));
-                          return (int)RLNC_OK;
-                        });
+  return gemm_k_chunked(K, kc, [&](size_t k0, size_t kn, bool acc) {
+    HIPC(kodr_amd::gf_gemm(dA + k0, lda, M, kn, dX + k0 * ldx, ldx, dY, ldy, ncols, ctx->stream, nullptr, acc));
+    return (int)RLNC_OK;
+  });
 }
 
 // Y = A (x) X over a bit-sliced X (kodr_amd::bitslice_rows), plain Y
@@ -238,12 +225,11 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
     g_last_error = "gf_gemm_bs: no launch plan for this shape";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
-  return gemm_k_chunked(ctx, dA, M, K, dX, ldx, dY, ldy, ncols, kc,
-                        [&](const uint8_t* a, size_t kn, const uint8_t* x, uint8_t* y) {
-                          HIPC(kodr_amd::gf_gemm_bs(a, lda, M, kn, x, ldx, y, ldy, ncols, ctx->device,
-                                                    ctx->stream));
-                          return (int)RLNC_OK;
-                        });
+  return gemm_k_chunked(K, kc, [&](size_t k0, size_t kn, bool acc) {
+    HIPC(kodr_amd::gf_gemm_bs(dA + k0, lda, M, kn, dX + k0 * ldx, ldx, dY, ldy, ncols, ctx->device, ctx->stream,
+                              acc));
+    return (int)RLNC_OK;
+  });
 }
 
 // Below this many output rows the perm-table kernel (gf_gemm) wins: the

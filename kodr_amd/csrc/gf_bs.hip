@@ -119,7 +119,7 @@ template <int KW, int MODE = 0>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
-    const uint32_t* __restrict__ tgt, uint32_t thi) {
+    const uint32_t* __restrict__ tgt, uint32_t thi, int accum) {
   // LDS: [0, 16 KiB) per-row XOR sums [8 rows x 8 planes][64 lanes];
   // [16, 17 KiB) the body target table (absolute lo words of copy 0; copy r
   // is r * KODR_BS_COPY_BYTES further); then each wave's program: per input
@@ -297,10 +297,17 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     bitslice32(d);
     uint8_t* dst = Y + (size_t)row * ldy + cc;
     if (cc + kBsBlock <= ncols) {
-      reinterpret_cast<uint4*>(dst)[0] = make_uint4(d[0], d[1], d[2], d[3]);
-      reinterpret_cast<uint4*>(dst)[1] = make_uint4(d[4], d[5], d[6], d[7]);
+      uint4 v0 = make_uint4(d[0], d[1], d[2], d[3]), v1 = make_uint4(d[4], d[5], d[6], d[7]);
+      if (accum) {  // a later row chunk of a K-split product: Y ^= this chunk's part
+        const uint4 o0 = reinterpret_cast<const uint4*>(dst)[0], o1 = reinterpret_cast<const uint4*>(dst)[1];
+        v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
+        v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
+      }
+      reinterpret_cast<uint4*>(dst)[0] = v0;
+      reinterpret_cast<uint4*>(dst)[1] = v1;
     } else {
-      for (int i = 0; cc + i < ncols; i++) dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
+      for (int i = 0; cc + i < ncols; i++)
+        dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
     }
   }
   if constexpr (MODE == 8) {  // timeline build: stamps past the M output rows (the caller sizes Y)
@@ -349,7 +356,7 @@ hipError_t bs_init(int dev, const BsDevice** out) {
     // where gf_bs_kernel runs means the export is wrong, and jumping there
     // would fault
     hipLaunchKernelGGL((gf_bs_kernel<1, 0>), dim3(1), dim3(64), 0, 0, nullptr, 0, 0, 0, nullptr, 0,
-                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u);
+                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u, 0);
     if ((e = hipGetLastError()) == hipSuccess) e = hipDeviceSynchronize();
     uint32_t kpc[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpy(kpc, buf, sizeof(kpc), hipMemcpyDeviceToHost);
@@ -383,10 +390,10 @@ hipError_t bs_init(int dev, const BsDevice** out) {
 template <int KW, int MODE = 0>
 hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, int ldx, uint8_t* Y,
                      size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes, const BsDevice* bd,
-                     hipStream_t st) {
+                     hipStream_t st, int accum) {
   const int nb = (ncx + 7) / 8 * 8 * nrg;
   hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
-                     ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi);
+                     ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum);
   return hipGetLastError();
 }
 
@@ -465,7 +472,7 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
 }
 
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
-                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream) {
+                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream, bool accumulate) {
   if (M == 0 || ncols == 0) return hipSuccess;
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
@@ -502,7 +509,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   }
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
-  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream)
+  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream, \
+                          accumulate ? 1 : 0)
 #ifdef KODR_TUNE_MODES
 #define KODR_BS_CASE(KW_)                                                                         \
   case KW_:                                                                                       \

@@ -74,7 +74,7 @@ template <int MT, int KW, int S, int RC, int P, int MODE = 0>
 __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K,
     const uint8_t* __restrict__ X, size_t ldx,
-    uint8_t* __restrict__ Y, size_t ldy, int ncols, int nx, int ny, int nbuf) {
+    uint8_t* __restrict__ Y, size_t ldy, int ncols, int nx, int ny, int nbuf, int accum) {
   static_assert(S == 1 || S == 2 || S == 4, "lane groups");
   static_assert(RC % (S * P) == 0, "ring: P row-steps of S rows must divide RC");
   constexpr int KC = KW * RC;
@@ -246,10 +246,15 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
     if (row >= M || cc >= ncols) return;
     uint8_t* dst = Y + (size_t)row * ldy + cc;
     if (cc + kLaneBytes <= ncols) {
+      if (accum) {  // a later row chunk of a K-split product: Y ^= this chunk's part
+        const uint4 o = *reinterpret_cast<const uint4*>(dst);
+        v = make_uint4(v.x ^ o.x, v.y ^ o.y, v.z ^ o.z, v.w ^ o.w);
+      }
       *reinterpret_cast<uint4*>(dst) = v;
     } else {
       const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-      for (int i = 0; cc + i < ncols; i++) dst[i] = (uint8_t)(vv[i >> 2] >> (8 * (i & 3)));
+      for (int i = 0; cc + i < ncols; i++)
+        dst[i] = (uint8_t)(vv[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
     }
   };
 
@@ -280,7 +285,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
 
 template <int MT, int KW, int S, int RC, int P, int MODE = 0>
 hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, size_t ldx,
-                  uint8_t* Y, size_t ldy, int ncols, hipStream_t stream) {
+                  uint8_t* Y, size_t ldy, int ncols, hipStream_t stream, int accum = 0) {
   constexpr int KC = KW * RC;
   constexpr int CB = 1024 / S;
   const int nx = (ncols + CB - 1) / CB;
@@ -290,7 +295,7 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
   const size_t lds = (size_t)nbuf * KC * MT * (16 + 4) + (KW > 1 ? (size_t)MT * 4 * (64 / S) * 4 : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, S, RC, P, MODE>), dim3(nx8 * ny), dim3(64 * KW), lds, stream,
-                     A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf);
+                     A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf, accum);
   return hipGetLastError();
 }
 
@@ -393,43 +398,6 @@ hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpi
   return hipGetLastError();
 }
 
-namespace {
-
-// dst row r ^= src row r over [0, ncols) (16-byte aligned rows and pitches)
-__global__ __launch_bounds__(256) void xor_rows_kernel(const uint8_t* __restrict__ src, size_t spitch,
-                                                      uint8_t* __restrict__ dst, size_t dpitch, int ncols) {
-  const int r = blockIdx.y;
-  const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
-  if (c >= ncols) return;
-  const uint8_t* s = src + (size_t)r * spitch + c;
-  uint8_t* d = dst + (size_t)r * dpitch + c;
-  if (c + kLaneBytes <= ncols) {
-    const uint4 a = *reinterpret_cast<const uint4*>(s);
-    uint4 b = *reinterpret_cast<const uint4*>(d);
-    b.x ^= a.x;
-    b.y ^= a.y;
-    b.z ^= a.z;
-    b.w ^= a.w;
-    *reinterpret_cast<uint4*>(d) = b;
-  } else {
-    for (int i = 0; c + i < ncols; i++) d[i] ^= s[i];
-  }
-}
-
-}  // namespace
-
-hipError_t xor_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
-                    hipStream_t stream) {
-  if (!rows || !ncols) return hipSuccess;
-  if (rows > 65535 || ncols > 0x7fffffff || (uintptr_t)src % 16 || (uintptr_t)dst % 16 || spitch % 16 ||
-      dpitch % 16)
-    return hipErrorInvalidValue;
-  const unsigned gx = (unsigned)((ncols + 256 * kLaneBytes - 1) / (256 * kLaneBytes));
-  hipLaunchKernelGGL(xor_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, src, spitch, dst, dpitch,
-                     (int)ncols);
-  return hipGetLastError();
-}
-
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;
@@ -518,7 +486,8 @@ static bool env_config(GemmConfig* g) {
 
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
-                   const GemmConfig* force) {
+                   const GemmConfig* force, bool accumulate) {
+  const int acc = accumulate ? 1 : 0;
   if (M == 0 || ncols == 0) return hipSuccess;
   GemmConfig g = force ? *force : choose_gemm_config(M, K, ncols);
   GemmConfig ge;
@@ -541,7 +510,7 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   (void)mode;
 #define KODR_TRY(MT_, KW_, S_, RC_, P_)                                               \
   if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))             \
-    return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+    return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc);
   KODR_TRY(1, 1, 2, 16, 8)
   KODR_TRY(2, 1, 2, 16, 8)
   KODR_TRY(4, 1, 2, 16, 8)

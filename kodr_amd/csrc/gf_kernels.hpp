@@ -16,10 +16,11 @@ struct GemmConfig {
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols);
 
 // Y[m][j] = XOR_k A[m][k] * X[k][j], m < M, j < ncols.  All pointers device.
+// accumulate: Y[m][j] ^= that product instead (one row chunk of a K-split).
 // ldx/ldy multiples of 16 and >= ncols; X rows readable up to round_up(ncols,16).
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
-                   const GemmConfig* force = nullptr);
+                   const GemmConfig* force = nullptr, bool accumulate = false);
 
 // dst (pitch dpitch) = width x rows contiguous bytes of host-mapped pinned
 // memory (a device pointer of a hipHostMalloc buffer), copied by a kernel
@@ -39,12 +40,6 @@ hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped
 // hipMemcpy2DAsync call.  rows <= 65535.
 hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
                      hipStream_t stream);
-
-// dst row r ^= src row r over [0, ncols): folds the partial products of a
-// K-split GEMM (generations past the kernels' 32-bit buffer offsets).  Rows and
-// pitches 16-byte aligned, rows <= 65535.
-hipError_t xor_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
-                    hipStream_t stream);
 
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream);
@@ -78,6 +73,7 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols);
 
 // Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
-                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream);
+                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream,
+                      bool accumulate = false);
 
 }  // namespace kodr_amd
