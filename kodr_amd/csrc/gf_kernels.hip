@@ -454,15 +454,15 @@ namespace {
 // double-buffered (2 x 256 x MT x 20 B of LDS), which rules out MT = 16.
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   // Few rows of X: the K-splitting tiles below give each of their waves 16-32
-  // rows, so with K < 256 most waves of a workgroup idle.  One wave per
-  // workgroup running all K rows wastes nothing; it needs many column chunks
-  // (512 B each) to fill the chip, which rows of 256 KiB or more (or K <= 16,
-  // where the wide tiles have a single busy wave anyway) provide, and the
-  // output rows are split over row tiles until there are >= 1024 workgroups.
-  // Measured 1.1-6.7x faster for K = 32-128, L = 256 KiB-4 MiB, M = 1-8
-  // (tools/sweep_fewrows.sh, profiles/r01/sweep_fewrows.log).
+  // rows, so with small K most waves of a workgroup idle.  One wave per
+  // workgroup running all K rows wastes nothing but needs many column chunks
+  // (512 B each) to fill the chip; output rows are split over row tiles until
+  // there are >= 1024 workgroups.  Where each side wins was measured over
+  // K = 16-200, L = 64 KiB-4 MiB, M = 1-8 (tools/sweep_fewrows*.sh,
+  // profiles/r01/sweep_fewrows*.log): K <= 32 always; K <= 64 from 128 KiB
+  // rows (from 64 KiB for M >= 4); K <= 128 from 256 KiB rows; not at K = 200.
   const size_t nxc = (ncols + 511) / 512;
-  if (M <= 8 && K < 256 && (K <= 16 || nxc >= 512)) {
+  if (M <= 8 && (K <= 32 || (K <= 64 && (M >= 4 || nxc >= 256)) || (K <= 128 && nxc >= 512))) {
     int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
     while (mt > 1 && nxc * ((M + mt - 1) / mt) < 1024) mt /= 2;
     return {mt, 1, 2, 8};
