@@ -251,7 +251,11 @@ constexpr size_t kBsTwinBudget = 16u << 20;  // bytes of new twin rows worth bui
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (M < kBsMinRows || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
+  // few rows of narrow pieces: gf_gemm's one-wave tiles beat the bit-sliced
+  // launch's fixed cost (K = 16, 128 KiB rows, 9-32 pieces: 4.8-7.2 us against
+  // 8.7-9.0; K = 32: up to 16 pieces; profiles/r01/bs_vs_gemm_small_k.log)
+  const bool few_narrow = K <= 32 && ncols <= ((size_t)256 << 10) && (K <= 16 || M <= 16);
+  if (M < kBsMinRows || few_narrow || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
       !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {

@@ -462,7 +462,8 @@ GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   // profiles/r01/sweep_fewrows*.log): K <= 32 always; K <= 64 from 128 KiB
   // rows (from 64 KiB for M >= 4); K <= 128 from 256 KiB rows; not at K = 200.
   const size_t nxc = (ncols + 511) / 512;
-  if (M <= 8 && (K <= 32 || (K <= 64 && (M >= 4 || nxc >= 256)) || (K <= 128 && nxc >= 512))) {
+  // (More than 8 output rows: 8-row tiles, each re-reading X from L2.)
+  if (K <= 32 || (K <= 64 && (M >= 4 || nxc >= 256)) || (K <= 128 && nxc >= 512)) {
     int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
     while (mt > 1 && nxc * ((M + mt - 1) / mt) < 1024) mt /= 2;
     return {mt, 1, 2, 8};

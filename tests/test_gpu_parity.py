@@ -148,7 +148,8 @@ def test_gf_matmul_vs_oracle(gpu_ctx, M, K):
 
 
 @pytest.mark.parametrize("M,K,ncols", [(1, 32, 262144 + 48), (3, 64, 262144), (8, 100, (1 << 20) + 16),
-                                       (5, 17, 300000 + 3), (2, 255, 262144), (8, 16, 65536 + 5)])
+                                       (5, 17, 300000 + 3), (2, 255, 262144), (8, 16, 65536 + 5),
+                                       (20, 24, 262144 + 32), (33, 64, 131072)])
 def test_gf_matmul_few_rows_wide_vs_oracle(gpu_ctx, M, K, ncols):
     # the one-wave gf_gemm tiles (K < 256 with rows of >= 256 KiB, or K <= 16),
     # split over row tiles: bit-exact, and nothing written past ncols
