@@ -247,15 +247,18 @@ constexpr size_t kBsMinRows = 9;
 constexpr size_t kBsMinRowsDecode = 16;
 constexpr size_t kBsTwinBudget = 16u << 20;  // bytes of new twin rows worth building for 9..15 rows
 
+// Few rows of narrow pieces: gf_gemm's one-wave tiles beat the bit-sliced
+// launch's fixed cost (K = 16, 128 KiB rows, 9-32 output rows: 4.8-7.2 us
+// against 8.7-9.0; K = 32: up to 16 rows; profiles/r01/bs_vs_gemm_small_k.log).
+bool few_narrow_rows(size_t M, size_t K, size_t ncols) {
+  return K <= 32 && ncols <= ((size_t)256 << 10) && (K <= 16 || M <= 16);
+}
+
 // Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  // few rows of narrow pieces: gf_gemm's one-wave tiles beat the bit-sliced
-  // launch's fixed cost (K = 16, 128 KiB rows, 9-32 pieces: 4.8-7.2 us against
-  // 8.7-9.0; K = 32: up to 16 pieces; profiles/r01/bs_vs_gemm_small_k.log)
-  const bool few_narrow = K <= 32 && ncols <= ((size_t)256 << 10) && (K <= 16 || M <= 16);
-  if (M < kBsMinRows || few_narrow || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
+  if (M < kBsMinRows || few_narrow_rows(M, K, ncols) || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
       !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   if (!twin_valid) {
@@ -889,7 +892,8 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   if (const char* env = getenv("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
 #endif
   d->last_bs = false;
-  if (M < min_rows || (d->pitch % 32) || !bs_chunk_rows(M, std::max<size_t>(recv, 1), d->pitch, d->L) ||
+  if (M < min_rows || few_narrow_rows(M, recv, d->L) || (d->pitch % 32) ||
+      !bs_chunk_rows(M, std::max<size_t>(recv, 1), d->pitch, d->L) ||
       !kodr_amd::bs_ready(ctx->device))
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
   d->last_bs = true;
@@ -1007,7 +1011,8 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
       HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
     else
       HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice, d->ctx->stream));
-    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0) {
+    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0 &&
+        !few_narrow_rows(d->core.piece_count(), row0 + pre, d->L)) {  // else dec_gemm takes gf_gemm
       d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
       if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
         TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
