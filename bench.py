@@ -168,16 +168,27 @@ def main():
     ctx = kdev.Context(local)
     k, L, B, G = K_PIECES, L_BYTES, args.batch, args.gens
 
-    # G resident generations of 32 MiB (+ B x k vectors per step, rotating)
+    # G resident generations of 32 MiB (+ B x k vectors per step, rotating).
+    # Construction (upload + the bit-sliced twin, rlnc_encoder_prepare) happens
+    # here, outside the timed loop, as kodr's bench constructs its encoder
+    # before b.Loop (benches/full/encoder_test.go:47-56); its cost is reported
+    # separately (construct_ms_per_generation).
     rng = np.random.default_rng(0x6B6F6472 + rank)
     import ctypes
-    encs = []
+    encs, datas = [], []
     for g in range(G):
-        data = rng.integers(0, 256, k * L, dtype=np.uint8)
+        datas.append(rng.integers(0, 256, k * L, dtype=np.uint8))
+    ctx.synchronize()
+    tc0 = time.perf_counter()
+    for g in range(G):
         h = ctypes.c_void_p()
-        errors.check(L_.rlnc_encoder_create(ctx.handle, 0, data.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+        errors.check(L_.rlnc_encoder_create(ctx.handle, 0, datas[g].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
                                             k, L, ctypes.byref(h)))
+        errors.check(L_.rlnc_encoder_prepare(h))
         encs.append(h)
+    ctx.synchronize()
+    construct_ms = (time.perf_counter() - tc0) * 1e3 / G
+    del datas
     nvec = 64
     V = rng.integers(0, 256, (nvec, B, k), dtype=np.uint8)
     dV = ctx.alloc(V.nbytes)
@@ -193,7 +204,9 @@ def main():
             dist.barrier()
         ctx.synchronize()
 
-    for i in range(args.warmup):
+    # W warmup steps, but never fewer than one pass over the G generations, so
+    # no generation is first touched inside the timed region
+    for i in range(max(args.warmup, G)):
         step(i)
     barrier()
     e0, e1 = ctx.event(), ctx.event()
@@ -211,18 +224,22 @@ def main():
     unit_bytes = setbytes(k, L)
     value = kdist.aggregate_rate(args.steps * B, unit_bytes, t_max, world)
     t_launch = t_local / args.steps
-    # roofline.achieved follows SURVEY §8(d): algorithmic bytes per launch =
-    # kodr's per-piece SetBytes x the B pieces one launch computes.  The launch
-    # reads the generation once for all B pieces, so its compulsory HBM traffic
-    # (generation + B vectors + B pieces out) is far lower; that figure and the
-    # PMC-measured traffic are reported beside it.
+    # Roofline of the dominant kernel, per launch (one launch = one step):
+    #  hbm:   the bytes a launch must move -- the generation once, B vectors
+    #         in, B pieces out -- over the launch time, against 8 TB/s.  (kodr's
+    #         SetBytes x B, the unit of `value`, counts the generation once per
+    #         piece, so it is not an HBM byte count: B pieces share one read.)
+    #  issue: GF MACs per second against the VALU floor of the bit-sliced
+    #         method, the bound that binds at B >= 9 (Roofline).
     algo_bytes = B * unit_bytes
     compulsory = k * L + B * k + B * L
-    achieved = algo_bytes / t_launch / 1e9
+    achieved = compulsory / t_launch / 1e9
+    macs = B * k * L
+    bs = B >= 9
 
-    extras = {}
+    extras = {"construct_ms_per_generation": round(construct_ms, 3)}
     if not args.no_extras and rank == 0:
-        extras = run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng)
+        extras.update(run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng))
     if world > 1 and not args.no_extras:
         try:
             c5 = run_relay(ctx, L_, errors, encs[0], k, L, rng, torch, dist, kdist)
@@ -250,22 +267,27 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded uniform random bytes and coding vectors)",
-            "config": {"workload": "Full RLNC encode, 32 MiB generation / 256 pieces (BASELINE configs[1])",
+            "config": {"workload": "Full RLNC encode, 32 MiB generation / 256 pieces (BASELINE configs[1]); "
+                                   "the decode leg (configs[2]) is extras.c2_decode",
                        "piece_count": k, "piece_size": L, "coded_pieces_per_step": B,
                        "resident_generations": G, "parallelism": f"generation-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, k, L),
-                         "kernel": "gf_bs_kernel" if B >= 9 else "gf_gemm_kernel",  # capi.cpp kBsMinRows
-                         "algorithmic_bytes_per_launch": algo_bytes,
-                         "compulsory_hbm_bytes_per_launch": compulsory,
-                         "compulsory_hbm_GBps": round(compulsory / t_launch / 1e9, 1),
-                         "compulsory_hbm_frac": round(compulsory / t_launch / 1e9 / HBM_PEAK_GBS, 4),
+                         "kernel": "gf_bs_kernel" if bs else "gf_gemm_kernel",  # capi.cpp kBsMinRows
+                         "hbm_bytes_per_launch": compulsory,
                          "avg_launch_us": round(t_launch * 1e6, 3),
-                         "note": "B coded pieces per launch share one read of the generation; "
-                                 "achieved counts kodr's SetBytes per piece (SURVEY 8d), so frac > 1 "
-                                 "means HBM reuse, see traffic; at B >= 9 the launch is bound by "
-                                 "instruction issue, not HBM (compulsory_hbm_frac, DESIGN.md Roofline)"},
+                         "issue": {"achieved_gf_macs_per_s": float(f"{macs / t_launch:.4g}"),
+                                   "peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
+                                   "frac": round(macs / t_launch / VALU_FLOOR_MACS_PER_S, 4) if bs else None,
+                                   "gf_macs_per_launch": macs},
+                         "kodr_setbytes_per_launch": algo_bytes,
+                         "note": "achieved/frac: the launch's compulsory HBM bytes (generation once + B vectors + "
+                                 "B pieces) / launch time / 8 TB/s; traffic: PMC-measured HBM bytes per launch "
+                                 "(profiles/, FETCH_SIZE x2 + WRITE_SIZE); issue: GF MACs/s against the "
+                                 "bit-sliced method's VALU floor (8 XOR3 + 26/8 table instructions per "
+                                 "coefficient per 2 KiB at 2.3 cycles per wave instruction on 1024 SIMDs), "
+                                 "the bound that binds at B >= 9 (DESIGN.md Roofline)"},
             "cpu_baseline": cpu,
             "wall_s": round(wall, 4),
         }
@@ -467,6 +489,9 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["c2_decode"]["roundtrip_ok"] = bool(np.array_equal(a, b))
     ctx.free(dWire)
     ctx.free(dDec)
+    out["north_star_grouped_encode"] = grouped_encode(ctx, L_, errors, encs, k, L, rng)
+    out["c2_recode"] = recode_c2(ctx, L_, errors, encs[0], k, L, rng)
+    out["c5_encode_recode_one_gpu"] = c5_one_gpu(ctx, L_, errors, encs[:8], k, L, rng)
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
     out["c1_roundtrip"] = c1_roundtrip(ctx, L_, errors, rng)
     out["encode_two_streams"] = two_streams(L_, errors, k, L, rng)
@@ -475,6 +500,11 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     return out
 
 
+# VALU floor of the bit-sliced method: per coefficient and 2 KiB wave slice 8
+# XOR3 (7.97 on average) + the row's 26 table instructions shared by 8 output
+# rows, 2048 MACs; 1024 SIMDs at 2.4 GHz issuing a wave instruction every 2.3
+# cycles with 4 waves per SIMD (profiles/r01/dispatch_probe.log, straight line).
+VALU_FLOOR_MACS_PER_S = 2048 / (7.97 + 26 / 8) * 1024 * 2.4e9 / 2.3
 # Issue ceiling of the apply kernels: 1024 SIMDs at 2.4 GHz issuing one wave
 # instruction per ~2.35 cycles with 4 waves per SIMD (profiles/r01/dispatch_probe.log),
 # times the GF MACs each instruction carries: gf_bs_kernel issues ~15 per
@@ -484,6 +514,120 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
 ISSUE_PER_S = 1024 * 2.4e9 / 2.35
 MACS_PER_INST_BS = 2048 / 15
 MACS_PER_INST_PERM = 256 / 5
+
+
+def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
+    """North-star shape (BASELINE north_star: encode of a 32 MiB/256
+    generation at >= 70 % of HBM read): `count` coded pieces of each of the G
+    resident generations in ONE launch (rlnc_encoder_group_coded_pieces_device,
+    gf_gemm_kernel with a generation grid dimension), so the launch and ramp
+    are paid once per G x 32 MiB.  HIP events on the context stream."""
+    import ctypes
+    import numpy as np
+    from kodr_amd import device as kdev
+    G = len(encs)
+    arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    res = {"generations_per_launch": G, "kernel": "gf_gemm_kernel (grouped)"}
+    e0, e1 = ctx.event(), ctx.event()
+    for count in (1, 2, 4, 8):
+        V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+        dV, dO = ctx.alloc(V.nbytes), ctx.alloc(G * count * L)
+        ctx.h2d(dV, V)
+        for i in range(5):
+            errors.check(L_.rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, L))
+        ctx.record(e0)
+        for i in range(iters):
+            errors.check(L_.rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, L))
+        ctx.record(e1)
+        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters
+        hbm = G * (k * L + count * (k + L))
+        res[str(count)] = {"us_per_launch": round(t * 1e6, 2), "us_per_generation": round(t / G * 1e6, 3),
+                           "coded_MBps": round(G * count * setbytes(k, L) / t / 1e6, 1),
+                           "hbm_GBps": round(hbm / t / 1e9, 1),
+                           "hbm_frac": round(hbm / t / 1e9 / HBM_PEAK_GBS, 4)}
+        ctx.free(dV)
+        ctx.free(dO)
+    res["note"] = ("hbm = generation read once per piece batch + vectors + pieces, per launch; "
+                   "count=1 is the north-star shape (one coded piece per 32 MiB generation)")
+    return res
+
+
+def recode_c2(ctx, L_, errors, enc, k, L, rng, iters=40):
+    """Full recode at 32 MiB/256 (kodr README.md:111: 1,074.82 MB/s on one
+    i7 core): a recoder holding n = k coded pieces (wire rows drawn by the
+    engine's encoder), B recoded pieces per call, kodr's SetBytes
+    (n+1)(k+L) per piece (benches/full/recoder_test.go:53).  The recoder's
+    bit-sliced twin is built at construction (rlnc_recoder_prepare)."""
+    import ctypes
+    import numpy as np
+    from kodr_amd import device as kdev
+    n, clen = k, k + L
+    pitch = (clen + 255) // 256 * 256
+    dW = ctx.alloc(n * pitch)
+    errors.check(L_.rlnc_encoder_coded_wire_device(enc, n, dW, pitch))
+    rh = ctypes.c_void_p()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    errors.check(L_.rlnc_recoder_create_device(ctx.handle, dW, n, clen, pitch, k, ctypes.byref(rh)))
+    errors.check(L_.rlnc_recoder_prepare(rh))
+    ctx.synchronize()
+    res = {"construct_ms": round((time.perf_counter() - t0) * 1e3, 3), "unit_bytes": (n + 1) * clen,
+           "kodr_published_MBps": 1074.82}
+    e0, e1 = ctx.event(), ctx.event()
+    R = rng.integers(0, 256, (256, n), dtype=np.uint8)
+    dR, dO = ctx.alloc(R.nbytes), ctx.alloc(256 * pitch)
+    ctx.h2d(dR, R)
+    for b in (1, 32, 256):
+        it = iters if b <= 32 else 10
+        for i in range(3):
+            errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, b, dO, pitch))
+        ctx.record(e0)
+        for i in range(it):
+            errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, b, dO, pitch))
+        ctx.record(e1)
+        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / it
+        res[str(b)] = {"us_per_call": round(t * 1e6, 2), "recoded_MBps": round(b * (n + 1) * clen / t / 1e6, 1),
+                       "kernel": "gf_bs_kernel" if b >= 9 else "gf_gemm_kernel"}
+    L_.rlnc_recoder_destroy(rh)
+    for p in (dW, dR, dO):
+        ctx.free(p)
+    return res
+
+
+def c5_one_gpu(ctx, L_, errors, encs, k, L, rng, reps=3):
+    """BASELINE config 5's per-GPU work on one GPU: for each of 8 resident
+    32 MiB/256 generations, k coded pieces in wire layout (device-drawn
+    vectors), a recoder built on those rows, k recoded pieces.  The N>1 run adds
+    the RCCL ring shift between the two (extras.c5_encode_relay_recode)."""
+    import ctypes
+    import numpy as np
+    clen = k + L
+    pitch = (clen + 255) // 256 * 256
+    G = len(encs)
+    dW, dO = ctx.alloc(k * pitch), ctx.alloc(k * pitch)
+    R = rng.integers(0, 256, (k, k), dtype=np.uint8)
+    dR = ctx.alloc(R.nbytes)
+    ctx.h2d(dR, R)
+    best = None
+    for rep in range(reps):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for e in encs:
+            errors.check(L_.rlnc_encoder_coded_wire_device(e, k, dW, pitch))
+            rh = ctypes.c_void_p()
+            errors.check(L_.rlnc_recoder_create_device(ctx.handle, dW, k, clen, pitch, k, ctypes.byref(rh)))
+            errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, k, dO, pitch))
+            L_.rlnc_recoder_destroy(rh)   # synchronises the stream
+        ctx.synchronize()
+        t = time.perf_counter() - t0
+        best = t if best is None else min(best, t)
+    for p in (dW, dO, dR):
+        ctx.free(p)
+    units = G * k * (setbytes(k, L) + (k + 1) * clen)
+    return {"generations": G, "ms": round(best * 1e3, 3), "ms_per_generation": round(best / G * 1e3, 3),
+            "coded_plus_recoded_MBps": round(units / best / 1e6, 1),
+            "note": "per generation: k encoded + k recoded pieces, kodr SetBytes units for both; host wall time, "
+                    "recoder construction (D2D copy of the received rows + twin) included"}
 
 
 def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):

@@ -163,6 +163,21 @@ int rlnc_encoder_coded_pieces_device(rlnc_encoder* enc, const uint8_t* d_vectors
 int rlnc_encoder_coded_wire_device(rlnc_encoder* enc, size_t count, uint8_t* d_wire, size_t wire_pitch);
 /* reseed the device vector stream (reproducible batches for tests/benches) */
 int rlnc_encoder_seed(rlnc_encoder* enc, uint64_t seed);
+/* construction-time preparation (the Go constructors' NewFullRLNCEncoder*,
+ * full/encoder.go:76-107, end here): builds the bit-sliced twin that batches
+ * of >= 9 coded pieces read, so that cost is paid once up front instead of by
+ * the first large batch.  Optional; idempotent.  Async on the ctx stream. */
+int rlnc_encoder_prepare(rlnc_encoder* enc);
+/* Many generations in one launch: coded pieces for each of n_enc resident
+ * generations (full/encoder.go:61-71 once per generation), all encoders on one
+ * ctx with equal piece count k and piece size L.  d_vectors: n_enc blocks of
+ * count x k bytes (generation i at i*count*k); d_out: n_enc blocks of count
+ * rows at out_pitch (generation i's first row at i*count*out_pitch).  Small
+ * batches (the streaming regime, count < 9) run as ONE kernel launch per 32
+ * generations; larger ones fall back to one launch per generation.
+ * Full-RLNC semantics.  Async on the ctx stream. */
+int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
+                                           size_t count, uint8_t* d_out, size_t out_pitch);
 
 /* ---- recoder: full/recoder.go ------------------------------------------ */
 /* NewFullRLNCRecoderWithFlattenData (full/recoder.go:63-70): flat holds
@@ -174,6 +189,9 @@ int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t piec
                                size_t coded_piece_len, size_t pitch, size_t pieces_coded_together,
                                rlnc_recoder** out);
 int rlnc_recoder_destroy(rlnc_recoder* rec);
+/* as rlnc_encoder_prepare: build the held rows' bit-sliced twin up front
+ * (NewFullRLNCRecoder*, full/recoder.go:52-70).  Optional; async. */
+int rlnc_recoder_prepare(rlnc_recoder* rec);
 size_t rlnc_recoder_piece_count(const rlnc_recoder* rec);        /* n held coded pieces */
 size_t rlnc_recoder_coded_piece_len(const rlnc_recoder* rec);    /* k + L */
 /* `count` CodedPiece() calls (full/recoder.go:27-46): r = count x n caller

@@ -254,18 +254,30 @@ bool few_narrow_rows(size_t M, size_t K, size_t ncols) {
   return K <= 32 && ncols <= ((size_t)256 << 10) && (K <= 16 || M <= 16);
 }
 
+// The bit-sliced twin of a resident, immutable X (K rows at pitch ldx), built
+// once: on the first product that needs it, or at construction time through
+// rlnc_encoder_prepare / rlnc_recoder_prepare.
+int build_twin(rlnc_ctx* ctx, const uint8_t* plain, DevBuf& twin, bool& twin_valid, size_t K, size_t ldx,
+               size_t ncols) {
+  if (twin_valid) return RLNC_OK;
+  TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
+  HIPC(kodr_amd::bitslice_rows(plain, twin.p, ldx, K, ncols, ctx->stream));
+  twin_valid = true;
+  return RLNC_OK;
+}
+
+// true when a product of M rows over this resident X takes the bit-sliced kernel
+bool resident_uses_bs(rlnc_ctx* ctx, size_t M, size_t K, size_t ldx, size_t ncols) {
+  return !(M < kBsMinRows || few_narrow_rows(M, K, ncols) || (ldx % 32) ||
+           !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) || !kodr_amd::bs_ready(ctx->device));
+}
+
 // Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
-  if (M < kBsMinRows || few_narrow_rows(M, K, ncols) || (ldx % 32) || !bs_chunk_rows(M, std::max<size_t>(K, 1), ldx, ncols) ||
-      !kodr_amd::bs_ready(ctx->device))
-    return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
-  if (!twin_valid) {
-    TRY(twin.reserve(std::max<size_t>(K * ldx, 1)));
-    HIPC(kodr_amd::bitslice_rows(plain, twin.p, ldx, K, ncols, ctx->stream));
-    twin_valid = true;
-  }
+  if (!resident_uses_bs(ctx, M, K, ldx, ncols)) return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
+  TRY(build_twin(ctx, plain, twin, twin_valid, K, ldx, ncols));
   return gemm_bs(ctx, dA, lda, M, K, twin.p, ldx, dY, ldy, ncols);
 }
 
@@ -634,6 +646,46 @@ int rlnc_encoder_coded_pieces_device(rlnc_encoder* e, const uint8_t* d_vectors, 
                        d_out, out_pitch, e->L);
 }
 
+int rlnc_encoder_prepare(rlnc_encoder* e) {
+  if (!e) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(e->ctx));
+  // any batch of >= kBsMinRows pieces that takes the bit-sliced kernel reads the twin
+  if (!resident_uses_bs(e->ctx, std::max<size_t>(e->k, 64), e->k, e->pitch, e->L)) return RLNC_OK;
+  return build_twin(e->ctx, e->pieces.p, e->pieces_bs, e->bs_valid, e->k, e->pitch, e->L);
+}
+
+int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
+                                           size_t count, uint8_t* d_out, size_t out_pitch) {
+  if (!encs || (n_enc && (!encs[0] || (count && (!d_vectors || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!n_enc || !count) return RLNC_OK;
+  rlnc_encoder* e0 = encs[0];
+  const size_t k = e0->k, L = e0->L;
+  if (out_pitch < L) return RLNC_ERR_INVALID_ARGUMENT;
+  for (size_t i = 1; i < n_enc; i++)
+    if (!encs[i] || encs[i]->ctx != e0->ctx || encs[i]->k != k || encs[i]->L != L) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(e0->ctx));
+  rlnc_ctx* ctx = e0->ctx;
+  const size_t vstride = count * k, ostride = count * out_pitch;
+  // one launch streams up to kGemmGroupMax generations where the product runs on
+  // gf_gemm in one row chunk; otherwise one product per generation
+  const bool grouped = !resident_uses_bs(ctx, count, k, e0->pitch, L) && k * e0->pitch < kMaxDescBytes &&
+                       (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
+  if (!grouped) {
+    for (size_t i = 0; i < n_enc; i++)
+      TRY(rlnc_encoder_coded_pieces_device(encs[i], d_vectors + i * vstride, count, d_out + i * ostride, out_pitch));
+    return RLNC_OK;
+  }
+  const uint8_t* xs[kodr_amd::kGemmGroupMax];
+  for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
+    const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
+    for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces.p;
+    const kodr_amd::GemmGroupArgs grp{(int)n, xs, vstride, ostride};
+    HIPC(kodr_amd::gf_gemm(d_vectors + g0 * vstride, k, count, k, xs[0], e0->pitch, d_out + g0 * ostride, out_pitch,
+                           L, ctx->stream, nullptr, false, &grp));
+  }
+  return RLNC_OK;
+}
+
 int rlnc_encoder_seed(rlnc_encoder* e, uint64_t seed) {
   if (!e) return RLNC_ERR_INVALID_ARGUMENT;
   e->seed = seed;
@@ -737,6 +789,13 @@ int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t n, s
   }
   *out = r;
   return RLNC_OK;
+}
+
+int rlnc_recoder_prepare(rlnc_recoder* r) {
+  if (!r) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(r->ctx));
+  if (!resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->pitch, r->clen)) return RLNC_OK;
+  return build_twin(r->ctx, r->flat.p, r->flat_bs, r->bs_valid, r->n, r->pitch, r->clen);
 }
 
 int rlnc_recoder_destroy(rlnc_recoder* r) {

@@ -70,11 +70,19 @@ __device__ __forceinline__ void lds_barrier() {
 // Coefficient tables for (MT x KC) are staged per K-chunk into LDS
 // (double-buffered when K > KC) and read back as (S-way) broadcasts.  Rows are
 // streamed through a P-deep ring of loads that runs across K-chunk barriers.
-template <int MT, int KW, int S, int RC, int P, int MODE = 0>
+//
+// Grouped launch (gridDim.y > 1): workgroup row y works on generation y of a
+// group of independent products that share M, K, ncols and the pitches --
+// X = xg.x[y], A and Y advanced by y strides -- so one launch streams G
+// resident generations (full/encoder.go:61-71 once per generation) and pays
+// the launch and ramp once.  AUX is the buffer loads' cache policy (2 = nt,
+// for rows read once per launch).
+template <int MT, int KW, int S, int RC, int P, int MODE = 0, int AUX = 0>
 __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K,
     const uint8_t* __restrict__ X, size_t ldx,
-    uint8_t* __restrict__ Y, size_t ldy, int ncols, int nx, int ny, int nbuf, int accum) {
+    uint8_t* __restrict__ Y, size_t ldy, int ncols, int nx, int ny, int nbuf, int accum,
+    GemmGroup xg, size_t a_gstride, size_t y_gstride) {
   static_assert(S == 1 || S == 2 || S == 4, "lane groups");
   static_assert(RC % (S * P) == 0, "ring: P row-steps of S rows must divide RC");
   constexpr int KC = KW * RC;
@@ -95,6 +103,12 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
   const int tx = (b / (8 * ny)) * 8 + (b & 7);
   if (tx >= nx) return;
   const int m0 = ty * MT;
+  if (gridDim.y > 1) {
+    const int gi = blockIdx.y;
+    X = xg.x[gi];
+    A += (size_t)gi * a_gstride;
+    Y += (size_t)gi * y_gstride;
+  }
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -116,7 +130,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
       const uint32_t h = (uint32_t)(row_of(q) * 0x9E3779B1u) ^ (uint32_t)col;
       return make_uint4(h, h * 3u, h * 5u, h * 7u);
     }
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, row_of(q) * ildx + col, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, row_of(q) * ildx + col, 0, AUX);
     return make_uint4(v[0], v[1], v[2], v[3]);
   };
 
@@ -283,9 +297,11 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
   }
 }
 
-template <int MT, int KW, int S, int RC, int P, int MODE = 0>
+// One product, or (grp != nullptr) grp->n products of the same shape in one launch.
+template <int MT, int KW, int S, int RC, int P, int MODE = 0, int AUX = 0>
 hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, size_t ldx,
-                  uint8_t* Y, size_t ldy, int ncols, hipStream_t stream, int accum = 0) {
+                  uint8_t* Y, size_t ldy, int ncols, hipStream_t stream, int accum = 0,
+                  const GemmGroupArgs* grp = nullptr) {
   constexpr int KC = KW * RC;
   constexpr int CB = 1024 / S;
   const int nx = (ncols + CB - 1) / CB;
@@ -294,8 +310,18 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
   const int nx8 = (nx + 7) / 8 * 8;
   const size_t lds = (size_t)nbuf * KC * MT * (16 + 4) + (KW > 1 ? (size_t)MT * 4 * (64 / S) * 4 : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, S, RC, P, MODE>), dim3(nx8 * ny), dim3(64 * KW), lds, stream,
-                     A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf, accum);
+  GemmGroup xg{};
+  size_t as = 0, ys = 0;
+  unsigned ng = 1;
+  if (grp) {
+    if (grp->n < 1 || grp->n > kGemmGroupMax) return hipErrorInvalidValue;
+    for (int i = 0; i < grp->n; i++) xg.x[i] = grp->x[i];
+    as = grp->a_stride;
+    ys = grp->y_stride;
+    ng = (unsigned)grp->n;
+  }
+  hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, S, RC, P, MODE, AUX>), dim3(nx8 * ny, ng), dim3(64 * KW), lds, stream,
+                     A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf, accum, xg, as, ys);
   return hipGetLastError();
 }
 
@@ -487,7 +513,7 @@ static bool env_config(GemmConfig* g) {
 
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
-                   const GemmConfig* force, bool accumulate) {
+                   const GemmConfig* force, bool accumulate, const GemmGroupArgs* grp) {
   const int acc = accumulate ? 1 : 0;
   if (M == 0 || ncols == 0) return hipSuccess;
   GemmConfig g = force ? *force : choose_gemm_config(M, K, ncols);
@@ -509,9 +535,16 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
     return launch<8, 4, 1, 64, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
 #endif
   (void)mode;
-#define KODR_TRY(MT_, KW_, S_, RC_, P_)                                               \
-  if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))             \
-    return launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc);
+  // grouped launches stream G generations once each per launch: nt loads
+  // (KODR_GROUP_AUX in tuning builds)
+  int aux = grp ? kGroupAux : 0;
+#ifdef KODR_TUNE_MODES
+  if (const char* e = getenv("KODR_GROUP_AUX")) aux = atoi(e);
+#endif
+#define KODR_TRY(MT_, KW_, S_, RC_, P_)                                                         \
+  if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))                       \
+    return aux == 2 ? launch<MT_, KW_, S_, RC_, P_, 0, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc, grp) \
+                    : launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc, grp);
   KODR_TRY(1, 1, 2, 16, 8)
   KODR_TRY(2, 1, 2, 16, 8)
   KODR_TRY(4, 1, 2, 16, 8)

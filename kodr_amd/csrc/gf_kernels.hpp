@@ -15,12 +15,28 @@ struct GemmConfig {
 
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols);
 
+// A group of independent products of one shape (M, K, ncols, pitches) in one
+// launch: product i reads X = x[i], A + i * a_stride and writes Y + i * y_stride.
+constexpr int kGemmGroupMax = 32;
+struct GemmGroup {
+  const uint8_t* x[kGemmGroupMax];
+};
+struct GemmGroupArgs {
+  int n;
+  const uint8_t* const* x;
+  size_t a_stride, y_stride;
+};
+// cache policy of a grouped launch's row loads (2 = nt: each generation is
+// read once per launch)
+constexpr int kGroupAux = 2;
+
 // Y[m][j] = XOR_k A[m][k] * X[k][j], m < M, j < ncols.  All pointers device.
 // accumulate: Y[m][j] ^= that product instead (one row chunk of a K-split).
 // ldx/ldy multiples of 16 and >= ncols; X rows readable up to round_up(ncols,16).
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
-                   const GemmConfig* force = nullptr, bool accumulate = false);
+                   const GemmConfig* force = nullptr, bool accumulate = false,
+                   const GemmGroupArgs* group = nullptr);
 
 // dst (pitch dpitch) = width x rows contiguous bytes of host-mapped pinned
 // memory (a device pointer of a hipHostMalloc buffer), copied by a kernel

@@ -1,0 +1,180 @@
+"""GPU parity of the exact launches bench.py times, byte for byte against the
+CPU oracle (oracle/kodr_oracle.c, a restatement of full/encoder.go:61-71 and
+full/recoder.go:27-46):
+
+- the headline: B coded pieces of a prepared 32 MiB/256 generation through
+  rlnc_encoder_coded_pieces_device (B = 32 is the bench's step; 64 and 256 are
+  the sweep's), every byte of every piece;
+- the grouped multi-generation launch (rlnc_encoder_group_coded_pieces_device,
+  the north-star leg): every generation's pieces, small shapes, more than one
+  launch's worth of generations, the bit-sliced fallback, C2-sized generations;
+- a prepared recoder at C2 (the bench's recode leg).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from kodr_amd import _lib, errors
+
+pytestmark = pytest.mark.gpu
+U8P = _lib._u8p
+
+
+def ptr(a):
+    return a.ctypes.data_as(U8P)
+
+
+def make_encoder(ctx, P, prepare=True):
+    h = ctypes.c_void_p()
+    k, L = P.shape
+    errors.check(_lib.lib().rlnc_encoder_create(ctx.handle, 0, ptr(np.ascontiguousarray(P)), k, L,
+                                                ctypes.byref(h)))
+    if prepare:
+        errors.check(_lib.lib().rlnc_encoder_prepare(h))
+    return h
+
+
+@pytest.fixture(scope="module")
+def c2_generation():
+    rng = np.random.default_rng(0x5EED32)
+    return rng.integers(0, 256, (256, 131072), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("B", [32, 64, 256])
+def test_headline_launch_full_compare(gpu_ctx, c2_generation, B):
+    # bench.py's step: device vectors -> B pieces at pitch L, bit-sliced kernel
+    P = c2_generation
+    k, L = P.shape
+    rng = np.random.default_rng(B)
+    V = rng.integers(0, 256, (B, k), dtype=np.uint8)
+    V[0] = 0                     # the zero vector codes the zero piece
+    V[1] = 0
+    V[1, 7] = 1                  # a unit vector codes piece 7 itself
+    e = make_encoder(gpu_ctx, P)
+    dV, dO = gpu_ctx.alloc(V.nbytes), gpu_ctx.alloc(B * L + 64)
+    try:
+        gpu_ctx.h2d(dV, V)
+        gpu_ctx.h2d(dO + B * L, np.full(64, 0xA5, np.uint8))   # canary past the last piece
+        errors.check(_lib.lib().rlnc_encoder_coded_pieces_device(e, dV, B, dO, L))
+        gpu_ctx.synchronize()
+        got = gpu_ctx.d2h(dO, B * L + 64)
+    finally:
+        gpu_ctx.free(dV)
+        gpu_ctx.free(dO)
+        _lib.lib().rlnc_encoder_destroy(e)
+    ref = oracle.encode(P, V)
+    assert np.array_equal(got[:B * L].reshape(B, L), ref)
+    assert (got[B * L:] == 0xA5).all()
+    assert not ref[0].any() and np.array_equal(ref[1], P[7])
+
+
+def test_prepare_matches_lazy_twin(gpu_ctx):
+    # prepare (eager twin) and the lazy twin of the first large batch give
+    # the same bytes; prepare is idempotent
+    rng = np.random.default_rng(11)
+    k, L = 64, 8192 + 32
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V = rng.integers(0, 256, (20, k), dtype=np.uint8)
+    outs = []
+    for prep in (0, 1, 2):
+        e = make_encoder(gpu_ctx, P, prepare=False)
+        for _ in range(prep):
+            errors.check(_lib.lib().rlnc_encoder_prepare(e))
+        out = np.empty((20, k + L), np.uint8)
+        errors.check(_lib.lib().rlnc_encoder_coded_pieces(e, ptr(V), 20, ptr(out)))
+        _lib.lib().rlnc_encoder_destroy(e)
+        outs.append(out)
+    ref = oracle.encode(P, V)
+    for out in outs:
+        assert np.array_equal(out[:, k:], ref)
+
+
+def group_run(ctx, gens, count, V, out_pitch=None, expect=0):
+    """Encode `count` pieces of every generation in one grouped call; returns
+    (G, count, L) from the device output."""
+    G = len(gens)
+    k, L = gens[0].shape
+    out_pitch = out_pitch or L
+    encs = [make_encoder(ctx, P, prepare=False) for P in gens]
+    arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    dV, dO = ctx.alloc(max(V.nbytes, 1)), ctx.alloc(G * count * out_pitch + 64)
+    try:
+        ctx.h2d(dV, V)
+        ctx.h2d(dO, np.full(G * count * out_pitch + 64, 0xA5, np.uint8))
+        st = _lib.lib().rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, out_pitch)
+        assert st == expect
+        ctx.synchronize()
+        raw = ctx.d2h(dO, G * count * out_pitch + 64)
+    finally:
+        ctx.free(dV)
+        ctx.free(dO)
+        for e in encs:
+            _lib.lib().rlnc_encoder_destroy(e)
+    assert (raw[G * count * out_pitch:] == 0xA5).all()
+    rows = raw[:G * count * out_pitch].reshape(G, count, out_pitch)
+    if out_pitch > L:
+        assert (rows[:, :, L:] == 0xA5).all(), "wrote past L"
+    return rows[:, :, :L]
+
+
+@pytest.mark.parametrize("G,k,L,count", [(1, 16, 4096, 1), (3, 16, 4096 + 16, 2), (5, 100, 8192 + 48, 1),
+                                         (8, 256, 65536, 4), (40, 32, 1024, 1), (33, 64, 2048, 8),
+                                         (6, 64, 4096, 12), (4, 20, 1000, 3)])
+def test_grouped_encode_vs_oracle(gpu_ctx, G, k, L, count):
+    # (40, ...) and (33, ...) span two launches of <= 32 generations; count 12
+    # takes the per-generation (bit-sliced) fallback; L = 1000 is not a
+    # multiple of 16 (ragged last chunk, padded pitch)
+    rng = np.random.default_rng(G * 1000 + k + count)
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+    got = group_run(gpu_ctx, gens, count, V, out_pitch=(L + 15) // 16 * 16 + 32)
+    for g in range(G):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
+def test_grouped_encode_c2_generations(gpu_ctx):
+    # the north-star shape: one coded piece of each of 4 generations of
+    # 32 MiB / 256 in one launch
+    rng = np.random.default_rng(0x6E5)
+    gens = [rng.integers(0, 256, (256, 131072), dtype=np.uint8) for _ in range(4)]
+    V = rng.integers(0, 256, (4, 1, 256), dtype=np.uint8)
+    got = group_run(gpu_ctx, gens, 1, V)
+    for g in range(4):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
+def test_grouped_encode_rejects_mixed_shapes(gpu_ctx):
+    rng = np.random.default_rng(5)
+    a = make_encoder(gpu_ctx, rng.integers(0, 256, (16, 1024), dtype=np.uint8), prepare=False)
+    b = make_encoder(gpu_ctx, rng.integers(0, 256, (17, 1024), dtype=np.uint8), prepare=False)
+    arr = (ctypes.c_void_p * 2)(a.value, b.value)
+    dV = gpu_ctx.alloc(64)
+    try:
+        st = _lib.lib().rlnc_encoder_group_coded_pieces_device(arr, 2, dV, 1, dV, 1024)
+        assert st == -1  # RLNC_ERR_INVALID_ARGUMENT
+    finally:
+        gpu_ctx.free(dV)
+        _lib.lib().rlnc_encoder_destroy(a)
+        _lib.lib().rlnc_encoder_destroy(b)
+
+
+def test_prepared_recoder_c2(gpu_ctx, c2_generation):
+    # the bench's recode leg: n = k = 256 wire rows, B = 32 recoded pieces
+    P = c2_generation
+    k, L = P.shape
+    rng = np.random.default_rng(77)
+    n, clen = k, k + L
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    flat = np.concatenate([V, oracle.encode(P, V)], axis=1)
+    rh = ctypes.c_void_p()
+    errors.check(_lib.lib().rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, n, k, ctypes.byref(rh)))
+    errors.check(_lib.lib().rlnc_recoder_prepare(rh))
+    R = rng.integers(0, 256, (32, n), dtype=np.uint8)
+    out = np.empty((32, clen), np.uint8)
+    try:
+        errors.check(_lib.lib().rlnc_recoder_coded_pieces(rh, ptr(R), 32, ptr(out)))
+    finally:
+        _lib.lib().rlnc_recoder_destroy(rh)
+    assert np.array_equal(out, oracle.recode(flat, k, R))
