@@ -242,7 +242,7 @@ def main():
         extras.update(run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng))
     if world > 1 and not args.no_extras:
         try:
-            c5 = run_relay(ctx, L_, errors, encs[0], k, L, rng, torch, dist, kdist)
+            c5 = run_relay(HipRelayEngine(ctx, L_, errors, encs[0]), k, L, rng, torch, dist, kdist)
         except Exception as e:  # secondary measurement: never lose the headline line
             c5 = {"error": repr(e)[:300]}
         if rank == 0:
@@ -309,50 +309,78 @@ def pmc_traffic(B, k, L):
         return json.load(f).get("hbm_bytes_per_launch")
 
 
-def run_relay(ctx, L_, errors, enc, k, L, rng, torch, dist, kdist):
+class HipRelayEngine:
+    """The engine's side of the config-5 relay hop (C ABI on the GPU): k
+    coded pieces of the rank's generation as wire rows with device-drawn
+    vectors, and a recoder built on the rows received."""
+
+    def __init__(self, ctx, L_, errors, enc):
+        self.ctx, self.L_, self.errors, self.enc = ctx, L_, errors, enc
+
+    def encode_wire(self, send, count, pitch):
+        self.errors.check(self.L_.rlnc_encoder_coded_wire_device(self.enc, count, send.data_ptr(), pitch))
+
+    def recode(self, recv, n, k, clen, pitch, dR, count, out):
+        import ctypes
+        rh = ctypes.c_void_p()
+        self.errors.check(self.L_.rlnc_recoder_create_device(self.ctx.handle, recv.data_ptr(), n, clen, pitch, k,
+                                                             ctypes.byref(rh)))
+        self.errors.check(self.L_.rlnc_recoder_coded_pieces_device(rh, dR, count, out.data_ptr(), pitch))
+        self.L_.rlnc_recoder_destroy(rh)
+
+    def upload(self, R, torch):
+        t = torch.from_numpy(R.reshape(-1)).to("cuda")
+        return t, t.data_ptr()
+
+    def synchronize(self):
+        self.ctx.synchronize()
+
+
+def run_relay(engine, k, L, rng, torch, dist, kdist, device="cuda", reps=6, keep=False):
     """BASELINE config 5 on N GPUs: every rank encodes k coded pieces of its
-    generation (wire layout), ring-shifts them to rank+1 over RCCL/xGMI, and
-    recodes the k pieces it received.  Returns per-phase times (max over ranks)."""
-    import ctypes
+    generation (wire layout, kodr_amd.dist.wire_pitch), ring-shifts them to
+    rank+1 over RCCL/xGMI, and recodes the k pieces it received.  Returns
+    per-phase times (max over ranks); keep=True also returns the last
+    repetition's buffers (tests check them against the oracle)."""
     import numpy as np
-    from kodr_amd import device as kdev
     clen = k + L
-    pitch = (clen + 255) // 256 * 256
-    send = torch.zeros(k * pitch, dtype=torch.uint8, device="cuda")
+    pitch = kdist.wire_pitch(k, L)
+    send = torch.zeros(k * pitch, dtype=torch.uint8, device=device)
     recv = torch.empty_like(send)
-    out = torch.empty_like(send)
+    out = torch.zeros_like(send)
     Rv = rng.integers(0, 256, (k, k), dtype=np.uint8)
-    dR = ctx.alloc(Rv.nbytes)
-    ctx.h2d(dR, Rv)
+    Rkeep, dR = engine.upload(Rv, torch)
     times = {"encode": [], "exchange": [], "recode": []}
-    for rep in range(6):
-        torch.cuda.synchronize()
+    for rep in range(reps):
+        engine.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        # k wire rows [vector | piece], vectors drawn on the device
-        errors.check(L_.rlnc_encoder_coded_wire_device(enc, k, send.data_ptr(), pitch))
-        ctx.synchronize()
+        engine.encode_wire(send, k, pitch)     # k wire rows [vector | piece]
+        engine.synchronize()
         t1 = time.perf_counter()
         kdist.ring_shift(send, recv)
-        torch.cuda.synchronize()
+        if device == "cuda":
+            torch.cuda.synchronize()
         t2 = time.perf_counter()
-        rh = ctypes.c_void_p()
-        errors.check(L_.rlnc_recoder_create_device(ctx.handle, recv.data_ptr(), k, clen, pitch, k,
-                                                   ctypes.byref(rh)))
-        errors.check(L_.rlnc_recoder_coded_pieces_device(rh, dR, k, out.data_ptr(), pitch))
-        ctx.synchronize()
+        engine.recode(recv, k, k, clen, pitch, dR, k, out)
+        engine.synchronize()
         t3 = time.perf_counter()
-        L_.rlnc_recoder_destroy(rh)
         if rep > 0:
             times["encode"].append(t1 - t0)
             times["exchange"].append(t2 - t1)
             times["recode"].append(t3 - t2)
-    ctx.free(dR)
     res = {}
     for name, ts in times.items():
-        res[name + "_ms"] = round(kdist.max_over_ranks(min(ts), device="cuda") * 1e3, 4)
+        res[name + "_ms"] = round(kdist.max_over_ranks(min(ts), device=device) * 1e3, 4)
     res["exchange_GBps_per_link"] = round(k * pitch / (res["exchange_ms"] / 1e3) / 1e9, 2)
+    # whole-job relay rate: every rank's k recoded pieces (kodr SetBytes (n+1)(k+L),
+    # benches/full/recoder_test.go:53) over the slowest rank's encode + exchange + recode
+    t_hop = (res["encode_ms"] + res["exchange_ms"] + res["recode_ms"]) / 1e3
+    res["relay_recoded_MBps"] = round(kdist.aggregate_rate(k, (k + 1) * clen, t_hop, dist.get_world_size()), 1)
     res["note"] = "recode includes staging the received rows into the recoder (one D2D copy)"
+    if keep:
+        return res, {"send": send.cpu().numpy().reshape(k, pitch), "recv": recv.cpu().numpy().reshape(k, pitch),
+                     "out": out.cpu().numpy().reshape(k, pitch), "R": Rv, "pitch": pitch, "clen": clen}
     return res
 
 

@@ -503,6 +503,23 @@ GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   return {8, 4, 1, 4};
 }
 
+// Grouped launches (G generations of one shape per launch) stream: every
+// workgroup owns a 1 KiB column chunk of one generation and its waves run long
+// row sequences through a deep ring of nt loads.  Measured at K = 256, 128 KiB
+// rows (tools/group_sweep.py, profiles/r02/group_sweep*.log): one coded piece
+// per generation 5.3-5.5 us per 32 MiB generation (6.1-6.3 TB/s) with one wave
+// per workgroup for G >= 8, 5.5 us with 8 waves splitting K for G = 4, against
+// 6.4-6.9 us on the single-launch tile {1, 16, 2}; 2-8 pieces per generation
+// 10-30 % faster on 4-wave tiles.
+GemmConfig choose_group_config(size_t M, size_t K, size_t ncols, size_t G) {
+  if (K < 64) return choose_gemm_config(M, K, ncols);
+  if (M <= 1) return G >= 8 ? GemmConfig{1, 1, 1, 16} : GemmConfig{1, 8, 1, 8};
+  if (M <= 2) return {2, 4, 1, 8};
+  if (M <= 4) return {4, 4, 1, 8};
+  if (M <= 8) return {8, 4, 1, 8};
+  return choose_gemm_config(M, K, ncols);
+}
+
 // KODR_GEMM_CFG="mt,kw,s" forces a tile (tuning runs only; see tools/tune_gemm.py)
 static bool env_config(GemmConfig* g) {
   const char* s = getenv("KODR_GEMM_CFG");
@@ -516,7 +533,8 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
                    const GemmConfig* force, bool accumulate, const GemmGroupArgs* grp) {
   const int acc = accumulate ? 1 : 0;
   if (M == 0 || ncols == 0) return hipSuccess;
-  GemmConfig g = force ? *force : choose_gemm_config(M, K, ncols);
+  GemmConfig g = force ? *force : grp ? choose_group_config(M, K, ncols, (size_t)grp->n)
+                                      : choose_gemm_config(M, K, ncols);
   GemmConfig ge;
   if (!force && env_config(&ge)) g = ge;
   const int iM = (int)M, iK = (int)K, ild = (int)lda, inc = (int)ncols;
@@ -545,6 +563,16 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))                       \
     return aux == 2 ? launch<MT_, KW_, S_, RC_, P_, 0, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc, grp) \
                     : launch<MT_, KW_, S_, RC_, P_>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream, acc, grp);
+  // streaming tiles for grouped launches of few rows (one 1 KiB column chunk
+  // per workgroup, long per-wave row runs through a deep ring)
+  KODR_TRY(1, 4, 1, 64, 8)
+  KODR_TRY(1, 4, 1, 64, 16)
+  KODR_TRY(1, 2, 1, 128, 16)
+  KODR_TRY(1, 1, 1, 256, 16)
+  KODR_TRY(1, 8, 1, 32, 8)
+  KODR_TRY(1, 8, 2, 32, 16)
+  KODR_TRY(2, 4, 1, 64, 8)
+  KODR_TRY(4, 4, 1, 64, 8)
   KODR_TRY(1, 1, 2, 16, 8)
   KODR_TRY(2, 1, 2, 16, 8)
   KODR_TRY(4, 1, 2, 16, 8)

@@ -27,6 +27,13 @@ def shard_generations(n_generations, world_size, rank):
     return list(range(start, start + base + (1 if rank < extra else 0)))
 
 
+def wire_pitch(k, L):
+    """Row pitch of the engine's device wire rows (vector ++ piece, k + L
+    bytes, CodedPiece.Flatten data.go:52-57) padded to the 256-byte alignment
+    of its recoder and decoder rows (capi.cpp kPitchAlign)."""
+    return (k + L + 255) // 256 * 256
+
+
 def ring_shift(send, recv, group=None):
     """Send `send` to rank+1 and receive into `recv` from rank-1 (one P2P step)."""
     import torch.distributed as dist

@@ -81,6 +81,92 @@ def test_two_rank_relay_and_aggregation():
     assert res[0][4] == pytest.approx(2 * 10 * 1e6 / 1.5 / 1e6)
 
 
+class OracleRelayEngine:
+    """CPU stand-in for bench.HipRelayEngine: the same wire layout (rows of
+    k + L bytes at kodr_amd.dist.wire_pitch) produced and recoded by the
+    oracle, on CPU tensors."""
+
+    def __init__(self, P, seed):
+        self.P = P
+        self.rng = np.random.default_rng(seed)
+
+    def encode_wire(self, send, count, pitch):
+        import oracle
+        k, L = self.P.shape
+        V = self.rng.integers(0, 256, (count, k), dtype=np.uint8)
+        rows = send.numpy().reshape(-1, pitch)
+        rows[:count, :k] = V
+        rows[:count, k:k + L] = oracle.encode(self.P, V)
+
+    def recode(self, recv, n, k, clen, pitch, R, count, out):
+        import oracle
+        src = recv.numpy().reshape(-1, pitch)[:n, :clen]
+        out.numpy().reshape(-1, pitch)[:count, :clen] = oracle.recode(np.ascontiguousarray(src), k, R[:count])
+
+    def upload(self, R, torch):
+        return R, R
+
+    def synchronize(self):
+        pass
+
+
+def _relay_worker(rank, ws, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import oracle
+    from kodr_amd import dist as kd
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=ws)
+    try:
+        k, L = 16, 1000
+        P = np.random.default_rng(200 + rank).integers(0, 256, (k, L), dtype=np.uint8)
+        eng = OracleRelayEngine(P, 300 + rank)
+        res, buf = bench.run_relay(eng, k, L, np.random.default_rng(7 + rank), torch, dist, kd, device="cpu",
+                                   reps=2, keep=True)
+        pitch, clen = buf["pitch"], buf["clen"]
+        assert pitch == (k + L + 255) // 256 * 256 and clen == k + L
+        sends = [None] * ws
+        dist.all_gather_object(sends, buf["send"])
+        prev = (rank - 1) % ws
+        shifted = np.array_equal(buf["recv"], sends[prev])
+        recoded = np.array_equal(buf["out"][:, :clen], oracle.recode(np.ascontiguousarray(buf["recv"][:, :clen]), k,
+                                                                         buf["R"]))
+        # the recoded rows decode the previous rank's generation
+        d = oracle.Decoder(k)
+        for row in buf["out"][:, :clen]:
+            if d.add(row[:k], row[k:]) == 3:
+                break
+        Pp = np.random.default_rng(200 + prev).integers(0, 256, (k, L), dtype=np.uint8)
+        decoded = d.is_decoded() and np.array_equal(np.stack([d.get_piece(i)[1] for i in range(k)]), Pp)
+        q.put((rank, shifted, recoded, decoded, sorted(res)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_run_relay_two_ranks():
+    # bench.py's own config-5 relay (run_relay: encode -> ring shift -> recode,
+    # max-over-ranks timing, aggregate rate) with an oracle engine on CPU tensors
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_relay_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(ws))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, shifted, recoded, decoded, keys in res:
+        assert shifted and recoded and decoded, rank
+        assert {"encode_ms", "exchange_ms", "recode_ms", "relay_recoded_MBps"} <= set(keys)
+
+
 def test_shard_generations_partition():
     from kodr_amd.dist import shard_generations
     for n in range(0, 20):
