@@ -879,7 +879,9 @@ int dec_reserve_rows(rlnc_decoder* d, size_t need, size_t have) {
   DevBuf nb;
   nb.bind(d->ctx->device, d->ctx->stream);
   TRY(nb.reserve(nrows * d->pitch));
-  HIPC(hipMemsetAsync(nb.p, 0, nrows * d->pitch, d->ctx->stream));
+  // the kernels read only rows < received, each through its pitch; only a
+  // pitch past the piece length has bytes (zero padding) no copy writes
+  if (d->pitch != d->L) HIPC(hipMemsetAsync(nb.p, 0, nrows * d->pitch, d->ctx->stream));
   if (d->recv.p && have)
     HIPC(hipMemcpyAsync(nb.p, d->recv.p, have * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
   d->recv.release();  // back to the pool, reusable once the stream passes the copy
@@ -1047,9 +1049,16 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   TRY(dec_check(d, k, rows + k, piece_len));
   const uint8_t* vecs = rows;
   size_t vpitch = pitch;
-  if (dev) {  // one strided copy of all coding vectors; the pieces never leave the device
+  // device rows: one strided copy of all coding vectors to the host (the
+  // pieces never leave the device).  A small one is only started here and
+  // awaited after the piece copies below are enqueued behind it.
+  int vticket = -1;
+  if (dev) {
     d->hvecs.resize(count * k);
-    HIPC(d->ctx->stage.d2h(d->hvecs.data(), k, rows, pitch, k, count, d->ctx->stream));
+    if (count * k <= kodr_amd::kDownloadSmallMax)
+      HIPC(d->ctx->stage.d2h_small_begin(rows, pitch, k, count, d->ctx->stream, &vticket));
+    else
+      HIPC(d->ctx->stage.d2h(d->hvecs.data(), k, rows, pitch, k, count, d->ctx->stream));
     vecs = d->hvecs.data();
     vpitch = k;
   }
@@ -1066,22 +1075,32 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   if (pre) {
     TRY(dec_reserve_rows(d, row0 + pre, row0));
     uint8_t* dst = d->recv.p + row0 * d->pitch;
-    if (dev)
-      HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
-    else
-      HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice, d->ctx->stream));
-    if (pre >= kBsMinRowsDecode && d->pitch % 32 == 0 &&
-        !few_narrow_rows(d->core.piece_count(), row0 + pre, d->L)) {  // else dec_gemm takes gf_gemm
+    const bool twin = pre >= kBsMinRowsDecode && d->pitch % 32 == 0 &&
+                      !few_narrow_rows(d->core.piece_count(), row0 + pre, d->L);  // else dec_gemm takes gf_gemm
+    if (twin) {
       d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
       if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
         TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
         d->bs_rows = 0;
       }
-      HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
-                                   d->pitch, row0 + pre - d->bs_rows, d->L, d->ctx->stream));
-      twin_end = row0 + pre;
     }
+    // device rows whose twin starts here: copy and bit-slice in one pass
+    const bool fused = twin && dev && d->bs_rows == row0 && d->L % 32 == 0 &&
+                       kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, d->recv_bs.p + row0 * d->pitch, d->pitch,
+                                                    pre, d->L, d->ctx->stream) == hipSuccess;
+    if (!fused) {
+      if (dev)
+        HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
+      else
+        HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice,
+                              d->ctx->stream));
+      if (twin)
+        HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
+                                     d->pitch, row0 + pre - d->bs_rows, d->L, d->ctx->stream));
+    }
+    if (twin) twin_end = row0 + pre;
   }
+  if (vticket >= 0) HIPC(d->ctx->stage.d2h_small_end(vticket, d->hvecs.data(), k, k, count));
   // coefficient side, exactly as repeated AddPiece calls
   size_t n = 0;
   const int st = d->core.add_many(vecs, vpitch, count, &n);

@@ -12,8 +12,64 @@ namespace kodr_amd {
 
 using hostgf::T;
 
-DecoderCore::DecoderCore(size_t piece_count) : k_(piece_count) {
+DecoderCore::DecoderCore(size_t piece_count) : k_(piece_count), ucnt_(piece_count, 0) {
   ensure_tcap(std::max<size_t>(k_ + 8, 16));
+}
+
+// column of the only non-zero byte of v[0..n), or -1 (none, or several)
+static int32_t unit_col(const uint8_t* v, size_t n) {
+  int32_t c = -1;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {  // 8 bytes per step; a coded row exits at once
+    uint64_t w;
+    memcpy(&w, v + i, 8);
+    if (!w) continue;
+    const unsigned b = (unsigned)__builtin_ctzll(w) >> 3;
+    if (c >= 0 || (w >> (8 * b) >> 8)) return -1;  // a second non-zero byte
+    c = (int32_t)(i + b);
+  }
+  for (; i < n; i++) {
+    if (!v[i]) continue;
+    if (c >= 0) return -1;
+    c = (int32_t)i;
+  }
+  return c;
+}
+
+void DecoderCore::push_row(uint8_t* row, int32_t p, int32_t t) {
+  rows_.push_back(row);
+  up_.push_back(p);
+  ut_.push_back(t);
+  if (p >= 0) ucnt_[p]++;
+  else ndense_++;
+}
+
+void DecoderCore::forget_row(size_t pos) {
+  if (up_[pos] >= 0) ucnt_[up_[pos]]--;
+  else ndense_--;
+}
+
+void DecoderCore::pop_row() {
+  forget_row(rows_.size() - 1);
+  rows_.pop_back();
+  up_.pop_back();
+  ut_.pop_back();
+}
+
+void DecoderCore::swap_rows(size_t a, size_t b) {
+  std::swap(rows_[a], rows_[b]);
+  std::swap(up_[a], up_[b]);
+  std::swap(ut_[a], ut_[b]);
+  std::swap(touched_[a], touched_[b]);
+}
+
+// row `pos` is about to change: it is no longer known to be a unit row
+void DecoderCore::make_dense(size_t pos) {
+  if (up_[pos] < 0) return;
+  ucnt_[up_[pos]]--;
+  up_[pos] = -1;
+  ndense_++;
+  dense_pos_.push_back(pos);
 }
 
 void DecoderCore::ensure_tcap(size_t need) {
@@ -39,20 +95,45 @@ void DecoderCore::ensure_tcap(size_t need) {
 
 // rows_[dst] ^= q * rows_[src] over coefficient columns [from, k) and all T
 // columns (the coded half in kodr is updated over its whole width, :66-73).
+// A unit source row has two non-zero bytes: the same result in two byte ops.
 void DecoderCore::axpy_row(size_t dst, size_t src, uint8_t q, size_t from) {
-  hostgf::axpy(rows_[dst] + from, rows_[src] + from, k_ - from + received_, q);
+  const int32_t p = up_[src];
+  if (p >= 0) {
+    const hostgf::Tables& t = T();
+    uint8_t* d = rows_[dst];
+    const uint8_t* s = rows_[src];
+    if ((size_t)p >= from) d[p] ^= t.mul(q, s[p]);
+    d[k_ + ut_[src]] ^= t.mul(q, s[k_ + ut_[src]]);
+  } else {
+    hostgf::axpy(rows_[dst] + from, rows_[src] + from, k_ - from + received_, q);
+  }
+  make_dense(dst);
   touched_[dst] = 1;
+}
+
+// rows_[i][from..) *= q (a unit row stays a unit row)
+void DecoderCore::scale_row(size_t i, size_t from, uint8_t q) {
+  const int32_t p = up_[i];
+  if (p >= 0) {
+    const hostgf::Tables& t = T();
+    uint8_t* r = rows_[i];
+    if ((size_t)p >= from) r[p] = t.mul(r[p], q);
+    r[k_ + ut_[i]] = t.mul(r[k_ + ut_[i]], q);
+    return;
+  }
+  hostgf::scale(rows_[i] + from, k_ - from + received_, q);
 }
 
 int DecoderCore::add(const uint8_t* vec) {
   if (is_decoded()) return 3;                       // full/decoder.go:52-54
+  if (received_ >= 2 && append_unit(vec)) return 0;
   ensure_tcap(received_ + 1);
   uint8_t* row = free_.back();                      // :205-208 (append)
   free_.pop_back();
   memcpy(row, vec, k_);
   memset(row + k_, 0, tcap_);
   row[k_ + received_] = 1;                          // T row = e_received
-  rows_.push_back(row);
+  push_row(row, unit_col(vec, k_), (int32_t)received_);
   received_++;                                      // full/decoder.go:57
   if (!(received_ > 1)) {                           // full/decoder.go:58-61
     useful_++;
@@ -74,6 +155,10 @@ int DecoderCore::add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* u
       st = 3;  // full/decoder.go:52-54
       break;
     }
+    if (received_ >= 2 && ndense_ == 0 && append_unit(vecs + i * pitch)) {
+      i++;
+      continue;
+    }
     const size_t np = std::min(std::min<size_t>(4, n - i), k_ - rows_.size());
     if (all_clean_ && received_ >= 1 && np >= 2) {
       const size_t c = add_panel(vecs + i * pitch, pitch, np);
@@ -86,6 +171,36 @@ int DecoderCore::add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* u
   }
   *used = i;
   return st;
+}
+
+// A systematic piece a*e_q on a state that an Rref produced (received >= 2)
+// whose rows are all unit rows, none with pivot q, with q >= R (the new row's
+// index).  kodr's passes then leave every existing row as it is:
+// clean_forward (:15-76) finds the new row zero in every column i < q, so it
+// neither swaps nor eliminates; clean_backward (:78-134) finds column q zero
+// above the new row and every other column as the previous pass left it;
+// remove_zero_rows finds nothing.  What remains is the append and, when q is
+// the diagonal (q == R), the normalization of the new row (:116-132).
+bool DecoderCore::append_unit(const uint8_t* vec) {
+  if (ndense_ != 0) return false;
+  const size_t R = rows_.size();
+  const int32_t q = unit_col(vec, k_);
+  if (q < 0 || (size_t)q < R || ucnt_[q] != 0) return false;
+  ensure_tcap(received_ + 1);
+  uint8_t* row = free_.back();
+  free_.pop_back();
+  memset(row, 0, k_ + tcap_);
+  const uint8_t a = vec[q];
+  const bool diag = (size_t)q == R;
+  row[q] = diag ? 1 : a;
+  row[k_ + received_] = diag ? T().inv(a) : 1;
+  push_row(row, q, (int32_t)received_);
+  received_++;
+  clean_[R] = diag ? 1 : 0;  // a diagonal pivot with a zero column above
+  all_clean_ = all_clean_ && diag;
+  touched_[R] = 0;
+  useful_ = rows_.size();
+  return true;
 }
 
 // np new rows on a state of r diagonal pivots [I_r | X] (all_clean_), as np
@@ -142,16 +257,32 @@ size_t DecoderCore::add_panel(const uint8_t* vecs, size_t pitch, size_t np) {
       if (f) hostgf::axpy(pr[q] + r + p, pr[p] + r + p, width - r - p, f);
     }
   }
-  if (c && r) {
+  if (c && r && ndense_ >= r) {  // every old row dense: one pass over all of them
     qbuf_.resize(r * c);
     for (size_t j = 0; j < r; j++)
       for (size_t p = 0; p < c; p++) qbuf_[j * c + p] = rows_[j][r + p];
     for (size_t p = 0; p < c; p++) vp[p] = pr[p] + r;
     hostgf::rank_multi(ptrs_.data(), qbuf_.data(), r, vp, c, width - r);
+  } else if (c && r && ndense_) {  // unit rows j < r are e_j: zero in the new pivot columns
+    // only rows with a non-zero entry in the c new pivot columns change
+    qbuf_.resize(r * c);
+    size_t nr = 0;
+    for (size_t j = 0; j < r; j++) {
+      bool any = false;
+      for (size_t p = 0; p < c; p++) {
+        qbuf_[nr * c + p] = rows_[j][r + p];
+        any = any || rows_[j][r + p];
+      }
+      if (!any) continue;
+      ptrs_[nr++] = rows_[j] + r;
+      make_dense(j);
+    }
+    for (size_t p = 0; p < c; p++) vp[p] = pr[p] + r;
+    if (nr) hostgf::rank_multi(ptrs_.data(), qbuf_.data(), nr, vp, c, width - r);
   }
   for (size_t p = np; p-- > c;) free_.push_back(pr[p]);
   for (size_t p = 0; p < c; p++) {
-    rows_.push_back(pr[p]);
+    push_row(pr[p], -1, 0);
     clean_[r + p] = 1;
   }
   received_ += c;
@@ -186,10 +317,9 @@ void DecoderCore::rref() {
   mark(last);
   touched_[last] = 1;  // the new row
   for (size_t i = 0; i < boundary; i++) {
-    if (rows_[i][i] == 0) {
+    if (up_[i] >= 0 ? up_[i] != (int32_t)i : rows_[i][i] == 0) {
       if (i < last && rows_[last][i] != 0) {
-        std::swap(rows_[i], rows_[last]);           // :37-48
-        std::swap(touched_[i], touched_[last]);
+        swap_rows(i, last);                         // :37-48
         mark(i);
       } else {
         continue;                                   // :33-35
@@ -197,7 +327,19 @@ void DecoderCore::rref() {
     }
     if (i < last) {
       const uint8_t c = rows_[last][i];
-      if (c != 0) axpy_row(last, i, t.div(c, rows_[i][i]), i);  // :51-74
+      if (c == 0) continue;
+      if (up_[i] == (int32_t)i) {
+        // unit pivot a*e_i | b*e_t: the new row's column i cancels and its T
+        // column t takes (c / a) * b -- axpy_row's two bytes, inline
+        uint8_t* v = rows_[last];
+        const uint8_t* s = rows_[i];
+        v[i] = 0;
+        v[k_ + ut_[i]] ^= t.mul(t.div(c, s[i]), s[k_ + ut_[i]]);
+        make_dense(last);
+        touched_[last] = 1;
+      } else {
+        axpy_row(last, i, t.div(c, rows_[i][i]), i);  // :51-74
+      }
     }
   }
 
@@ -205,27 +347,61 @@ void DecoderCore::rref() {
   // previous pass unchanged with a non-zero diagonal was zeroed above the
   // diagonal then, so only the rows changed by this forward pass can be
   // non-zero there; every other column is scanned in full, as kodr does.
+  //
+  // Within column i only rows that can be non-zero there are visited: dense
+  // rows, and unit rows whose pivot is i (a unit row is zero everywhere else).
+  // Each elimination changes only its target row, so the order of the rows
+  // within a column does not matter.
   std::sort(dirty_list, dirty_list + ndirty);
   std::sort(dirty_big.begin(), dirty_big.end());
+  dense_pos_.clear();
+  for (size_t j = 0; j < rows_.size(); j++)
+    if (up_[j] < 0) dense_pos_.push_back(j);
+  // that set is also exact for a clean column; take it there too when it is
+  // smaller than the rows this forward pass changed (a systematic state after
+  // a coded piece filled a gap: every unit row after the gap moved)
+  const bool sparse = dense_pos_.size() < ndirty + dirty_big.size();
   for (size_t ii = boundary; ii-- > 0;) {
     const size_t i = ii;
+    if (up_[i] >= 0 && up_[i] != (int32_t)i) continue;  // a unit row off its diagonal
     const uint8_t d = rows_[i][i];
     if (d == 0) continue;                           // :86-88
+    const int32_t ci = (int32_t)i;
     const bool full = dirty_[i] || !clean_[i];
-    if (full) {
-      for (size_t j = 0; j < i; j++) {              // :90-114
-        const uint8_t c = rows_[j][i];
-        if (c != 0) axpy_row(j, i, t.div(c, d), i);
+    if (full || sparse) {                           // :90-114
+      const bool unit_i = up_[i] == ci;
+      const uint8_t tq = unit_i ? rows_[i][k_ + ut_[i]] : 0;
+      for (size_t n = 0; n < dense_pos_.size(); n++) {
+        const size_t j = dense_pos_[n];
+        if (j >= i) continue;
+        uint8_t* rj = rows_[j];
+        const uint8_t c = rj[i];
+        if (c == 0) continue;
+        if (unit_i) {  // axpy_row from a unit pivot, inline (row j is dense already)
+          rj[i] = 0;
+          rj[k_ + ut_[i]] ^= t.mul(t.div(c, d), tq);
+          touched_[j] = 1;
+        } else {
+          axpy_row(j, i, t.div(c, d), i);
+        }
+      }
+      // rows below i are zero in column i, so every unit row with pivot i
+      // other than row i itself lies above it
+      if (ucnt_[i] > (up_[i] == ci ? 1u : 0u)) {
+        for (size_t j = 0; j < i; j++)
+          if (up_[j] == ci) axpy_row(j, i, t.div(rows_[j][i], d), i);
       }
     } else {
       for (size_t n = 0; n < ndirty; n++) {
         const size_t j = dirty_list[n];
         if (j >= i) break;
+        if (up_[j] >= 0 && up_[j] != ci) continue;
         const uint8_t c = rows_[j][i];
         if (c != 0) axpy_row(j, i, t.div(c, d), i);
       }
       for (size_t j : dirty_big) {
         if (j >= i) break;
+        if (up_[j] >= 0 && up_[j] != ci) continue;
         const uint8_t c = rows_[j][i];
         if (c != 0) axpy_row(j, i, t.div(c, d), i);
       }
@@ -233,7 +409,7 @@ void DecoderCore::rref() {
     if (d == 1) continue;                           // :116-118
     // :120-132: coeffs[i][i] = 1, coeffs[i][j>i] *= inv, coded[i] *= inv.
     // Columns < i of row i are zero here, so scaling from column i is exact.
-    hostgf::scale(rows_[i] + i, k_ - i + received_, t.inv(d));
+    scale_row(i, i, t.inv(d));
   }
   for (size_t n = 0; n < ndirty; n++) dirty_[dirty_list[n]] = 0;
   for (size_t j : dirty_big) dirty_[j] = 0;
@@ -247,12 +423,18 @@ void DecoderCore::rref() {
     const bool t = touched_[i];
     touched_[i] = 0;
     if (t && hostgf::all_zero(rows_[i], k_)) {
+      forget_row(i);
       free_.push_back(rows_[i]);
     } else {
-      rows_[out++] = rows_[i];
+      rows_[out] = rows_[i];
+      up_[out] = up_[i];
+      ut_[out] = ut_[i];
+      out++;
     }
   }
   rows_.resize(out);
+  up_.resize(out);
+  ut_.resize(out);
   // a row with a non-zero diagonal after this pass has a clean column above
   update_clean();
 }
@@ -260,7 +442,7 @@ void DecoderCore::rref() {
 void DecoderCore::update_clean() {
   all_clean_ = true;
   for (size_t i = 0; i < rows_.size(); i++) {
-    clean_[i] = (i < k_ && rows_[i][i] != 0) ? 1 : 0;
+    clean_[i] = (i < k_ && (up_[i] >= 0 ? up_[i] == (int32_t)i : rows_[i][i] != 0)) ? 1 : 0;
     all_clean_ = all_clean_ && clean_[i];
   }
 }
@@ -280,24 +462,44 @@ void DecoderCore::rref_clean() {
   const hostgf::Tables& t = T();
   const size_t r = rows_.size() - 1, width = k_ + received_;
   uint8_t* v = rows_[r];
-  qbuf_.assign(v, v + r);
   // columns < r of the result are exactly zero (pivot i cancels v[i], every
-  // other pivot row is 0 there); accumulate only columns [r, k + received)
-  ptrs_.resize(r);
-  for (size_t i = 0; i < r; i++) ptrs_[i] = rows_[i] + r;
-  hostgf::accumulate(v + r, ptrs_.data(), qbuf_.data(), r, width - r);
-  memset(v, 0, r);
+  // other pivot row is 0 there); accumulate only columns [r, k + received).
+  // A new row already zero there (a systematic piece e_q, q >= r) is unchanged.
+  if (!hostgf::all_zero(v, r)) {
+    qbuf_.assign(v, v + r);
+    ptrs_.resize(r);
+    for (size_t i = 0; i < r; i++) ptrs_[i] = rows_[i] + r;
+    hostgf::accumulate(v + r, ptrs_.data(), qbuf_.data(), r, width - r);
+    memset(v, 0, r);
+    make_dense(r);
+  }
   const uint8_t d = v[r];
   if (d != 0) {
-    // row_j[r..] ^= (c_j / d) * v[r..]  for every j < r, as one pass
+    // row_j[r..] ^= (c_j / d) * v[r..]  for every j < r with c_j != 0, as
+    // one pass; unit rows j < r are e_j, zero in column r
     const uint8_t dinv = t.inv(d);
-    ptrs_.resize(r);
-    for (size_t j = 0; j < r; j++) {
-      qbuf_[j] = t.mul(rows_[j][r], dinv);  // == Div(c_j, d) (gf256.go:121-127)
-      ptrs_[j] = rows_[j] + r;
+    size_t nr = 0;
+    if (ndense_ > r) {  // every row dense (the new one included): one pass
+      qbuf_.resize(r);
+      ptrs_.resize(r);
+      for (size_t j = 0; j < r; j++) {
+        qbuf_[j] = t.mul(rows_[j][r], dinv);  // == Div(c_j, d) (gf256.go:121-127)
+        ptrs_[j] = rows_[j] + r;
+      }
+      nr = r;
+    } else if (ndense_) {
+      qbuf_.resize(r);
+      ptrs_.resize(r);
+      for (size_t j = 0; j < r; j++) {
+        const uint8_t c = rows_[j][r];
+        if (!c) continue;
+        qbuf_[nr] = t.mul(c, dinv);  // == Div(c_j, d) (gf256.go:121-127)
+        ptrs_[nr++] = rows_[j] + r;
+        make_dense(j);
+      }
     }
-    hostgf::rank1(ptrs_.data(), qbuf_.data(), r, v + r, width - r);
-    if (d != 1) hostgf::scale(v + r, width - r, t.inv(d));
+    if (nr) hostgf::rank1(ptrs_.data(), qbuf_.data(), nr, v + r, width - r);
+    if (d != 1) scale_row(r, r, t.inv(d));
     clean_[r] = 1;  // all_clean_ stays true
     return;
   }
@@ -305,7 +507,7 @@ void DecoderCore::rref_clean() {
   // or kept as an off-diagonal row (kodr's rank over-count quirk)
   if (hostgf::all_zero(v, k_)) {
     free_.push_back(v);
-    rows_.pop_back();
+    pop_row();
     return;
   }
   clean_[r] = 0;

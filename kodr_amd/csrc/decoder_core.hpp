@@ -55,9 +55,17 @@ class DecoderCore {
   void rref();
   void rref_clean();
   size_t add_panel(const uint8_t* vecs, size_t pitch, size_t np);
+  bool append_unit(const uint8_t* vec);
   void update_clean();
   void ensure_tcap(size_t need);
   void axpy_row(size_t dst, size_t src, uint8_t q, size_t from);
+  void scale_row(size_t i, size_t from, uint8_t q);
+  // row bookkeeping; up_/ut_ move with rows_
+  void push_row(uint8_t* row, int32_t p, int32_t t);
+  void pop_row();
+  void swap_rows(size_t a, size_t b);
+  void make_dense(size_t pos);
+  void forget_row(size_t pos);
 
   size_t k_;
   size_t useful_ = 0, received_ = 0;
@@ -71,6 +79,17 @@ class DecoderCore {
   bool all_clean_ = false;             // every row is a diagonal pivot with a clean column
   std::vector<uint8_t> qbuf_;          // quotients of the blocked passes
   std::vector<uint8_t*> ptrs_;
+  // Sparse rows.  A row is "unit" when its coefficient half is a*e_p and its
+  // T half is b*e_t (a systematic piece that no row operation has touched
+  // yet); up_[i] = p and ut_[i] = t for such a row, up_[i] = -1 otherwise
+  // ("dense": any content).  Only the bookkeeping is sparse -- the bytes of
+  // every row stay complete -- and it is used only to skip work that is
+  // provably zero: a row operation with a unit source touches two bytes, and
+  // a unit row is non-zero in exactly one coefficient column.
+  std::vector<int32_t> up_, ut_;       // parallel to rows_
+  std::vector<uint32_t> ucnt_;         // per coefficient column: unit rows with that pivot
+  size_t ndense_ = 0;                  // dense rows in rows_
+  std::vector<size_t> dense_pos_;      // positions of dense rows (rebuilt per literal pass)
 };
 
 }  // namespace kodr_amd

@@ -90,6 +90,29 @@ __global__ __launch_bounds__(256) void bitslice_kernel(const uint8_t* src, uint8
   p[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// dst row r = src row r (bytes [0, nblk * 32)), and dst_bs row r = its
+// bit-sliced form: one read of the source for both, for the decoder's
+// received rows (plain rows for the GetPiece paths, the twin for T x R).
+// src, spitch, dpitch: multiples of 16 (checked by the host).
+__global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __restrict__ src, size_t spitch,
+                                                           uint8_t* __restrict__ dst, uint8_t* __restrict__ dst_bs,
+                                                           size_t dpitch, int rows, int nblk) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(i / (size_t)nblk), b = (int)(i % (size_t)nblk);
+  if (r >= rows) return;
+  const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)r * spitch + (size_t)b * kBsBlock);
+  const size_t off = (size_t)r * dpitch + (size_t)b * kBsBlock;
+  const uint4 a = q[0], c = q[1];
+  uint4* p = reinterpret_cast<uint4*>(dst + off);
+  p[0] = a;
+  p[1] = c;
+  uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  bitslice32(d);
+  uint4* t = reinterpret_cast<uint4*>(dst_bs + off);
+  t[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  t[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+
 // The bodies' only home: this kernel exports the absolute address of body
 // (0, 0) and every body's offset from it (out[i] for body i = copy * 256 + c,
 // out[1024] lo, out[1025] hi) and never runs them; gf_bs_kernel jumps here.
@@ -410,6 +433,20 @@ hipError_t bs_body_offsets(int device, uint32_t* host_out) {
 bool bs_ready(int device) {
   const BsDevice* bd = nullptr;
   return bs_init(device, &bd) == hipSuccess && bd->ok;
+}
+
+hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, uint8_t* dst_bs, size_t dpitch,
+                              size_t rows, size_t ncols, hipStream_t stream) {
+  if (!rows || !ncols) return hipSuccess;
+  if (ncols % kBsBlock || dpitch % kBsBlock || dpitch < ncols || (uintptr_t)src % 16 || spitch % 16 ||
+      (uintptr_t)dst % 16 || (uintptr_t)dst_bs % 16)
+    return hipErrorInvalidValue;
+  const size_t nblk = ncols / kBsBlock;
+  const size_t total = rows * nblk;
+  if (rows > 0x7fffffff || nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(copy_bitslice_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src,
+                     spitch, dst, dst_bs, dpitch, (int)rows, (int)nblk);
+  return hipGetLastError();
 }
 
 hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,

@@ -376,7 +376,7 @@ hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped
                           hipStream_t stream) {
   if (!width || !rows) return hipSuccess;
   const size_t total = width * rows;
-  if (total > kUploadSmallMax) return hipErrorInvalidValue;
+  if (total > kDownloadSmallMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(download_small_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src,
                      spitch, dst_mapped, (int)width, (int)total);
   return hipGetLastError();

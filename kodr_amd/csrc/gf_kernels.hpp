@@ -42,6 +42,9 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
 // memory (a device pointer of a hipHostMalloc buffer), copied by a kernel
 // rather than a DMA engine.  width x rows <= kUploadSmallMax.
 constexpr size_t kUploadSmallMax = 64 * 1024;
+// download_small: up to this many bytes (the coding vectors of a batched
+// AddPiece: 258 x 256 B at 32 MiB/256)
+constexpr size_t kDownloadSmallMax = 256 * 1024;
 hipError_t upload_small(const uint8_t* src_mapped, uint8_t* dst, size_t dpitch, size_t width, size_t rows,
                         hipStream_t stream);
 // the reverse: width x rows bytes of device memory (pitch spitch) into
@@ -72,6 +75,13 @@ hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t
 // written.
 hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,
                          hipStream_t stream);
+
+// dst rows = the first ncols bytes of src rows, and dst_bs rows = the same
+// rows bit-sliced (as bitslice_rows), from one read of src.  ncols and dpitch
+// multiples of 32; src, spitch, dst, dst_bs 16-byte aligned (else
+// hipErrorInvalidValue: the caller copies and bit-slices in two passes).
+hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, uint8_t* dst_bs, size_t dpitch,
+                              size_t rows, size_t ncols, hipStream_t stream);
 
 // byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);

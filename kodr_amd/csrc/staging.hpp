@@ -69,6 +69,31 @@ class Staging {
     return hipSuccess;
   }
 
+  // Split small download: begin enqueues the copy into a pinned chunk and
+  // records its event (work enqueued after it does not delay end); end waits
+  // for that event and unpacks into dst.  width * height <= kDownloadSmallMax.
+  hipError_t d2h_small_begin(const uint8_t* src, size_t spitch, size_t width, size_t height, hipStream_t s,
+                             int* ticket) {
+    hipError_t e = ensure();
+    if (e != hipSuccess) return e;
+    const int b = next_;
+    next_ ^= 1;
+    if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+    pending_[b] = false;
+    if ((e = download_small(src, spitch, dev_[b], width, height, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
+    pending_[b] = true;  // any other use of chunk b waits for the download
+    *ticket = b;
+    return hipSuccess;
+  }
+  hipError_t d2h_small_end(int b, uint8_t* dst, size_t dpitch, size_t width, size_t height) {
+    hipError_t e = hipEventSynchronize(ev_[b]);
+    if (e != hipSuccess) return e;
+    pending_[b] = false;
+    pack(dst, dpitch, buf_[b], width, width, height);
+    return hipSuccess;
+  }
+
   hipError_t d2h(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                  size_t height, hipStream_t s) {
     if (!width || !height) return hipSuccess;
@@ -78,16 +103,10 @@ class Staging {
     }
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
-    if (width * height <= kUploadSmallMax) {  // coding vectors of a batch: a kernel writes the pinned chunk
-      const int b = next_;
-      next_ ^= 1;
-      if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
-      if ((e = download_small(src, spitch, dev_[b], width, height, s)) != hipSuccess) return e;
-      if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
-      if ((e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
-      pending_[b] = false;
-      pack(dst, dpitch, buf_[b], width, width, height);
-      return hipSuccess;
+    if (width * height <= kDownloadSmallMax) {  // coding vectors of a batch: a kernel writes the pinned chunk
+      int b;
+      if ((e = d2h_small_begin(src, spitch, width, height, s, &b)) != hipSuccess) return e;
+      return d2h_small_end(b, dst, dpitch, width, height);
     }
     if (width > kChunk) {
       for (size_t r = 0; r < height; r++) {

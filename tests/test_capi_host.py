@@ -267,6 +267,37 @@ def test_core_fuzz_mixed_streams(seed):
     check_stream(k, stream)
 
 
+@pytest.mark.parametrize("seed", range(30))
+def test_core_systematic_order_streams(seed):
+    # systematic pieces in encoder order with losses (and sometimes scaled,
+    # duplicated, or interrupted by coded or zero rows), then coded pieces:
+    # the unit-row bookkeeping (append without a pass, two-byte row
+    # operations from unit pivots, sparse column scans) against the oracle
+    # after every AddPiece
+    rng = np.random.default_rng(8800 + seed)
+    k = int(rng.choice([3, 8, 17, 40, 64]))
+    lost = set(rng.choice(k, int(rng.integers(0, k // 3 + 2)), replace=False).tolist())
+    rows = []
+    for i in range(k):
+        if i in lost:
+            continue
+        v = np.zeros(k, np.uint8)
+        v[i] = 1 if rng.random() < 0.8 else rng.integers(2, 256)
+        rows.append(v)
+        r = rng.random()
+        if r < 0.05:
+            rows.append(v.copy())                       # duplicate systematic piece
+        elif r < 0.08:
+            rows.append(rng.integers(0, 256, k, dtype=np.uint8))  # coded piece in between
+        elif r < 0.10:
+            rows.append(np.zeros(k, np.uint8))
+    rows += [rng.integers(0, 256 if seed % 3 else 3, k, dtype=np.uint8) for _ in range(len(lost) + 4)]
+    stream = [(v, rng.integers(0, 256, 6, dtype=np.uint8)) for v in rows]
+    check_stream(k, stream)
+    R = np.ascontiguousarray(np.stack(rows))
+    _batch_vs_rows(k, R, sorted(set(rng.integers(1, len(rows) + 1, 2).tolist()) | {len(rows)}))
+
+
 def _batch_vs_rows(k, R, cuts):
     """rlnc_decoder_add_pieces over R (one row per received piece) split at
     `cuts` == the same rows through rlnc_decoder_add_piece one by one (which
