@@ -264,6 +264,86 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()
     return t
 
 
+# Dynamic rows (gf_bs.hip MODE 20): the KW waves of a workgroup share one
+# program (K rows x 8 targets in LDS) and take input rows one at a time from
+# an LDS counter, so a wave the SIMD's arbiter serves less takes fewer rows
+# and the waves of a workgroup finish together (with a static K split they
+# finished 18-35 k cycles apart, profiles/r01/bs_timeline.log).  Per row the
+# wave knows its row I (SC) and its next row I' (SN); during row I it loads
+# row I' (ring) and its targets (PG/PGN, alternating), and fetches the row
+# after I' with one ds_add_rtn_u32 from a single lane.
+D_EX = 46          # s[46:47] exec save
+D_SC, D_SN, D_SK, D_SKM1, D_TMP = 48, 49, 50, 51, 52
+D_VAT = 107        # the fetched row index (lane 0)
+D_PG, D_PGN = RING + 8 * P, RING + 8 * P + 1   # targets of the current / next row (lanes 0..7)
+D_VADDR, D_VCNT, D_VONE = D_PG + 2, D_PG + 3, D_PG + 4
+D_VMAX = D_VONE + 1
+D_ROWS = 4         # rows per loop iteration (priority rotation j % 4, PG/PGN alternate)
+
+
+def row_lines_dyn(j, dispatch=True, prio=ROW_PRIO):
+    assert P == 1
+    pgc, pgn = (D_PG, D_PGN) if j % 2 == 0 else (D_PGN, D_PG)
+    h = lambda i: T0 + 2 * i  # noqa: E731
+    t = [f"s_cmp_ge_u32 s{D_SC}, s{D_SK}", "s_cbranch_scc1 .Ldone_%="]
+    t += [f"s_setprio {prio(j)}"] if prio else []
+    t += ["s_waitcnt vmcnt(0)"]
+    t += [f"v_readlane_b32 s{h(m)}, v{pgc}, {m}" for m in range(4)]
+    t += table_lines(0)
+    b = RING
+    t += [f"s_mul_i32 s44, s{D_SN}, s45",
+          f"buffer_load_dwordx4 v[{b}:{b + 3}], %[col], s[40:43], s44 offen",
+          f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16"]
+    t += [f"v_readlane_b32 s{H2 + 2 * m}, v{pgc}, {4 + m}" for m in range(4)]
+    t += [f"s_min_u32 s{D_TMP}, s{D_SN}, s{D_SKM1}", f"s_lshl_b32 s{D_TMP}, s{D_TMP}, 5",
+          f"v_add_u32_e32 v{D_VADDR}, s{D_TMP}, v{PL}", f"ds_read_b32 v{pgn}, v{D_VADDR}",
+          f"s_mov_b64 s[{D_EX}:{D_EX + 1}], exec", "s_mov_b64 exec, 1",
+          f"ds_add_rtn_u32 v{D_VAT}, v{D_VCNT}, v{D_VONE}", f"s_mov_b64 exec, s[{D_EX}:{D_EX + 1}]"]
+    if dispatch:
+        t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{STUB}:{STUB + 1}]",
+              f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]",
+              "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
+              f"s_setpc_b64 s[{h(0)}:{h(0) + 1}]",
+              f".Lret{j}_%=:",
+              "s_set_gpr_idx_off"]
+    t += ["s_waitcnt lgkmcnt(0)", f"s_mov_b32 s{D_SC}, s{D_SN}", f"v_readfirstlane_b32 s{D_SN}, v{D_VAT}"]
+    return t
+
+
+def main_loop_dyn(dispatch=True, prio=ROW_PRIO):
+    """Prologue (descriptor, stub/return addresses, hi words, row registers,
+    the first row's targets, zeroed accumulators), the stub, and the 4-row
+    loop; exits when the wave's next row is past K.  Operands: %[sc] the
+    wave's first row, %[sn] its second, %[nk] K, %[km1] K - 1, %[r0x32] the
+    first row * 32, %[pl] this lane's program address (program + (lane & 7) * 4),
+    %[cnt] the counter's LDS address."""
+    pro = ["s_mov_b32 s40, %[xlo]", "s_and_b32 s41, %[xhi], 0xffff", "s_mov_b32 s42, %[nrec]",
+           "s_mov_b32 s43, 0x00020000", "s_mov_b32 s45, %[ldx]",
+           f"s_getpc_b64 s[{GPC}:{GPC + 1}]", ".Lpc_%=:"]
+    if dispatch:
+        for reg, lab in [(STUB, "stub")] + [(RET + 2 * j, f"ret{j}") for j in range(D_ROWS)]:
+            pro += [f"s_add_u32 s{reg}, s{GPC}, .L{lab}_%= - .Lpc_%=",
+                    f"s_addc_u32 s{reg + 1}, s{GPC + 1}, 0"]
+    pro += [f"s_mov_b32 s{T0 + 2 * i + 1}, %[thi]" for i in range(4)]
+    pro += [f"s_mov_b32 s{H2 + 2 * i + 1}, %[thi]" for i in range(4)]
+    pro += [f"s_mov_b32 s{D_SC}, %[sc]", f"s_mov_b32 s{D_SN}, %[sn]", f"s_mov_b32 s{D_SK}, %[nk]",
+            f"s_mov_b32 s{D_SKM1}, %[km1]",
+            f"v_mov_b32 v{PL}, %[pl]", f"v_mov_b32 v{D_VCNT}, %[cnt]", f"v_mov_b32 v{D_VONE}, 1",
+            f"v_add_u32_e32 v{D_VADDR}, %[r0x32], v{PL}", f"ds_read_b32 v{D_PG}, v{D_VADDR}"]
+    pro += [f"v_mov_b32 v{ACC + r}, 0" for r in range(64)]
+    pro += ["s_waitcnt lgkmcnt(0)"]
+    t = pro
+    if dispatch:
+        t += ["s_branch .Lloop_%="] + stub_lines()
+    t += [".Lloop_%=:"]
+    for j in range(D_ROWS):
+        t += row_lines_dyn(j, dispatch, prio)
+    t += ["s_branch .Lloop_%=", ".Ldone_%=:"]
+    if prio:
+        t += ["s_setprio 0"]
+    return t
+
+
 def dump_lines():
     """Bring-up only (MODE 9): the prologue and the first row's target reads,
     then s[60:99] and M0 stored to %[ydbg] (lane 0's values), no jump taken."""
@@ -349,6 +429,9 @@ def main():
     # program through scalar loads instead of LDS + v_readlane (MODE 14)
     out += emit("KODR_BS_MAIN_SLOAD", main_loop(True, True, ROW_PRIO, None, (), True))
     out += emit("KODR_BS_DUMP", dump_lines())
+    # dynamic rows (MODE 20)
+    out += emit("KODR_BS_MAIN_DYN", main_loop_dyn(True))
+    out.append(f"#define KODR_BS_DYN_VMAX {D_VMAX}")
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)
     # the ring v[RING..RING+8P) is bound to in/out operands, not clobbered
@@ -356,6 +439,10 @@ def main():
     assert CNT <= 101 and GPC + 1 < T0
     clob += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
     out.append("#define KODR_BS_CLOBBERS " + ", ".join(clob) + ', "scc", "memory"')
+    dclob = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, D_VMAX))]
+    dclob += [f'"s{r}"' for r in list(range(40, 46)) + list(range(D_EX, D_TMP + 1)) + [GPC, GPC + 1] +
+              list(range(T0, RET + 2 * D_ROWS))]
+    out.append("#define KODR_BS_CLOBBERS_DYN " + ", ".join(dclob) + ', "scc", "memory"')
     out.append("#define KODR_BS_CLOBBERS_SLOAD " + ", ".join(clob + [f'"s{r}"' for r in range(SP, SL + 8)]) +
                ', "scc", "memory"')
     out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "

@@ -162,6 +162,107 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   uint32_t* tgt_l = lds + 64 * 64;
   uint32_t* prog_l = tgt_l + 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if constexpr (MODE == 20) {
+    // Dynamic rows: one program for the workgroup (K rows x 8 targets) and
+    // a row counter after it; wave w starts on rows w and w + KW and then
+    // takes rows one at a time (gen_bs_bodies.py main_loop_dyn).
+    const int b = blockIdx.x;
+    const int rg = (b >> 3) % nrg;
+    const int cx = (b / (8 * nrg)) * 8 + (b & 7);
+    if (cx >= ncx) return;
+    const int m0 = rg * kBsRows;
+    const int kpad = (K + kBsChunk - 1) / kBsChunk * kBsChunk;
+    uint32_t* cnt = prog_l + kpad * kBsRows;
+    constexpr int kTgt = 256;
+    uint32_t ot[(kTgt + 63) / 64];
+#pragma unroll
+    for (int j = 0; j < (kTgt + 63) / 64; j++) {
+      const int i = tid + j * 64 * KW;
+      ot[j] = i < kTgt ? tgt[i] : 0u;
+    }
+    const int ne = kpad * kBsRows;
+    auto coef = [&](int e) -> uint32_t {
+      const int k = e >> 3, row = m0 + (e & 7);
+      return (e < ne && k < K && row < M) ? (uint32_t)A[(size_t)row * lda + k] : 0u;
+    };
+    uint32_t c[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) c[j] = coef(tid + j * 64 * KW);
+    const uint32_t col = (uint32_t)(cx * 64 + lane) * kBsBlock;
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane((uint32_t)K * (uint32_t)ldx);
+    const uint32_t sldx = __builtin_amdgcn_readfirstlane((uint32_t)ldx);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)nrec, 0x00020000);
+    u32x4 ring[2 * KODR_BS_P];
+    ring[0] = __builtin_amdgcn_raw_buffer_load_b128(xr, col, (uint32_t)w * sldx, 0);
+    ring[1] = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, (uint32_t)w * sldx, 0);
+#pragma unroll
+    for (int j = 0; j < (kTgt + 63) / 64; j++) {
+      const int i = tid + j * 64 * KW;
+      if (i < kTgt) tgt_l[i] = ot[j];
+    }
+    for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
+    if (tid == 0) *cnt = 2u * KW;
+    __syncthreads();
+    for (int e0 = 0; e0 < ne; e0 += 4 * 64 * KW) {
+      if (e0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) c[j] = coef(e0 + tid + j * 64 * KW);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int e = e0 + tid + j * 64 * KW;
+        if (e < ne) prog_l[e] = tgt_l[c[j]] + (uint32_t)(e & 3) * KODR_BS_COPY_BYTES;
+      }
+    }
+    __syncthreads();
+    const uint64_t xa = reinterpret_cast<uint64_t>(X);
+    const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
+    const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
+    const uint32_t sthi = __builtin_amdgcn_readfirstlane(thi);
+    const uint32_t sc = __builtin_amdgcn_readfirstlane((uint32_t)w);
+    const uint32_t sn = __builtin_amdgcn_readfirstlane((uint32_t)(w + KW));
+    const uint32_t nk = __builtin_amdgcn_readfirstlane((uint32_t)K);
+    const uint32_t km1 = __builtin_amdgcn_readfirstlane((uint32_t)max(K - 1, 0));
+    const uint32_t r0x32 = __builtin_amdgcn_readfirstlane((uint32_t)w * 32u);
+    const uint32_t pl = (uint32_t)reinterpret_cast<uintptr_t>(prog_l) + (uint32_t)(lane & 7) * 4u;
+    const uint32_t cnta = (uint32_t)reinterpret_cast<uintptr_t>(cnt);
+    if (K > 0) {
+      asm volatile(KODR_BS_MAIN_DYN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS
+                   : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [ldx] "s"(sldx), [thi] "s"(sthi),
+                     [col] "v"(col), [lds] "v"((uint32_t)reinterpret_cast<uintptr_t>(red) + (uint32_t)lane * 4u),
+                     [sc] "s"(sc), [sn] "s"(sn), [nk] "s"(nk), [km1] "s"(km1), [r0x32] "s"(r0x32), [pl] "v"(pl),
+                     [cnt] "v"(cnta)
+                   : KODR_BS_CLOBBERS_DYN);
+    }
+    __syncthreads();
+    for (int it = tid; it < kBsRows * 64; it += 64 * KW) {
+      const int m = it >> 6, l = it & 63;
+      const int row = m0 + m;
+      const int cc = (cx * 64 + l) * kBsBlock;
+      if (row >= M || cc >= ncols) continue;
+      uint32_t d[8];
+#pragma unroll
+      for (int p = 0; p < 8; p++) d[p] = red[(m * 8 + p) * 64 + l];
+      bitslice32(d);
+      uint8_t* dst = Y + (size_t)row * ldy + cc;
+      if (cc + kBsBlock <= ncols) {
+        uint4 v0 = make_uint4(d[0], d[1], d[2], d[3]), v1 = make_uint4(d[4], d[5], d[6], d[7]);
+        if (accum) {
+          const uint4 o0 = reinterpret_cast<const uint4*>(dst)[0], o1 = reinterpret_cast<const uint4*>(dst)[1];
+          v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
+          v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
+        }
+        reinterpret_cast<uint4*>(dst)[0] = v0;
+        reinterpret_cast<uint4*>(dst)[1] = v1;
+      } else {
+        for (int i = 0; cc + i < ncols; i++)
+          dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
+      }
+    }
+    return;
+  }
   // XCD-aware order: the nrg row groups of one column chunk go to blocks
   // b, b+8, ... (one XCD) and re-read that chunk from its L2.  Speed only.
   const int b = blockIdx.x;
@@ -471,7 +572,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;
 
 // row sums, the body target table, and KW programs of rpw rows x 8 targets
 size_t bs_lds_bytes(int kw, int rpw) {
-  return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4;
+  return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4 + 16;  // + the dynamic rows' counter
 }
 
 }  // namespace
@@ -556,7 +657,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 8 ? KODR_BS_CALL(KW_, 8) : mode == 9 ? KODR_BS_CALL(KW_, 9)                    \
          : mode == 10 ? KODR_BS_CALL(KW_, 10) : mode == 11 ? KODR_BS_CALL(KW_, 11)                \
          : mode == 12 ? KODR_BS_CALL(KW_, 12) : mode == 13 ? KODR_BS_CALL(KW_, 13)                \
-         : mode == 14 ? KODR_BS_CALL(KW_, 14) : KODR_BS_CALL(KW_, 0);
+         : mode == 14 ? KODR_BS_CALL(KW_, 14) : mode == 20 ? KODR_BS_CALL(KW_, 20)           \
+                                               : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
   case KW_:               \

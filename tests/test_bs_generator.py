@@ -179,75 +179,80 @@ class _Wave:
             op, _, rest = ln.partition(" ")
             a = [t.strip() for t in rest.split(",")]
             r = [int(x) for x in re.findall(r"v\[?(\d+)", ln)]
-            if op == "s_getpc_b64":
-                self.s[gen.GPC], self.s[gen.GPC + 1] = 0x1000_0000, 0
-            elif op == "s_add_u32" and "- .Lpc" in ln:
-                lab = a[2].split(" - ")[0]
-                self.s[int(a[0][1:])] = 0x1000_0000 + 4 * self.labels[lab]
-            elif op == "s_addc_u32":
-                self.s[int(a[0][1:])] = 0
-            elif op == "s_mov_b32":
-                self.s[int(a[0][1:])] = self.val(a[1])
-            elif op == "s_and_b32":
-                self.s[int(a[0][1:])] = self.val(a[1]) & self.val(a[2])
-            elif op == "s_add_u32" and a[0] == "m0":
-                assert self.idx_on
-                self.m0 += self.val(a[2])
-            elif op == "s_add_u32":
-                self.s[int(a[0][1:])] = self.val(a[1]) + self.val(a[2])
-            elif op == "s_sub_u32":
-                self.s[int(a[0][1:])] = self.val(a[1]) - self.val(a[2])
-            elif op == "s_cmp_lg_u32":
-                self.scc = self.val(a[0]) != self.val(a[1])
-            elif op == "s_cbranch_scc1":
-                if self.scc:
-                    pc = self.labels[a[0]]
-            elif op == "s_branch":
-                pc = self.labels[a[0]]
-            elif op == "s_mov_b64":
-                d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
-                self.s[d], self.s[d + 1] = self.s[sr], self.s[sr + 1]
-            elif op == "s_load_dwordx8":
-                d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
-                addr = (self.s[sr + 1] << 32) | self.s[sr]
-                for i in range(8):
-                    self.s[d + i] = self.gmem.get(addr + 4 * i, 0xDEAD)
-            elif op == "s_setpc_b64":
-                lo = int(re.findall(r"s\[(\d+):", ln)[0])
-                pc = self.addr[(self.s[lo + 1] << 32) | self.s[lo]]
-            elif op == "s_set_gpr_idx_on":
-                assert a[0] == "0"
-                self.idx_on, self.m0 = True, 0
-            elif op == "s_set_gpr_idx_off":
-                self.idx_on = False
-            elif op == "s_waitcnt":
-                continue
-            elif op == "v_mov_b32" and r[0] == gen.PL:
-                self.v[gen.PL] = list(self.pl_lanes)
-            elif op == "v_mov_b32" and r[0] in self.VEC:
-                self.v[r[0]] = list(self.v[r[1]])
-            elif op == "v_mov_b32":
-                self.v[r[0]] = self.val(a[1])
-            elif op == "v_readlane_b32":
-                assert not self.idx_on
-                self.s[int(a[0][1:])] = self.v[r[0]][int(a[2])]
-            elif op == "v_add_u32_e32":
-                assert r[0] == r[1] == gen.PL
-                self.v[gen.PL] = [x + int(a[1]) for x in self.v[gen.PL]]
-            elif op == "ds_read_b32":
-                off = int(ln.split("offset:")[1]) if "offset:" in ln else 0
-                self.v[r[0]] = [self.lds.get(x + off, 0xDEAD) for x in self.v[r[1]]]
-            elif op == "buffer_load_dwordx4":
-                half = 1 if "offset:16" in ln else 0
-                self._load_row(r[0] - 4 * half, self.s[44], half)
-            elif op == "s_setprio":  # scheduling only
-                assert 0 <= int(a[0]) <= 3
-            elif op in ("v_pk_mov_b32", "v_xor_b32_e32", "v_xor_b32_e64", "v_bitop3_b32"):
-                idx = self.m0 if self.idx_on else 0
-                run([ln], self.v, idx)
-            else:
-                raise AssertionError(ln)
+            pc = self.step(ln, op, a, r, pc)
         return np.array([[self.v[gen.ACC + 8 * m + j] for j in range(8)] for m in range(8)], np.uint32)
+
+    def step(self, ln, op, a, r, pc):
+        """One instruction; returns the next pc."""
+        if op == "s_getpc_b64":
+            self.s[gen.GPC], self.s[gen.GPC + 1] = 0x1000_0000, 0
+        elif op == "s_add_u32" and "- .Lpc" in ln:
+            lab = a[2].split(" - ")[0]
+            self.s[int(a[0][1:])] = 0x1000_0000 + 4 * self.labels[lab]
+        elif op == "s_addc_u32":
+            self.s[int(a[0][1:])] = 0
+        elif op == "s_mov_b32":
+            self.s[int(a[0][1:])] = self.val(a[1])
+        elif op == "s_and_b32":
+            self.s[int(a[0][1:])] = self.val(a[1]) & self.val(a[2])
+        elif op == "s_add_u32" and a[0] == "m0":
+            assert self.idx_on
+            self.m0 += self.val(a[2])
+        elif op == "s_add_u32":
+            self.s[int(a[0][1:])] = self.val(a[1]) + self.val(a[2])
+        elif op == "s_sub_u32":
+            self.s[int(a[0][1:])] = self.val(a[1]) - self.val(a[2])
+        elif op == "s_cmp_lg_u32":
+            self.scc = self.val(a[0]) != self.val(a[1])
+        elif op == "s_cbranch_scc1":
+            if self.scc:
+                return self.labels[a[0]]
+        elif op == "s_branch":
+            return self.labels[a[0]]
+        elif op == "s_mov_b64":
+            d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
+            self.s[d], self.s[d + 1] = self.s[sr], self.s[sr + 1]
+        elif op == "s_load_dwordx8":
+            d, sr = [int(x) for x in re.findall(r"s\[(\d+):", ln)]
+            addr = (self.s[sr + 1] << 32) | self.s[sr]
+            for i in range(8):
+                self.s[d + i] = self.gmem.get(addr + 4 * i, 0xDEAD)
+        elif op == "s_setpc_b64":
+            lo = int(re.findall(r"s\[(\d+):", ln)[0])
+            return self.addr[(self.s[lo + 1] << 32) | self.s[lo]]
+        elif op == "s_set_gpr_idx_on":
+            assert a[0] == "0"
+            self.idx_on, self.m0 = True, 0
+        elif op == "s_set_gpr_idx_off":
+            self.idx_on = False
+        elif op == "s_waitcnt":
+            pass
+        elif op == "v_mov_b32" and r[0] == gen.PL:
+            self.v[gen.PL] = list(self.pl_lanes)
+        elif op == "v_mov_b32" and r[0] in self.VEC:
+            self.v[r[0]] = list(self.v[r[1]])
+        elif op == "v_mov_b32":
+            self.v[r[0]] = self.val(a[1])
+        elif op == "v_readlane_b32":
+            assert not self.idx_on
+            self.s[int(a[0][1:])] = self.v[r[0]][int(a[2])]
+        elif op == "v_add_u32_e32":
+            assert r[0] == r[1] == gen.PL
+            self.v[gen.PL] = [x + int(a[1]) for x in self.v[gen.PL]]
+        elif op == "ds_read_b32":
+            off = int(ln.split("offset:")[1]) if "offset:" in ln else 0
+            self.v[r[0]] = [self.lds.get(x + off, 0xDEAD) for x in self.v[r[1]]]
+        elif op == "buffer_load_dwordx4":
+            half = 1 if "offset:16" in ln else 0
+            self._load_row(r[0] - 4 * half, self.s[44], half)
+        elif op == "s_setprio":  # scheduling only
+            assert 0 <= int(a[0]) <= 3
+        elif op in ("v_pk_mov_b32", "v_xor_b32_e32", "v_xor_b32_e64", "v_bitop3_b32"):
+            idx = self.m0 if self.idx_on else 0
+            run([ln], self.v, idx)
+        else:
+            raise AssertionError(ln)
+        return pc
 
 
 # the shipped loop and the tuning build's variants (gf_bs.hip MODE 10-14)
@@ -273,3 +278,96 @@ def test_threaded_dispatch_end_to_end_vs_oracle(variant):
             for k in range(nr):
                 exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
             assert np.array_equal(got, exp), (nr, m)
+
+
+class _DynWave(_Wave):
+    """The dynamic-row loop (gen.main_loop_dyn, gf_bs.hip MODE 20): one
+    wave of a workgroup sharing the program and the row counter in `shared`.
+    Rows are taken one at a time; every row must be consumed exactly once
+    across the waves, whatever order they run in."""
+
+    VEC = (gen.D_PG, gen.D_PGN, gen.PL, gen.D_VADDR, gen.D_VCNT, gen.D_VONE, gen.D_VAT)
+
+    def __init__(self, X, A, K, w, kw, shared):
+        self.X, self.A, self.nr = X, A, K
+        offs, _ = gen.body_offsets()
+        self.code, self.addr = [], {}
+        for r in range(gen.NCOPY):
+            for c in range(256):
+                self.addr[self.BASE + offs[r * 256 + c]] = len(self.code)
+                self.code += gen.body_lines(c, r)
+        self.main0 = len(self.code)
+        self.code += [ln.replace("_%=", "") for ln in gen.main_loop_dyn(True)] + ["END"]
+        self.labels = {ln[:-1]: i for i, ln in enumerate(self.code) if ln.endswith(":")}
+        for name, i in self.labels.items():
+            self.addr[0x1000_0000 + 4 * i] = i
+        self.s, self.v = {}, {}
+        self.m0, self.idx_on = 0, False
+        self.lds = shared                      # program at 0x400, counter at 0x40
+        self.exec1 = False
+        prog = 0x400
+        self.ops = {"xlo": 0, "xhi": 0, "nrec": K * 32, "ldx": 32, "thi": self.BASE >> 32, "col": 0,
+                    "sc": w, "sn": w + kw, "nk": K, "km1": K - 1, "r0x32": w * 32,
+                    "pl": None, "cnt": 0x40}
+        self.pl_lanes = [prog + 4 * (lane & 7) for lane in range(64)]
+        self.rows_done = []
+        self._load_row(gen.RING, w * 32)       # the compiler's first ring load (row w)
+
+    def step(self, ln, op, a, r, pc):
+        if op == "s_cmp_ge_u32":
+            self.scc = self.val(a[0]) >= self.val(a[1])
+            if not self.scc:
+                self.rows_done.append(self.s[gen.D_SC])
+        elif op == "s_mul_i32":
+            self.s[int(a[0][1:])] = self.val(a[1]) * self.val(a[2])
+        elif op == "s_min_u32":
+            self.s[int(a[0][1:])] = min(self.val(a[1]), self.val(a[2]))
+        elif op == "s_lshl_b32":
+            self.s[int(a[0][1:])] = self.val(a[1]) << int(a[2])
+        elif op == "v_mov_b32" and r[0] in (gen.D_VCNT, gen.D_VONE):
+            self.v[r[0]] = [self.val(a[1])] * 64
+        elif op == "v_add_u32_e32" and r[0] == gen.D_VADDR:
+            self.v[r[0]] = [self.val(a[1]) + x for x in self.v[gen.PL]]
+        elif op == "s_mov_b64" and a[0] == "exec":
+            self.exec1 = a[1] == "1"
+        elif op == "s_mov_b64" and a[1] == "exec":
+            assert not self.exec1
+        elif op == "ds_add_rtn_u32":
+            assert self.exec1                 # one lane: one row per fetch
+            addr = self.v[r[1]][0]
+            self.v[r[0]] = [self.lds[addr]] + [0xDEAD] * 63
+            self.lds[addr] += self.v[r[2]][0]
+        elif op == "v_readfirstlane_b32":
+            self.s[int(a[0][1:])] = self.v[r[0]][0]
+        elif op == "s_cbranch_scc1":
+            return self.labels[a[0]] if self.scc else pc
+        else:
+            return super().step(ln, op, a, r, pc)
+        return pc
+
+
+@pytest.mark.parametrize("K,kw", [(8, 1), (13, 2), (40, 3), (33, 4)])
+def test_dynamic_rows_end_to_end_vs_oracle(K, kw):
+    rng = np.random.default_rng(100 + K)
+    X = rng.integers(0, 256, (K, 32), dtype=np.uint8)
+    A = rng.integers(0, 256, (8, K), dtype=np.uint8)
+    A[0, 0], A[5, 1] = 0, 1
+    offs, _ = gen.body_offsets()
+    shared = {0x40: 2 * kw}                       # rows 0..2kw-1 are the waves' first two
+    for k in range(K):
+        for m in range(8):
+            shared[0x400 + 4 * (8 * k + m)] = (_Wave.BASE + offs[(m & 3) * 256 + int(A[m, k])]) & 0xFFFFFFFF
+    total = np.zeros((8, 8), np.uint32)
+    done = []
+    order = list(range(kw))[::-1] if K % 2 else list(range(kw))   # any wave order
+    for w in order:
+        wave = _DynWave(X, A, K, w, kw, shared)
+        total ^= wave.run()
+        done += wave.rows_done
+    assert sorted(done) == list(range(K))         # every row exactly once
+    for m in range(8):
+        got = bitslice_np(total[m].view(np.uint8).copy())
+        exp = np.zeros(32, np.uint8)
+        for k in range(K):
+            exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
+        assert np.array_equal(got, exp), (K, kw, m)
