@@ -225,6 +225,24 @@ int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size
  * async, only the coding vectors are read back). */
 int rlnc_decoder_add_pieces(rlnc_decoder* dec, const uint8_t* rows, size_t count, size_t pitch,
                             size_t piece_len, int is_device, size_t* consumed);
+/* The same batch AddPiece over DEVICE wire rows, with the elimination
+ * (decoder_state.go:15-182) on the GPU: one workgroup runs kodr's pivots for
+ * the rows that land on their diagonals (gf_elim.hip); the rest of the batch,
+ * if any, continues on the host from the state it left.  Same state, return
+ * code and *consumed as rlnc_decoder_add_pieces (is_device = 1).  Used on a
+ * fresh decoder with 2 <= piece_count <= 256; otherwise it IS
+ * rlnc_decoder_add_pieces. */
+int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t count, size_t pitch,
+                                size_t piece_len, size_t* consumed);
+/* G decoders of one context and one piece_count at once: one GPU launch
+ * eliminates every eligible decoder's batch (a workgroup each), so G
+ * generations cost about one.  d_rows[g], counts[g]: decoder g's batch;
+ * per-decoder results in consumed[g] and status[g] (what
+ * rlnc_decoder_add_pieces_gpu would return).  The call itself fails only on
+ * bad arguments or device errors. */
+int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
+                                 const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
+                                 int* status);
 int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */
 size_t rlnc_decoder_required(const rlnc_decoder* dec);       /* Required  :38-40 */
 size_t rlnc_decoder_useful(const rlnc_decoder* dec);         /* rank */

@@ -7,6 +7,7 @@
 // is no CPU compute fallback: without a usable HIP device every data call
 // fails with RLNC_ERR_NO_DEVICE / RLNC_ERR_HIP.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 #include <sys/random.h>
 
@@ -89,6 +90,9 @@ struct rlnc_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   kodr_amd::Staging stage;   // pinned chunks for host-pointer copies
+  DevBuf elim_tab;           // gf_elim's field tables (once per context)
+  bool elim_tab_ok = false;
+  DevBuf elim_out;           // gf_elim's per-generation states and counts
 };
 
 struct rlnc_encoder {
@@ -385,6 +389,8 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   ctx->stage.release();
+  ctx->elim_tab.release();
+  ctx->elim_out.release();
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
@@ -1037,6 +1043,70 @@ int rlnc_decoder_add_piece_device(rlnc_decoder* d, const uint8_t* vec, size_t vl
   return dec_add(d, vec, vlen, d_piece, plen, true);
 }
 
+namespace {
+
+// Data side of a batched AddPiece, before the elimination: device rows and
+// rows from pinned host memory are copied (and, for a large batch,
+// bit-sliced into the decoder's twin) first, so the GPU work overlaps the
+// elimination; rows past the ones accepted land beyond the received range
+// and are never read.  The rows that can still be accepted before full rank
+// (plus some slack for dependent ones) are copied first; the rest, if any are
+// accepted, after (dec_batch_post).
+struct BatchCopy {
+  size_t row0 = 0, pre = 0, twin_end = 0;
+  bool early = false;
+};
+
+int dec_batch_pre(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch, bool dev, BatchCopy* bc) {
+  const size_t k = d->core.piece_count();
+  bc->row0 = d->core.received();
+  bc->early = d->ctx && (dev || kodr_amd::Staging::is_pinned(rows));
+  bc->pre = bc->early ? std::min(count, d->core.required() + 16) : 0;
+  bc->twin_end = 0;
+  const size_t row0 = bc->row0, pre = bc->pre;
+  if (!pre) return RLNC_OK;
+  TRY(dec_reserve_rows(d, row0 + pre, row0));
+  uint8_t* dst = d->recv.p + row0 * d->pitch;
+  const bool twin = pre >= kBsMinRowsDecode && d->pitch % 32 == 0 &&
+                    !few_narrow_rows(d->core.piece_count(), row0 + pre, d->L);  // else dec_gemm takes gf_gemm
+  if (twin) {
+    d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
+    if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
+      TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
+      d->bs_rows = 0;
+    }
+  }
+  // device rows whose twin starts here: copy and bit-slice in one pass
+  const bool fused = twin && dev && d->bs_rows == row0 && d->L % 32 == 0 &&
+                     kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, d->recv_bs.p + row0 * d->pitch, d->pitch,
+                                                  pre, d->L, d->ctx->stream) == hipSuccess;
+  if (!fused) {
+    if (dev)
+      HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
+    else
+      HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice, d->ctx->stream));
+    if (twin)
+      HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
+                                   d->pitch, row0 + pre - d->bs_rows, d->L, d->ctx->stream));
+  }
+  if (twin) bc->twin_end = row0 + pre;
+  return RLNC_OK;
+}
+
+// after the elimination accepted n rows of the batch
+int dec_batch_post(rlnc_decoder* d, const uint8_t* rows, size_t pitch, bool dev, const BatchCopy& bc, size_t n) {
+  const size_t k = d->core.piece_count();
+  if (n) d->decoded_ready = false;
+  if (bc.twin_end) d->bs_rows = bc.row0 + std::min(n, bc.pre);  // only accepted rows' twin counts
+  // accepted rows not copied yet (dependent rows past the slack, or the
+  // staged path) -> one 2D copy
+  if (n > bc.pre) TRY(dec_store_pieces(d, bc.row0 + bc.pre, rows + bc.pre * pitch + k, pitch, n - bc.pre, dev));
+  if (bc.early && !dev) HIPC(hipStreamSynchronize(d->ctx->stream));  // the caller may reuse rows on return
+  return RLNC_OK;
+}
+
+}  // namespace
+
 int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
                             size_t piece_len, int is_device, size_t* consumed) {
   if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
@@ -1051,7 +1121,7 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   size_t vpitch = pitch;
   // device rows: one strided copy of all coding vectors to the host (the
   // pieces never leave the device).  A small one is only started here and
-  // awaited after the piece copies below are enqueued behind it.
+  // awaited after the piece copies are enqueued behind it.
   int vticket = -1;
   if (dev) {
     d->hvecs.resize(count * k);
@@ -1062,55 +1132,135 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
     vecs = d->hvecs.data();
     vpitch = k;
   }
-  // Device rows and rows from pinned host memory are copied (and, for a large
-  // batch, bit-sliced into the decoder's twin) before the elimination, so the
-  // GPU work overlaps it; rows past the ones accepted land beyond the received
-  // range and are never read.
-  // The rows that can still be accepted before full rank (plus some slack for
-  // dependent ones) are copied first; the rest, if any are accepted, after.
-  const size_t row0 = d->core.received();
-  const bool early = d->ctx && (dev || kodr_amd::Staging::is_pinned(rows));
-  const size_t pre = early ? std::min(count, d->core.required() + 16) : 0;
-  size_t twin_end = 0;
-  if (pre) {
-    TRY(dec_reserve_rows(d, row0 + pre, row0));
-    uint8_t* dst = d->recv.p + row0 * d->pitch;
-    const bool twin = pre >= kBsMinRowsDecode && d->pitch % 32 == 0 &&
-                      !few_narrow_rows(d->core.piece_count(), row0 + pre, d->L);  // else dec_gemm takes gf_gemm
-    if (twin) {
-      d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
-      if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
-        TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
-        d->bs_rows = 0;
-      }
-    }
-    // device rows whose twin starts here: copy and bit-slice in one pass
-    const bool fused = twin && dev && d->bs_rows == row0 && d->L % 32 == 0 &&
-                       kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, d->recv_bs.p + row0 * d->pitch, d->pitch,
-                                                    pre, d->L, d->ctx->stream) == hipSuccess;
-    if (!fused) {
-      if (dev)
-        HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
-      else
-        HIPC(hipMemcpy2DAsync(dst, d->pitch, rows + k, pitch, d->L, pre, hipMemcpyHostToDevice,
-                              d->ctx->stream));
-      if (twin)
-        HIPC(kodr_amd::bitslice_rows(d->recv.p + d->bs_rows * d->pitch, d->recv_bs.p + d->bs_rows * d->pitch,
-                                     d->pitch, row0 + pre - d->bs_rows, d->L, d->ctx->stream));
-    }
-    if (twin) twin_end = row0 + pre;
-  }
+  BatchCopy bc;
+  TRY(dec_batch_pre(d, rows, count, pitch, dev, &bc));
   if (vticket >= 0) HIPC(d->ctx->stage.d2h_small_end(vticket, d->hvecs.data(), k, k, count));
   // coefficient side, exactly as repeated AddPiece calls
   size_t n = 0;
   const int st = d->core.add_many(vecs, vpitch, count, &n);
-  if (n) d->decoded_ready = false;
-  if (twin_end) d->bs_rows = row0 + std::min(n, pre);  // only accepted rows' twin counts
-  // data side: accepted rows not copied yet (dependent rows past the slack,
-  // or the staged path) -> one 2D copy
-  if (n > pre) TRY(dec_store_pieces(d, row0 + pre, rows + pre * pitch + k, pitch, n - pre, dev));
-  if (early && !dev) HIPC(hipStreamSynchronize(d->ctx->stream));  // the caller may reuse rows on return
+  TRY(dec_batch_post(d, rows, pitch, dev, bc, n));
   *consumed = n;
+  return st;
+}
+
+namespace {
+
+// the field tables gf_elim reads (uploaded once per context)
+int ctx_elim_tables(rlnc_ctx* ctx) {
+  if (ctx->elim_tab_ok) return RLNC_OK;
+  ctx->elim_tab.bind(ctx->device, ctx->stream);
+  TRY(ctx->elim_tab.reserve(kodr_amd::kElimTableWords * 4));
+  std::vector<uint32_t> t(kodr_amd::kElimTableWords);
+  kodr_amd::elim_tables(t.data());
+  HIPC(ctx->stage.h2d(ctx->elim_tab.p, t.size() * 4, reinterpret_cast<const uint8_t*>(t.data()), t.size() * 4,
+                      t.size() * 4, 1, ctx->stream));
+  ctx->elim_tab_ok = true;
+  return RLNC_OK;
+}
+
+}  // namespace
+
+int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_t* const* rows,
+                                 const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
+                                 int* status) {
+  if (!ds || !rows || !counts || !consumed || !status || !G) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
+  if (!ctx) return RLNC_ERR_NO_DEVICE;
+  const size_t k = ds[0]->core.piece_count();
+  for (size_t g = 0; g < G; g++) {
+    if (!ds[g] || !rows[g]) return RLNC_ERR_INVALID_ARGUMENT;
+    if (ds[g]->ctx != ctx || ds[g]->core.piece_count() != k) return RLNC_ERR_INVALID_ARGUMENT;
+    consumed[g] = 0;
+    status[g] = RLNC_OK;
+  }
+  if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  // GPU elimination for fresh decoders with >= 2 rows (kElimMaxGens per
+  // launch); every other decoder takes rlnc_decoder_add_pieces
+  std::vector<size_t> gpu;
+  std::vector<BatchCopy> bcs(G);
+  for (size_t g = 0; g < G; g++) {
+    rlnc_decoder* d = ds[g];
+    const bool ok = k >= 2 && k <= 256 && counts[g] >= 2 && d->core.received() == 0;
+    if (!ok) {
+      status[g] = rlnc_decoder_add_pieces(d, rows[g], counts[g], pitch, piece_len, 1, &consumed[g]);
+      continue;
+    }
+    if ((status[g] = dec_check(d, k, rows[g] + k, piece_len)) != RLNC_OK) continue;
+    if ((status[g] = dec_batch_pre(d, rows[g], counts[g], pitch, true, &bcs[g])) != RLNC_OK) continue;
+    gpu.push_back(g);
+  }
+  if (gpu.empty()) return RLNC_OK;
+  TRY(ctx_elim_tables(ctx));
+  const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
+  const size_t chunk = std::min<size_t>(gpu.size(), kodr_amd::kElimMaxGens);
+  ctx->elim_out.bind(ctx->device, ctx->stream);
+  TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
+  std::vector<uint8_t> host(hdr + chunk * ostride);
+  for (size_t c0 = 0; c0 < gpu.size(); c0 += chunk) {
+    const size_t nc = std::min(chunk, gpu.size() - c0);
+    kodr_amd::ElimArgs a = {};
+    for (size_t i = 0; i < nc; i++) {
+      const size_t g = gpu[c0 + i];
+      a.vecs[i] = rows[g];
+      a.n[i] = (int)std::min(counts[g], k);
+    }
+    a.vpitch = pitch;
+    a.tables = reinterpret_cast<const uint32_t*>(ctx->elim_tab.p);
+    a.out = ctx->elim_out.p + hdr;
+    a.out_gen_stride = ostride;
+    a.out_pitch = opitch;
+    a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
+    a.k = (int)k;
+    HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
+    HIPC(ctx->stage.d2h(host.data(), hdr + nc * ostride, ctx->elim_out.p, hdr + nc * ostride, hdr + nc * ostride,
+                        1, ctx->stream));
+#ifdef KODR_ELIM_TIMING
+    if (const char* dump = getenv("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
+      if (FILE* fp = fopen(dump, "wb")) {
+        fwrite(host.data(), 1, hdr + nc * ostride, fp);
+        fclose(fp);
+      }
+      for (size_t i = 0; i < nc; i++) memset(host.data() + i * sizeof(int), 0, sizeof(int));
+    }
+#endif
+    const int* cnt = reinterpret_cast<const int*>(host.data());
+    for (size_t i = 0; i < nc; i++) {
+      const size_t g = gpu[c0 + i];
+      rlnc_decoder* d = ds[g];
+      size_t c = (size_t)std::max(cnt[i], 0);
+      if (c && !d->core.load_rref(host.data() + hdr + i * ostride, opitch, c)) c = 0;
+      // the rest of the batch (past a row off its diagonal, or past k) through
+      // kodr's algorithm on the host, from the state the GPU left
+      int st = RLNC_OK;
+      size_t n = c;
+      if (c < counts[g]) {
+        if (d->core.is_decoded()) {
+          st = RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;  // full/decoder.go:52-54
+        } else {
+          const size_t rest = counts[g] - c;
+          d->hvecs.resize(rest * k);
+          HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, ctx->stream));
+          size_t m = 0;
+          st = d->core.add_many(d->hvecs.data(), k, rest, &m);
+          n += m;
+        }
+      }
+      const int pst = dec_batch_post(d, rows[g], pitch, true, bcs[g], n);
+      consumed[g] = n;
+      status[g] = pst != RLNC_OK ? pst : st;
+    }
+  }
+  return RLNC_OK;
+}
+
+int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
+                                size_t piece_len, size_t* consumed) {
+  if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
+  *consumed = 0;
+  if (!count) return RLNC_OK;
+  int st = RLNC_OK;
+  TRY(rlnc_decoders_add_pieces_gpu(&d, 1, &rows, &count, pitch, piece_len, consumed, &st));
   return st;
 }
 

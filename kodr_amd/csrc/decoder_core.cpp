@@ -514,6 +514,28 @@ void DecoderCore::rref_clean() {
   all_clean_ = false;
 }
 
+bool DecoderCore::load_rref(const uint8_t* state, size_t pitch, size_t c) {
+  if (received_ != 0 || c < 2 || c > k_) return false;
+  ensure_tcap(c);
+  for (size_t i = 0; i < c; i++) {
+    const uint8_t* src = state + i * pitch;
+    if (src[i] != 1) return false;  // not the RREF with diagonal pivots: refuse (state untouched so far)
+  }
+  for (size_t i = 0; i < c; i++) {
+    uint8_t* row = free_.back();
+    free_.pop_back();
+    memcpy(row, state + i * pitch, k_ + c);
+    memset(row + k_ + c, 0, tcap_ - c);
+    push_row(row, -1, 0);
+    clean_[i] = 1;
+    touched_[i] = 0;
+  }
+  received_ = c;
+  useful_ = c;
+  all_clean_ = true;
+  return true;
+}
+
 int DecoderCore::piece_available(size_t idx) const {
   if (idx >= k_) return 12;                         // :222-224 ErrPieceOutOfBound
   if (idx >= rows_.size()) return 11;               // :225-227 ErrPieceNotDecodedYet

@@ -34,6 +34,14 @@ class DecoderCore {
   // existing rows per 4 new ones); the result is the same state.
   int add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* used);
 
+  // A fresh decoder (nothing received) takes the state kodr reaches after c
+  // >= 2 pieces that all landed on their diagonals: the reduced row echelon
+  // form of [first c vectors | I_c], given as c rows of k + c bytes
+  // (coefficients, then T) at `pitch` -- computed elsewhere (gf_elim.hip).
+  // Later add() / add_many() calls continue exactly as if those c pieces had
+  // been added one by one.  Returns false (and changes nothing) otherwise.
+  bool load_rref(const uint8_t* state, size_t pitch, size_t c);
+
   bool is_decoded() const { return useful_ >= k_; }   // full/decoder.go:32-34
   size_t required() const { return k_ - useful_; }    // full/decoder.go:38-40
   size_t useful() const { return useful_; }

@@ -68,6 +68,27 @@ hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, siz
 hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
                         size_t n_sys, size_t sys_first, hipStream_t stream);
 
+// ---- decoder elimination on the GPU (gf_elim.hip) ----
+// One workgroup per decoder: Gauss-Jordan of the first n coding vectors of
+// generation g in arrival order while every pivot lands on its diagonal; the
+// state after c clean rows (c x (k + c) bytes: coefficients [I | X], T) is
+// written at out + g * out_gen_stride with row pitch out_pitch, and c (0 when
+// fewer than 2 rows were clean) at counts[g].  2 <= k <= 256.
+constexpr int kElimMaxGens = 64;
+struct ElimArgs {
+  const uint8_t* vecs[kElimMaxGens];  // generation g's first coding vector (device)
+  int n[kElimMaxGens];                // its rows
+  uint64_t vpitch;                    // bytes between consecutive vectors
+  const uint32_t* tables;             // elim_tables(), on the device
+  uint8_t* out;
+  uint64_t out_gen_stride, out_pitch; // out_pitch >= 256 (k <= 128) or 512
+  int* counts;
+  int k;
+};
+constexpr size_t kElimTableWords = 256 * 8 + 64;
+void elim_tables(uint32_t* host_out);  // kElimTableWords dwords
+hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
+
 // ---- bit-sliced path (gf_bs.hip) ----
 // dst = src with every 32-byte block of rows [0, rows) x [0, round_up(ncols,
 // 32)) turned into 8 bit planes (self-inverse); src == dst works in place.

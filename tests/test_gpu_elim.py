@@ -1,0 +1,205 @@
+"""GPU elimination (gf_elim.hip through rlnc_decoder_add_pieces_gpu /
+rlnc_decoders_add_pieces_gpu) against the host elimination (DecoderCore,
+itself tied to the oracle's literal restatement of decoder_state.go in
+tests/test_capi_host.py) and the oracle: return codes, rows consumed,
+counters, the coefficient matrix and the transform T byte for byte, and the
+decoded pieces."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from kodr_amd import _lib, errors
+
+pytestmark = pytest.mark.gpu
+U8P = _lib._u8p
+
+
+class Dec:
+    def __init__(self, ctx, k):
+        self.k = k
+        self.h = ctypes.c_void_p()
+        errors.check(_lib.lib().rlnc_decoder_create(ctx.handle, k, ctypes.byref(self.h)))
+
+    def state(self):
+        L = _lib.lib()
+        return (L.rlnc_decoder_useful(self.h), L.rlnc_decoder_received(self.h),
+                L.rlnc_decoder_required(self.h), bool(L.rlnc_decoder_is_decoded(self.h)))
+
+    def coefficients(self):
+        r = _lib.lib().rlnc_decoder_useful(self.h)
+        out = np.empty((r, self.k), np.uint8)
+        if r:
+            errors.check(_lib.lib().rlnc_decoder_coefficients(self.h, out.ctypes.data_as(U8P)))
+        return out
+
+    def transform(self):
+        L = _lib.lib()
+        r, n = L.rlnc_decoder_useful(self.h), L.rlnc_decoder_received(self.h)
+        out = np.empty((r, n), np.uint8)
+        if r:
+            errors.check(L.rlnc_decoder_transform(self.h, out.ctypes.data_as(U8P)))
+        return out
+
+    def get_all(self):
+        L = _lib.lib()
+        n, pl = L.rlnc_decoder_useful(self.h), L.rlnc_decoder_piece_length(self.h)
+        out = np.empty((n, pl), np.uint8)
+        st = L.rlnc_decoder_get_pieces(self.h, out.ctypes.data_as(U8P))
+        return st, out
+
+    def __del__(self):
+        _lib.lib().rlnc_decoder_destroy(self.h)
+
+
+def _vectors(rng, kind, n, k):
+    if kind == "dense":
+        return rng.integers(0, 256, (n, k), dtype=np.uint8)
+    if kind == "tiny":  # zero diagonals, dependent rows, duplicates
+        return rng.integers(0, 3, (n, k), dtype=np.uint8)
+    if kind == "lowrank":
+        B = rng.integers(0, 256, (max(1, k // 2), k), dtype=np.uint8)
+        return oracle.matmul(rng.integers(0, 256, (n, B.shape[0]), dtype=np.uint8), B)[1]
+    if kind == "zero_mid":  # a zero row in the middle of a clean run
+        V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        V[min(n - 1, k // 2)] = 0
+        return V
+    if kind == "systematic":  # units in order with a loss, then coded rows
+        eye = np.eye(k, dtype=np.uint8)[[i for i in range(k) if i != k // 3]]
+        return np.concatenate([eye, rng.integers(0, 256, (n, k), dtype=np.uint8)])[:n]
+    if kind == "first_zero":  # the first piece is all zero (counted useful, full/decoder.go:58-61)
+        V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        V[0] = 0
+        return V
+    raise ValueError(kind)
+
+
+def _rows(ctx, V, P, L):
+    n, k = V.shape
+    pitch = ((k + L + 15) // 16) * 16 + 16
+    rows = np.zeros((n, pitch), np.uint8)
+    rows[:, :k] = V
+    rows[:, k:k + L] = oracle.encode(P, V)
+    d = ctx.alloc(rows.nbytes)
+    ctx.h2d(d, rows)
+    return d, pitch
+
+
+def _same(a, b):
+    assert a.state() == b.state()
+    assert np.array_equal(a.coefficients(), b.coefficients())
+    assert np.array_equal(a.transform(), b.transform())
+
+
+@pytest.mark.parametrize("kind", ["dense", "tiny", "lowrank", "zero_mid", "systematic", "first_zero"])
+@pytest.mark.parametrize("k", [2, 3, 16, 65, 128, 200, 256])
+def test_gpu_elimination_matches_host(gpu_ctx, kind, k):
+    rng = np.random.default_rng(k * 31 + len(kind))
+    L = 40
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    n = k + 3
+    V = _vectors(rng, kind, n, k)
+    drows, pitch = _rows(gpu_ctx, V, P, L)
+    host, gpu = Dec(gpu_ctx, k), Dec(gpu_ctx, k)
+    ch, cg = ctypes.c_size_t(), ctypes.c_size_t()
+    sh = _lib.lib().rlnc_decoder_add_pieces(host.h, ctypes.c_void_p(drows), n, pitch, L, 1, ctypes.byref(ch))
+    sg = _lib.lib().rlnc_decoder_add_pieces_gpu(gpu.h, ctypes.c_void_p(drows), n, pitch, L, ctypes.byref(cg))
+    assert (sg, cg.value) == (sh, ch.value)
+    _same(host, gpu)
+    # and the oracle's literal decoder, step by step
+    ref = oracle.Decoder(k)
+    C = oracle.encode(P, V)
+    exp_n = 0
+    for i in range(n):
+        if ref.add(V[i], C[i]) != 0:
+            break
+        exp_n += 1
+    assert cg.value == exp_n
+    assert gpu.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+    assert np.array_equal(gpu.coefficients(), ref.coeffs())
+    if ref.is_decoded():
+        st, out = gpu.get_all()
+        assert st == 0 and np.array_equal(out, P)
+    gpu_ctx.synchronize()
+    gpu_ctx.free(drows)
+
+
+def test_gpu_elimination_batched_generations(gpu_ctx):
+    """Several decoders in one launch: fresh ones with clean and quirky
+    batches, one that already holds a piece (host path), one with a single
+    row (host path); each ends exactly as rlnc_decoder_add_pieces leaves it."""
+    rng = np.random.default_rng(77)
+    k, L = 64, 100
+    kinds = ["dense", "tiny", "dense", "lowrank", "dense", "systematic", "dense"]
+    gens = []
+    for gi, kind in enumerate(kinds):
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        n = 1 if gi == 4 else k + int(rng.integers(0, 5))
+        V = _vectors(rng, kind, n, k)
+        gens.append((P, V))
+    pitch = ((k + L + 15) // 16) * 16
+    bufs, hosts, gpus = [], [], []
+    for gi, (P, V) in enumerate(gens):
+        rows = np.zeros((V.shape[0], pitch), np.uint8)
+        rows[:, :k], rows[:, k:k + L] = V, oracle.encode(P, V)
+        d = gpu_ctx.alloc(rows.nbytes)
+        gpu_ctx.h2d(d, rows)
+        bufs.append(d)
+        hosts.append(Dec(gpu_ctx, k))
+        gpus.append(Dec(gpu_ctx, k))
+    # decoder 2 already holds one piece: not fresh, takes the host path
+    c0 = ctypes.c_size_t()
+    for dec in (hosts[2], gpus[2]):
+        assert _lib.lib().rlnc_decoder_add_pieces(dec.h, ctypes.c_void_p(bufs[2]), 1, pitch, L, 1,
+                                                  ctypes.byref(c0)) == 0
+    G = len(gens)
+    off = [1 if gi == 2 else 0 for gi in range(G)]
+    counts = (ctypes.c_size_t * G)(*[gens[gi][1].shape[0] - off[gi] for gi in range(G)])
+    rows_p = (ctypes.c_void_p * G)(*[bufs[gi] + off[gi] * pitch for gi in range(G)])
+    decs = (ctypes.c_void_p * G)(*[g.h.value for g in gpus])
+    consumed = (ctypes.c_size_t * G)()
+    status = (ctypes.c_int * G)()
+    errors.check(_lib.lib().rlnc_decoders_add_pieces_gpu(decs, G, rows_p, counts, pitch, L, consumed, status))
+    for gi in range(G):
+        c = ctypes.c_size_t()
+        st = _lib.lib().rlnc_decoder_add_pieces(hosts[gi].h, ctypes.c_void_p(rows_p[gi]), counts[gi], pitch, L, 1,
+                                                ctypes.byref(c))
+        assert (status[gi], consumed[gi]) == (st, c.value), gi
+        _same(hosts[gi], gpus[gi])
+        if hosts[gi].state()[3]:
+            s1, a = gpus[gi].get_all()
+            assert s1 == 0 and np.array_equal(a, gens[gi][0])
+    gpu_ctx.synchronize()
+    for d in bufs:
+        gpu_ctx.free(d)
+
+
+def test_gpu_elimination_c2_round_trip(gpu_ctx):
+    """32 MiB / 256 (BASELINE config 2): k + 2 device wire rows drawn by the
+    engine, eliminated on the GPU, GetPieces equals the generation."""
+    k, L = 256, 131072
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, k * L, dtype=np.uint8)
+    eh = ctypes.c_void_p()
+    errors.check(_lib.lib().rlnc_encoder_create(gpu_ctx.handle, 0, data.ctypes.data_as(U8P), k, L,
+                                                ctypes.byref(eh)))
+    W = k + L
+    n = k + 2
+    dW = gpu_ctx.alloc(n * W)
+    errors.check(_lib.lib().rlnc_encoder_coded_wire_device(eh, n, dW, W))
+    dec, host = Dec(gpu_ctx, k), Dec(gpu_ctx, k)
+    c = ctypes.c_size_t()
+    st = _lib.lib().rlnc_decoder_add_pieces_gpu(dec.h, ctypes.c_void_p(dW), n, W, L, ctypes.byref(c))
+    ch = ctypes.c_size_t()
+    sh = _lib.lib().rlnc_decoder_add_pieces(host.h, ctypes.c_void_p(dW), n, W, L, 1, ctypes.byref(ch))
+    assert (st, c.value) == (sh, ch.value)
+    assert dec.state()[3]
+    assert np.array_equal(dec.transform(), host.transform())
+    dDec = gpu_ctx.alloc(k * L)
+    errors.check(_lib.lib().rlnc_decoder_get_pieces_device(dec.h, dDec, L))
+    assert np.array_equal(gpu_ctx.d2h(dDec, k * L), data)
+    _lib.lib().rlnc_encoder_destroy(eh)
+    gpu_ctx.synchronize()
+    gpu_ctx.free(dW)
+    gpu_ctx.free(dDec)
