@@ -521,6 +521,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["c2_recode"] = recode_c2(ctx, L_, errors, encs[0], k, L, rng)
     out["c5_encode_recode_one_gpu"] = c5_one_gpu(ctx, L_, errors, encs[:8], k, L, rng)
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
+    out["batched_decode_elimination"] = batched_elim(ctx, L_, errors, rng)
     out["c1_roundtrip"] = c1_roundtrip(ctx, L_, errors, rng)
     out["encode_two_streams"] = two_streams(L_, errors, k, L, rng)
     out["host_path"] = host_roundtrip(ctx, L_, errors, k, L, rng)
@@ -656,6 +657,57 @@ def c5_one_gpu(ctx, L_, errors, encs, k, L, rng, reps=3):
             "coded_plus_recoded_MBps": round(units / best / 1e6, 1),
             "note": "per generation: k encoded + k recoded pieces, kodr SetBytes units for both; host wall time, "
                     "recoder construction (D2D copy of the received rows + twin) included"}
+
+
+def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
+    """Batched AddPiece on G fresh decoders (k + 2 device wire rows each,
+    short pieces so the coefficient side dominates): host elimination
+    (rlnc_decoder_add_pieces per decoder) against one GPU launch
+    (rlnc_decoders_add_pieces_gpu, gf_elim.hip: a workgroup per decoder)."""
+    import ctypes
+    import numpy as np
+    n = k + 2
+    pitch = (k + L + 15) // 16 * 16
+    bufs = []
+    for g in range(G):
+        rows = rng.integers(0, 256, (n, pitch), dtype=np.uint8)
+        d = ctx.alloc(rows.nbytes)
+        ctx.h2d(d, rows)
+        bufs.append(d)
+    res = {"k": k, "generations": G, "piece_len": L}
+    for mode in ("host", "gpu"):
+        best, ok = None, True
+        for rep in range(reps):
+            decs = []
+            for g in range(G):
+                h = ctypes.c_void_p()
+                errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+                decs.append(h)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            if mode == "host":
+                for g in range(G):
+                    c = ctypes.c_size_t()
+                    st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g], n, pitch, L, 1, ctypes.byref(c))
+                    ok = ok and st in (0, 3)
+            else:
+                cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+                errors.check(L_.rlnc_decoders_add_pieces_gpu((ctypes.c_void_p * G)(*[x.value for x in decs]), G,
+                                                             (ctypes.c_void_p * G)(*bufs), (ctypes.c_size_t * G)(*([n] * G)),
+                                                             pitch, L, cons, sts))
+                ok = ok and all(s_ in (0, 3) for s_ in sts)
+            ctx.synchronize()
+            t = time.perf_counter() - t0
+            ok = ok and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
+            for x in decs:
+                L_.rlnc_decoder_destroy(x)
+            best = t if best is None else min(best, t)
+        res[mode + "_ms"] = round(best * 1e3, 3)
+        res[mode + "_ok"] = ok
+    res["gpu_speedup"] = round(res["host_ms"] / res["gpu_ms"], 2)
+    for d in bufs:
+        ctx.free(d)
+    return res
 
 
 def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3):

@@ -254,8 +254,9 @@ constexpr size_t kBsTwinBudget = 16u << 20;  // bytes of new twin rows worth bui
 // Few rows of narrow pieces: gf_gemm's one-wave tiles beat the bit-sliced
 // launch's fixed cost (K = 16, 128 KiB rows, 9-32 output rows: 4.8-7.2 us
 // against 8.7-9.0; K = 32: up to 16 rows; profiles/r01/bs_vs_gemm_small_k.log).
+// Capped at the measured range: M <= 32.
 bool few_narrow_rows(size_t M, size_t K, size_t ncols) {
-  return K <= 32 && ncols <= ((size_t)256 << 10) && (K <= 16 || M <= 16);
+  return K <= 32 && ncols <= ((size_t)256 << 10) && M <= 32 && (K <= 16 || M <= 16);
 }
 
 // The bit-sliced twin of a resident, immutable X (K rows at pitch ldx), built

@@ -487,8 +487,13 @@ GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   // K = 16-200, L = 64 KiB-4 MiB, M = 1-8 (tools/sweep_fewrows*.sh,
   // profiles/r01/sweep_fewrows*.log): K <= 32 always; K <= 64 from 128 KiB
   // rows (from 64 KiB for M >= 4); K <= 128 from 256 KiB rows; not at K = 200.
+  // The rule also takes more than 8 output rows (8-row tiles, each re-reading
+  // X from L2).  Timed there only at M <= 32, K = 16-128, 128 KiB and 1 MiB
+  // rows (tools/bs_vs_gemm_small_k.py, profiles/r01/bs_vs_gemm_small_k.log);
+  // callers with M >= 9 normally take the bit-sliced kernel instead
+  // (capi.cpp kBsMinRows, few_narrow_rows), so larger M reaches this only
+  // where that kernel cannot take the shape.
   const size_t nxc = (ncols + 511) / 512;
-  // (More than 8 output rows: 8-row tiles, each re-reading X from L2.)
   if (K <= 32 || (K <= 64 && (M >= 4 || nxc >= 256)) || (K <= 128 && nxc >= 512)) {
     int mt = M <= 1 ? 1 : M <= 2 ? 2 : M <= 4 ? 4 : 8;
     while (mt > 1 && nxc * ((M + mt - 1) / mt) < 1024) mt /= 2;

@@ -151,8 +151,10 @@ def test_gf_matmul_vs_oracle(gpu_ctx, M, K):
                                        (5, 17, 300000 + 3), (2, 255, 262144), (8, 16, 65536 + 5),
                                        (20, 24, 262144 + 32), (33, 64, 131072)])
 def test_gf_matmul_few_rows_wide_vs_oracle(gpu_ctx, M, K, ncols):
-    # the one-wave gf_gemm tiles (K < 256 with rows of >= 256 KiB, or K <= 16),
-    # split over row tiles: bit-exact, and nothing written past ncols
+    # the one-wave gf_gemm tiles (choose_gemm_config: K <= 32 always, K <= 64
+    # from 128 KiB rows or M >= 4, K <= 128 from 256 KiB rows), split over row
+    # tiles, including more than 8 output rows: bit-exact, nothing written
+    # past ncols
     rng = np.random.default_rng(M * 7919 + K)
     ld = (ncols + 255) // 256 * 256
     A = rng.integers(0, 256, (M, K), dtype=np.uint8)
