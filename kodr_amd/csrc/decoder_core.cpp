@@ -148,6 +148,10 @@ int DecoderCore::add(const uint8_t* vec) {
 }
 
 int DecoderCore::add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* used) {
+  if (received_ == 0 && n >= k_ && solve_systematic_batch(vecs, pitch)) {
+    *used = k_;
+    return n > k_ ? 3 : 0;  // full/decoder.go:52-54 for the rows past k
+  }
   size_t i = 0;
   int st = 0;
   while (i < n) {
@@ -201,6 +205,84 @@ bool DecoderCore::append_unit(const uint8_t* vec) {
   touched_[R] = 0;
   useful_ = rows_.size();
   return true;
+}
+
+// A fresh decoder handed k or more rows whose first k coding vectors C are
+// linearly independent ends, whatever route kodr's passes take, in the state
+// [I | C^-1] with all k rows accepted: an independent row never becomes zero,
+// rank counts kept rows, and the kept k x k coefficient half has a zero strict
+// lower triangle, so it is upper triangular, invertible, hence diagonal, and
+// the backward pass normalizes it (gf_elim.hip, full batches).  For a
+// systematic batch -- unit rows a*e_p with distinct pivots and m dense rows
+// among the first k, m small -- C^-1 follows from the m x m block X of the
+// dense rows on the m columns no unit row covers ("lost"):
+//  * column p of a unit row (arrival i, scale a): T[p] = inv(a) * e_i;
+//  * lost column j (index j' among the lost ones): with x = row j' of X^-1,
+//    w = sum_d x_d * dense row d is e_j plus entries w[p] on unit columns, so
+//    T[j] = sum_d x_d * e_arrival(d) + sum_p w[p] * inv(a_p) * e_arrival(p).
+// Returns false (nothing changed) when the batch is not of that form or C is
+// singular; add_many then takes kodr's route row by row.
+bool DecoderCore::solve_systematic_batch(const uint8_t* vecs, size_t pitch) {
+  const size_t k = k_;
+  if (received_ != 0 || k < 2) return false;
+  const size_t mmax = std::max<size_t>(8, k / 8);
+  std::vector<int32_t> unit_at(k, -1);  // arrival index of the unit row with pivot p
+  std::vector<size_t> dense;
+  for (size_t i = 0; i < k; i++) {
+    const int32_t p = unit_col(vecs + i * pitch, k);
+    if (p < 0) {
+      if (dense.size() == mmax) return false;
+      dense.push_back(i);
+    } else {
+      if (unit_at[p] >= 0) return false;  // two rows on one pivot: C singular
+      unit_at[p] = (int32_t)i;
+    }
+  }
+  const size_t m = dense.size();
+  if (m == 0 || m == k) return false;  // no dense rows: the unit appends are as cheap; none: panels
+  std::vector<size_t> lost;
+  for (size_t c = 0; c < k; c++)
+    if (unit_at[c] < 0) lost.push_back(c);
+  // [X | I_m] -> [I_m | X^-1] by Gauss-Jordan with a pivot search
+  const hostgf::Tables& t = T();
+  const size_t w2 = 2 * m;
+  std::vector<uint8_t> M(m * w2, 0);
+  for (size_t r = 0; r < m; r++) {
+    const uint8_t* v = vecs + dense[r] * pitch;
+    for (size_t c = 0; c < m; c++) M[r * w2 + c] = v[lost[c]];
+    M[r * w2 + m + r] = 1;
+  }
+  for (size_t c = 0; c < m; c++) {
+    size_t pr = c;
+    while (pr < m && !M[pr * w2 + c]) pr++;
+    if (pr == m) return false;  // X singular, so is C
+    if (pr != c)
+      for (size_t q = 0; q < w2; q++) std::swap(M[pr * w2 + q], M[c * w2 + q]);
+    hostgf::scale(&M[c * w2], w2, t.inv(M[c * w2 + c]));
+    for (size_t r = 0; r < m; r++)
+      if (r != c && M[r * w2 + c]) hostgf::axpy(&M[r * w2], &M[c * w2], w2, M[r * w2 + c]);
+  }
+  // state rows [e_j | T[j]], T over the k accepted rows in arrival order
+  const size_t w = 2 * k;
+  std::vector<uint8_t> S(k * w, 0), wrow(k);
+  for (size_t p = 0; p < k; p++) {
+    S[p * w + p] = 1;
+    if (unit_at[p] >= 0) S[p * w + k + unit_at[p]] = t.inv(vecs[(size_t)unit_at[p] * pitch + p]);
+  }
+  for (size_t jj = 0; jj < m; jj++) {
+    const uint8_t* x = &M[jj * w2 + m];
+    uint8_t* row = &S[lost[jj] * w];
+    std::fill(wrow.begin(), wrow.end(), 0);
+    for (size_t d = 0; d < m; d++) {
+      if (!x[d]) continue;
+      row[k + dense[d]] = x[d];
+      hostgf::axpy(wrow.data(), vecs + dense[d] * pitch, k, x[d]);
+    }
+    for (size_t p = 0; p < k; p++)
+      if (unit_at[p] >= 0 && wrow[p])
+        row[k + unit_at[p]] = t.mul(wrow[p], t.inv(vecs[(size_t)unit_at[p] * pitch + p]));
+  }
+  return load_rref(S.data(), w, k);
 }
 
 // np new rows on a state of r diagonal pivots [I_r | X] (all_clean_), as np

@@ -354,3 +354,35 @@ def test_batch_add_matches_row_by_row(seed):
         R = rng.integers(0, 3, (n, k), dtype=np.uint8)
     cuts = sorted(set(rng.integers(1, n + 1, 3).tolist()) | {n})
     _batch_vs_rows(k, np.ascontiguousarray(R), cuts)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_systematic_full_batch_solve(seed):
+    # one batched AddPiece of >= k rows on a fresh decoder, mostly systematic
+    # pieces (any order, some scaled) plus a few coded ones anywhere among
+    # them: DecoderCore solves the small block of coded rows instead of
+    # eliminating row by row (decoder_core.cpp solve_systematic_batch); the
+    # state, counters and T must equal row-by-row AddPiece -- also when the
+    # coded rows are dependent (C singular: the row-by-row route is taken)
+    rng = np.random.default_rng(5500 + seed)
+    k = int(rng.choice([4, 9, 16, 40, 64, 128]))
+    m = int(rng.integers(1, max(2, k // 8) + 1))
+    lost = rng.choice(k, m, replace=False)
+    units = [i for i in range(k) if i not in set(lost.tolist())]
+    if seed % 2:
+        rng.shuffle(units)
+    rows = []
+    for i in units:
+        v = np.zeros(k, np.uint8)
+        v[i] = 1 if rng.random() < 0.85 else rng.integers(2, 256)
+        rows.append(v)
+    coded = rng.integers(0, 256, (m, k), dtype=np.uint8)
+    if seed % 5 == 3 and m >= 2:
+        coded[1] = coded[0]                           # dependent: C singular
+    if seed % 7 == 4:
+        coded[0, lost] = 0                            # zero on every lost column: singular
+    for v in coded:
+        rows.insert(int(rng.integers(0, len(rows) + 1)), v)
+    rows += [rng.integers(0, 256, k, dtype=np.uint8) for _ in range(int(rng.integers(0, 4)))]
+    R = np.ascontiguousarray(np.stack(rows))
+    _batch_vs_rows(k, R, [R.shape[0]])
