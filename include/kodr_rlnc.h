@@ -267,6 +267,35 @@ int rlnc_decoder_apply_stats(const rlnc_decoder* dec, size_t* gf_rows, size_t* c
 int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* dec);
 int rlnc_decoder_transform(const rlnc_decoder* dec, uint8_t* out);
 
+/* ---- progressive decode (an extension) ---------------------- */
+/* kodr's GetPiece before full rank follows decoder_state.go:233-256, whose
+ * test ("every other coefficient non-zero") almost never holds, so a consumer
+ * cannot read pieces early through it.  These read every original piece that
+ * IS decoded: some row of the state is a*e_j on the coefficient side (a
+ * systematic piece on arrival, every piece at full rank).
+ * Data-side policy: LAZY (default) materializes on request; EAGER also
+ * materializes, in every AddPiece call, the pieces that call decoded (on the
+ * context stream, asynchronously), so a later read is a copy.  The state and
+ * kodr's API results are the same under both. */
+#define RLNC_DECODE_LAZY  0
+#define RLNC_DECODE_EAGER 1
+int rlnc_decoder_set_policy(rlnc_decoder* dec, int policy);
+/* mask[j] = 1 for each decoded original piece j (mask: piece_count bytes or
+ * NULL); returns how many are decoded */
+size_t rlnc_decoder_decoded_mask(const rlnc_decoder* dec, uint8_t* mask);
+/* original piece j (L bytes) into out (host, or device when is_device), or
+ * RLNC_ERR_PIECE_NOT_DECODED_YET / RLNC_ERR_PIECE_OUT_OF_BOUND */
+int rlnc_decoder_get_decoded(rlnc_decoder* dec, size_t j, uint8_t* out, int is_device);
+/* Bind a device buffer (piece_count rows at `pitch`, both 16-byte aligned,
+ * pitch >= piece length; AddPiece must have fixed the length) as the home of
+ * the decoded generation: original piece j is materialized straight to
+ * d_out + j * pitch (under EAGER, by the AddPiece call that decoded it, on the
+ * context stream), so a consumer reads it in place once rlnc_decoder_decoded_mask
+ * shows it and the context stream has passed that call.  NULL unbinds.
+ * Binding drops the pieces materialized before it; GetPiece/GetPieces are
+ * unchanged. */
+int rlnc_decoder_bind_output(rlnc_decoder* dec, uint8_t* d_out, size_t pitch);
+
 /* ---- raw kernel entry: Y = A (x) X over GF(2^8) ------------------------ */
 /* Y[m][j] = XOR_k mul(A[m][k], X[k][j]) for m<M, j<ncols.  A is M x K host
  * bytes (row stride lda); X and Y are device rows at pitches ldx/ldy (multiples

@@ -78,6 +78,10 @@ SIGNATURES = {
     "rlnc_decoder_add_piece_device": (_int, [_vp, _u8p, _sz, _vp, _sz]),
     "rlnc_decoder_add_pieces": (_int, [_vp, _vp, _sz, _sz, _sz, _int, _szp]),
     "rlnc_decoder_add_pieces_gpu": (_int, [_vp, _vp, _sz, _sz, _sz, _szp]),
+    "rlnc_decoder_set_policy": (_int, [_vp, _int]),
+    "rlnc_decoder_decoded_mask": (_sz, [_vp, _u8p]),
+    "rlnc_decoder_get_decoded": (_int, [_vp, _sz, _vp, _int]),
+    "rlnc_decoder_bind_output": (_int, [_vp, _vp, _sz]),
     "rlnc_decoders_add_pieces_gpu": (_int, [_vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp]),
     "rlnc_decoder_is_decoded": (_int, [_vp]),
     "rlnc_decoder_required": (_sz, [_vp]),

@@ -18,6 +18,7 @@
 
 #include "../../include/kodr_rlnc.h"
 #include "decoder_core.hpp"
+#include "host_gf.hpp"
 #include "gf_kernels.hpp"
 #include "pool.hpp"
 #include "staging.hpp"
@@ -136,6 +137,18 @@ struct rlnc_decoder {
   DevBuf scratch;              // GF rows before the gather
   size_t last_gf_rows = 0, last_copy_rows = 0;
   bool last_bs = false;         // the last GF product ran on the bit-sliced kernel
+  // progressive decode: original pieces materialized before
+  // GetPieces, in slots of `prog` in the order they were made, or at row j of
+  // the caller's bound output (rlnc_decoder_bind_output)
+  int policy = RLNC_DECODE_LAZY;
+  DevBuf prog;
+  std::vector<int32_t> slot_of;  // per original piece: its slot, or -1
+  size_t nslots = 0;
+  uint8_t* out_ext = nullptr;    // bound output: piece j at out_ext + j * out_pitch
+  size_t out_pitch = 0;
+  std::vector<uint8_t*> hdst;    // per materialized row: its destination
+  std::vector<int32_t> drow;     // DecoderCore::decoded() scratch
+  std::vector<uint8_t> dscale;
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -873,6 +886,7 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   d->rowbuf.release();
   d->scratch.release();
   d->recv_bs.release();
+  d->prog.release();
   delete d;
   return RLNC_OK;
 }
@@ -922,6 +936,8 @@ int dec_check(rlnc_decoder* d, size_t vlen, const uint8_t* piece, size_t plen) {
   return RLNC_OK;
 }
 
+int dec_progress(rlnc_decoder* d, long only);
+
 int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
             bool dev) {
   if (!d) return RLNC_ERR_INVALID_ARGUMENT;
@@ -930,7 +946,9 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   TRY(dec_check(d, vlen, piece, plen));
   TRY(d->core.add(vec));
   d->decoded_ready = false;
-  return dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev);
+  TRY(dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev));
+  if (d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
+  return RLNC_OK;
 }
 
 // bit-sliced twin of the received rows: rows [bs_rows, received) added
@@ -976,7 +994,9 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
 // copied, and only the other m rows go through the GF kernel: m x recv x L
 // MACs instead of rows x recv x L (systematic/decoder.go:96-104
 // leaves this undone).  The bytes are identical either way.
-int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, size_t dpitch) {
+// With hdst (host array of rows destinations), row i goes to hdst[i] instead.
+int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, size_t dpitch,
+              uint8_t* const* hdst = nullptr) {
   const size_t recv = d->core.received();
   hipStream_t st = d->ctx->stream;
   d->hsrc.assign(rows, nullptr);
@@ -992,7 +1012,7 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
   }
   d->last_gf_rows = m;
   d->last_copy_rows = rows - m;
-  if (m == rows || rows > 65535 || dpitch % 16) {  // no unit rows: straight into dst
+  if (!hdst && (m == rows || rows > 65535 || dpitch % 16)) {  // no unit rows: straight into dst
     d->last_gf_rows = rows;
     d->last_copy_rows = 0;
     TRY(d->tmat.reserve(std::max<size_t>(rows * recv, 1)));
@@ -1000,11 +1020,13 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
     return dec_gemm(d, d->tmat.p, rows, dst, dpitch);
   }
   // one upload ahead of both kernels: [the m GF rows of T | the gather's
-  // source-row table].  A small H2D costs ~15-20 us of DMA latency, so a
-  // second one between the kernels would stall the stream.
+  // source-row table | its destination table, if any].  A small H2D costs
+  // ~15-20 us of DMA latency, so a second one between the kernels would stall
+  // the stream.
   const size_t tbytes = (m * recv + 15) / 16 * 16, pbytes = rows * sizeof(uint8_t*);
+  const size_t dbytes = hdst ? pbytes : 0;
   if (m) TRY(d->scratch.reserve(m * d->pitch));
-  d->hTc.resize(tbytes + pbytes);
+  d->hTc.resize(tbytes + pbytes + dbytes);
   for (size_t i = 0, t = 0; i < rows; i++)
     if (!d->hsrc[i]) {
       memcpy(d->hTc.data() + t * recv, trows + i * recv, recv);
@@ -1012,11 +1034,71 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
       t++;
     }
   memcpy(d->hTc.data() + tbytes, d->hsrc.data(), pbytes);
-  TRY(d->tmat.reserve(tbytes + pbytes));
-  HIPC(d->ctx->stage.h2d(d->tmat.p, tbytes + pbytes, d->hTc.data(), tbytes + pbytes, tbytes + pbytes, 1, st));
+  if (hdst) memcpy(d->hTc.data() + tbytes + pbytes, hdst, dbytes);
+  const size_t up = tbytes + pbytes + dbytes;
+  TRY(d->tmat.reserve(up));
+  HIPC(d->ctx->stage.h2d(d->tmat.p, up, d->hTc.data(), up, up, 1, st));
   if (m) TRY(dec_gemm(d, d->tmat.p, m, d->scratch.p, d->pitch));
   HIPC(kodr_amd::gather_rows(reinterpret_cast<const uint8_t* const*>(d->tmat.p + tbytes), dst, dpitch, rows, d->L,
-                             st));
+                             st, hdst ? reinterpret_cast<uint8_t* const*>(d->tmat.p + tbytes + pbytes) : nullptr));
+  return RLNC_OK;
+}
+
+// Materialize decoded original pieces that have no slot yet (all of them
+// when `only` < 0, else just piece `only`) into new slots of d->prog: row
+// T_i * inv(a) of the state row a*e_j, one dec_apply for the lot (systematic
+// pieces are unit rows of T: copies).  Asynchronous on the context stream.
+int dec_progress(rlnc_decoder* d, long only) {
+  const size_t k = d->core.piece_count();
+  if (!d->ctx || !d->have_len) return RLNC_OK;
+  d->core.decoded(&d->drow, &d->dscale);
+  if (d->slot_of.size() != k) d->slot_of.assign(k, -1);
+  const size_t recv = d->core.received();
+  std::vector<size_t> todo;
+  for (size_t j = 0; j < k; j++)
+    if (d->drow[j] >= 0 && d->slot_of[j] < 0 && (only < 0 || (size_t)only == j)) todo.push_back(j);
+  if (todo.empty()) return RLNC_OK;
+  if (d->out_ext) {  // straight into the caller's generation buffer, row j
+    const kodr_amd::hostgf::Tables& t = kodr_amd::hostgf::T();
+    for (size_t q0 = 0; q0 < todo.size(); q0 += 32768) {
+      const size_t nq = std::min<size_t>(todo.size() - q0, 32768);
+      std::vector<uint8_t> hT(nq * recv);
+      d->hdst.resize(nq);
+      for (size_t q = 0; q < nq; q++) {
+        const size_t j = todo[q0 + q];
+        const uint8_t* tr = d->core.t_row((size_t)d->drow[j]);
+        const uint8_t a = d->dscale[j];
+        for (size_t c = 0; c < recv; c++) hT[q * recv + c] = a == 1 ? tr[c] : t.mul(tr[c], t.inv(a));
+        d->hdst[q] = d->out_ext + j * d->out_pitch;
+      }
+      TRY(dec_apply(d, nq, hT.data(), nullptr, 0, d->hdst.data()));
+      for (size_t q = 0; q < nq; q++) d->slot_of[todo[q0 + q]] = (int32_t)todo[q0 + q];
+    }
+    return RLNC_OK;
+  }
+  if (d->prog.cap < k * d->pitch) {
+    if (d->nslots) {  // keep the slots made so far
+      DevBuf nb;
+      nb.bind(d->ctx->device, d->ctx->stream);
+      TRY(nb.reserve(k * d->pitch));
+      HIPC(hipMemcpyAsync(nb.p, d->prog.p, d->nslots * d->pitch, hipMemcpyDeviceToDevice, d->ctx->stream));
+      d->prog.release();
+      d->prog = nb;
+    } else {
+      TRY(d->prog.reserve(k * d->pitch));
+    }
+  }
+  const kodr_amd::hostgf::Tables& t = kodr_amd::hostgf::T();
+  std::vector<uint8_t> hT(todo.size() * recv);
+  for (size_t q = 0; q < todo.size(); q++) {
+    const size_t j = todo[q];
+    const uint8_t* tr = d->core.t_row((size_t)d->drow[j]);
+    const uint8_t a = d->dscale[j];
+    for (size_t c = 0; c < recv; c++) hT[q * recv + c] = a == 1 ? tr[c] : t.mul(tr[c], t.inv(a));
+  }
+  TRY(dec_apply(d, todo.size(), hT.data(), d->prog.p + d->nslots * d->pitch, d->pitch));
+  for (size_t q = 0; q < todo.size(); q++) d->slot_of[todo[q]] = (int32_t)(d->nslots + q);
+  d->nslots += todo.size();
   return RLNC_OK;
 }
 
@@ -1140,6 +1222,7 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   size_t n = 0;
   const int st = d->core.add_many(vecs, vpitch, count, &n);
   TRY(dec_batch_post(d, rows, pitch, dev, bc, n));
+  if (n && d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
   *consumed = n;
   return st;
 }
@@ -1247,7 +1330,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
           n += m;
         }
       }
-      const int pst = dec_batch_post(d, rows[g], pitch, true, bcs[g], n);
+      int pst = dec_batch_post(d, rows[g], pitch, true, bcs[g], n);
+      if (pst == RLNC_OK && n && d->policy == RLNC_DECODE_EAGER) pst = dec_progress(d, -1);
       consumed[g] = n;
       status[g] = pst != RLNC_OK ? pst : st;
     }
@@ -1338,6 +1422,72 @@ int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {
 int rlnc_decoder_transform(const rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
   d->core.copy_transform(out, d->core.received());
+  return RLNC_OK;
+}
+
+int rlnc_decoder_bind_output(rlnc_decoder* d, uint8_t* d_out, size_t pitch) {
+  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  if (d_out && (!d->ctx || !d->have_len || pitch < d->L || pitch % 16 || (uintptr_t)d_out % 16))
+    return RLNC_ERR_INVALID_ARGUMENT;
+  d->out_ext = d_out;
+  d->out_pitch = d_out ? pitch : 0;
+  d->slot_of.assign(d->core.piece_count(), -1);  // slots made so far are dropped
+  d->nslots = 0;
+  if (d_out && d->policy == RLNC_DECODE_EAGER) {
+    TRY(set_dev(d->ctx));
+    TRY(dec_progress(d, -1));  // what is decoded already
+  }
+  return RLNC_OK;
+}
+
+int rlnc_decoder_set_policy(rlnc_decoder* d, int policy) {
+  if (!d || (policy != RLNC_DECODE_LAZY && policy != RLNC_DECODE_EAGER)) return RLNC_ERR_INVALID_ARGUMENT;
+  d->policy = policy;
+  if (policy == RLNC_DECODE_EAGER && d->ctx && d->have_len) {
+    TRY(set_dev(d->ctx));
+    TRY(dec_progress(d, -1));  // what is decoded already
+  }
+  return RLNC_OK;
+}
+
+size_t rlnc_decoder_decoded_mask(const rlnc_decoder* d, uint8_t* mask) {
+  if (!d) return 0;
+  std::vector<int32_t> row;
+  std::vector<uint8_t> sc;
+  const size_t n = d->core.decoded(&row, &sc);
+  if (mask)
+    for (size_t j = 0; j < row.size(); j++) mask[j] = row[j] >= 0 ? 1 : 0;
+  return n;
+}
+
+int rlnc_decoder_get_decoded(rlnc_decoder* d, size_t j, uint8_t* out, int is_device) {
+  if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  if (j >= d->core.piece_count()) return RLNC_ERR_PIECE_OUT_OF_BOUND;
+  std::vector<int32_t> row;
+  std::vector<uint8_t> sc;
+  d->core.decoded(&row, &sc);
+  if (row[j] < 0) return RLNC_ERR_PIECE_NOT_DECODED_YET;
+  if (!d->ctx) return RLNC_ERR_NO_DEVICE;
+  TRY(set_dev(d->ctx));
+  hipStream_t st = d->ctx->stream;
+  const uint8_t* src = nullptr;
+  auto slot = [d](size_t j) -> const uint8_t* {
+    return d->out_ext ? d->out_ext + j * d->out_pitch : d->prog.p + (size_t)d->slot_of[j] * d->pitch;
+  };
+  if (d->slot_of.size() == d->core.piece_count() && d->slot_of[j] >= 0) {
+    src = slot(j);
+  } else if (d->decoded_ready && sc[j] == 1 && !d->out_ext) {  // GetPieces' rows: row i of the state is piece j
+    src = d->decoded.p + (size_t)row[j] * d->pitch;
+  } else {
+    TRY(dec_progress(d, (long)j));
+    src = slot(j);
+  }
+  if (is_device) {
+    if (out != src) HIPC(hipMemcpyAsync(out, src, d->L, hipMemcpyDeviceToDevice, st));
+    return RLNC_OK;
+  }
+  HIPC(d->ctx->stage.d2h(out, d->L, src, d->pitch, d->L, 1, st));
+  HIPC(hipStreamSynchronize(st));
   return RLNC_OK;
 }
 

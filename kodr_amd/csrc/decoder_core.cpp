@@ -618,6 +618,20 @@ bool DecoderCore::load_rref(const uint8_t* state, size_t pitch, size_t c) {
   return true;
 }
 
+size_t DecoderCore::decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const {
+  row_of->assign(k_, -1);
+  scale->assign(k_, 0);
+  size_t n = 0;
+  for (size_t i = 0; i < rows_.size(); i++) {
+    const int32_t p = up_[i] >= 0 ? up_[i] : unit_col(rows_[i], k_);
+    if (p < 0 || (*row_of)[p] >= 0) continue;
+    (*row_of)[p] = (int32_t)i;
+    (*scale)[p] = rows_[i][p];
+    n++;
+  }
+  return n;
+}
+
 int DecoderCore::piece_available(size_t idx) const {
   if (idx >= k_) return 12;                         // :222-224 ErrPieceOutOfBound
   if (idx >= rows_.size()) return 11;               // :225-227 ErrPieceNotDecodedYet

@@ -53,6 +53,11 @@ class DecoderCore {
   // idx of the coded matrix may be returned, else kodr's error code.
   int piece_available(size_t idx) const;
 
+  // original pieces decoded now: for each row whose coefficient half is a*e_j,
+  // row_of[j] = that row and scale[j] = a (row_of[j] = -1 otherwise);
+  // returns the count
+  size_t decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const;
+
   const uint8_t* coeff_row(size_t i) const { return rows_[i]; }
   const uint8_t* t_row(size_t i) const { return rows_[i] + k_; }
   // copy T (rank x received) densely into out (row stride = received)

@@ -325,17 +325,20 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
   return hipGetLastError();
 }
 
-// dst row r = bytes [0, ncols) of the device row src[r] (16-byte aligned rows).
-// Used where a row of the product is a plain copy: unit rows of the decode
-// transform (systematic pieces) and gathers of GEMM scratch rows.
+// dst row r = bytes [0, ncols) of the device row src[r] (16-byte aligned rows);
+// dst row r is dtab[r] when a destination table is given (a scatter into the
+// caller's generation buffer), else dst + r * dpitch.  Used where a row of the
+// product is a plain copy: unit rows of the decode transform (systematic
+// pieces) and gathers of GEMM scratch rows.
 __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* const* __restrict__ src,
+                                                         uint8_t* const* __restrict__ dtab,
                                                          uint8_t* __restrict__ dst, size_t dpitch,
                                                          int ncols) {
   const int r = blockIdx.y;
   const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
   if (c >= ncols) return;
   const uint8_t* s = src[r] + c;
-  uint8_t* d = dst + (size_t)r * dpitch + c;
+  uint8_t* d = (dtab ? dtab[r] : dst + (size_t)r * dpitch) + c;
   if (c + kLaneBytes <= ncols) {
     *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
   } else {
@@ -425,12 +428,12 @@ hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpi
 }
 
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
-                       hipStream_t stream) {
+                       hipStream_t stream, uint8_t* const* d_dst) {
   if (!rows || !ncols) return hipSuccess;
   if (rows > 65535) return hipErrorInvalidValue;
   const unsigned gx = (unsigned)((ncols + 256 * kLaneBytes - 1) / (256 * kLaneBytes));
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, d_src, dY, ldy,
-                     (int)ncols);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(gx, (unsigned)rows), dim3(256), 0, stream, d_src, d_dst, dY,
+                     ldy, (int)ncols);
   return hipGetLastError();
 }
 

@@ -60,8 +60,10 @@ hipError_t download_small(const uint8_t* src, size_t spitch, uint8_t* dst_mapped
 hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows, size_t ncols,
                      hipStream_t stream);
 
+// dst row r = device row d_src[r] (16-byte aligned); written at d_dst[r] when
+// d_dst (a device table) is given, else at dY + r * ldy.  rows <= 65535.
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
-                       hipStream_t stream);
+                       hipStream_t stream, uint8_t* const* d_dst = nullptr);
 
 // rows x k coding vectors at row pitch ldv: rows [0, n_sys) = e_(sys_first+r),
 // the rest counter-based pseudo-random bytes of (seed, row0 + r).  rows <= 65535.
