@@ -2,6 +2,7 @@
 // kodr_internals/matrix/decoder_state.go unless stated otherwise.
 #include "decoder_core.hpp"
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -148,7 +149,7 @@ int DecoderCore::add(const uint8_t* vec) {
 }
 
 int DecoderCore::add_many(const uint8_t* vecs, size_t pitch, size_t n, size_t* used) {
-  if (received_ == 0 && n >= k_ && solve_systematic_batch(vecs, pitch)) {
+  if (received_ == 0 && n >= k_ && (solve_systematic_batch(vecs, pitch) || solve_full_batch(vecs, pitch))) {
     *used = k_;
     return n > k_ ? 3 : 0;  // full/decoder.go:52-54 for the rows past k
   }
@@ -283,6 +284,129 @@ bool DecoderCore::solve_systematic_batch(const uint8_t* vecs, size_t pitch) {
         row[k + unit_at[p]] = t.mul(wrow[p], t.inv(vecs[(size_t)unit_at[p] * pitch + p]));
   }
   return load_rref(S.data(), w, k);
+}
+
+// ---- full batches: [C | I] -> [I | C^-1] by blocked Gauss-Jordan ----------
+// Same premise as solve_systematic_batch: a fresh decoder handed k or more
+// rows whose first k vectors C are independent ends in [I | C^-1], whatever
+// route kodr's passes take, so any exact inversion gives kodr's state byte for
+// byte.  The inversion runs on [C | I] in the decoder's own row slots, in
+// panels of kFullNB columns:
+//  A: pick kFullNB rows whose panel block is invertible -- rows that are no
+//     pivot yet, in index order, each reduced against the rows picked so far
+//     (Gauss-Jordan on [panel | tracking] vectors, so the tracking half ends
+//     as S, the inverse of the picked rows' panel block);
+//  B: per 64-byte column chunk, right to left (the panel's own chunk last, so
+//     every row's panel bytes are still the multipliers Q): the new pivot
+//     rows S x (picked rows), and every other row ^= Q[row] x (new pivot rows).
+// Columns left of the panel never change (zero in every picked row), and T
+// column t stays zero in every row until row t is picked (each unpicked row's
+// own identity entry aside), so a row's bytes in play are [jb, k + tmax).  A
+// panel with too few independent rows means C is singular: nothing is kept
+// and add_many takes kodr's route.  One thread: the matrix is ~160 KB, and a
+// spin-barrier thread pool splitting its 64-byte column chunks over cores
+// (measured on the box: 2 threads 365 us, 8 threads 456 us, against 88 us on
+// one) moved more cache lines between cores per panel than it saved.
+namespace {
+
+constexpr int kFullNB = 16;
+// Below this the 4-row panels of add_panel are faster on the box's EPYC
+// (tools/full_solve_time.sh: k = 192 route 40 us vs 48 blocked; k = 256 103 vs 94).
+constexpr size_t kFullMinK = 224;
+
+struct FullSolve {
+  size_t k = 0;
+  std::vector<uint8_t*> rows;           // physical rows, [C | I] at start
+  std::vector<int16_t> cur;             // per row: panel column it pivots in this block, or -1
+  std::vector<uint8_t> used;            // per row: a pivot already (this or an earlier block)
+  std::vector<int32_t> pivrow;          // per column: its pivot row
+  uint8_t S[kFullNB][kFullNB];          // S[q][t]: new pivot row q = sum_t S[q][t] * picked row t
+  int32_t brow[kFullNB];                // picked rows
+  int bpiv[kFullNB];                    // panel column of picked row q
+  int nb = 0;
+  size_t tmax = 0;                      // T columns [0, tmax) can be non-zero in a row not picked yet
+
+  bool phase_a(size_t jb) {
+    const hostgf::Tables& t = T();
+    for (int q = 0; q < nb; q++) cur[brow[q]] = -1;  // the previous block's pivots
+    nb = (int)std::min<size_t>(kFullNB, k - jb);
+    alignas(64) uint8_t bas[kFullNB][2 * kFullNB];
+    int nbas = 0;
+    for (size_t i = 0; i < k && nbas < nb; i++) {
+      if (used[i]) continue;
+      alignas(64) uint8_t v[2 * kFullNB] = {0};
+      memcpy(v, rows[i] + jb, nb);
+      v[kFullNB + nbas] = 1;
+      for (int q = 0; q < nbas; q++)
+        if (const uint8_t c = v[bpiv[q]]) hostgf::axpy32(v, bas[q], c);
+      int pc = -1;
+      for (int c = 0; c < nb && pc < 0; c++)
+        if (v[c]) pc = c;
+      if (pc < 0) continue;  // dependent on the rows picked so far in this panel
+      if (v[pc] != 1) hostgf::scale32(v, t.inv(v[pc]));
+      for (int q = 0; q < nbas; q++)
+        if (const uint8_t c = bas[q][pc]) hostgf::axpy32(bas[q], v, c);
+      memcpy(bas[nbas], v, sizeof(v));
+      bpiv[nbas] = pc;
+      brow[nbas] = (int32_t)i;
+      nbas++;
+    }
+    if (nbas < nb) return false;
+    for (int q = 0; q < nb; q++) {
+      memcpy(S[q], bas[q] + kFullNB, kFullNB);
+      cur[brow[q]] = (int16_t)bpiv[q];
+      used[brow[q]] = 1;
+      tmax = std::max<size_t>(tmax, (size_t)brow[q] + 1);
+      pivrow[jb + bpiv[q]] = brow[q];
+    }
+    return true;
+  }
+
+  void phase_b(size_t jb) {
+    const size_t end = k + tmax, nch = (end - jb + 63) / 64;
+    for (size_t ch = nch; ch-- > 0;) {
+      const size_t o = jb + ch * 64, w = std::min<size_t>(64, end - o);
+      hostgf::panel_update<kFullNB>(rows.data(), k, o, w, jb, brow, bpiv, S, nb, cur.data());
+    }
+  }
+};
+
+}  // namespace
+
+bool DecoderCore::solve_full_batch(const uint8_t* vecs, size_t pitch) {
+  const size_t k = k_;
+  static const bool enabled = !getenv("KODR_FULL_SOLVE") || atoi(getenv("KODR_FULL_SOLVE")) != 0;
+  if (!enabled || received_ != 0 || k < kFullMinK || !hostgf::have_gfni512()) return false;
+  ensure_tcap(k);
+  FullSolve F;
+  F.k = k;
+  F.rows.resize(k);
+  for (size_t i = 0; i < k; i++) {
+    uint8_t* r = free_[free_.size() - 1 - i];
+    memcpy(r, vecs + i * pitch, k);
+    memset(r + k, 0, tcap_);
+    r[k + i] = 1;
+    F.rows[i] = r;
+  }
+  F.cur.assign(k, -1);
+  F.used.assign(k, 0);
+  F.pivrow.assign(k, -1);
+  for (size_t jb = 0; jb < k; jb += kFullNB) {
+    if (!F.phase_a(jb)) return false;  // C singular; the slots are still free: nothing changed
+    F.phase_b(jb);
+  }
+  for (size_t c = 0; c < k; c++)
+    if (F.rows[F.pivrow[c]][c] != 1) return false;  // cannot happen: refuse rather than load a wrong state
+  free_.resize(free_.size() - k);
+  for (size_t c = 0; c < k; c++) {
+    push_row(F.rows[F.pivrow[c]], -1, 0);
+    clean_[c] = 1;
+    touched_[c] = 0;
+  }
+  received_ = k;
+  useful_ = k;
+  all_clean_ = true;
+  return true;
 }
 
 // np new rows on a state of r diagonal pivots [I_r | X] (all_clean_), as np

@@ -70,6 +70,7 @@ class DecoderCore {
   size_t add_panel(const uint8_t* vecs, size_t pitch, size_t np);
   bool append_unit(const uint8_t* vec);
   bool solve_systematic_batch(const uint8_t* vecs, size_t pitch);
+  bool solve_full_batch(const uint8_t* vecs, size_t pitch);
   void update_clean();
   void ensure_tcap(size_t need);
   void axpy_row(size_t dst, size_t src, uint8_t q, size_t from);

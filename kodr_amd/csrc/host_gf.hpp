@@ -291,6 +291,64 @@ __attribute__((target("avx512f,avx512bw,gfni"))) inline void rank_multi_gfni512(
     }
   }
 }
+
+// 32-byte vectors (the panel pivot search of solve_full_batch)
+__attribute__((target("avx2,gfni"))) inline void axpy32(uint8_t* dst, const uint8_t* src, uint8_t q) {
+  const __m256i A = _mm256_set1_epi64x((long long)T().affine[q]);
+  const __m256i x = _mm256_loadu_si256((const __m256i*)src);
+  _mm256_storeu_si256((__m256i*)dst, _mm256_xor_si256(_mm256_loadu_si256((const __m256i*)dst),
+                                                      _mm256_gf2p8affine_epi64_epi8(x, A, 0)));
+}
+__attribute__((target("avx2,gfni"))) inline void scale32(uint8_t* v, uint8_t q) {
+  const __m256i A = _mm256_set1_epi64x((long long)T().affine[q]);
+  _mm256_storeu_si256((__m256i*)v, _mm256_gf2p8affine_epi64_epi8(_mm256_loadu_si256((const __m256i*)v), A, 0));
+}
+
+// One 64-byte column chunk [o, o + w) of a blocked Gauss-Jordan step
+// (decoder_core.cpp, solve_full_batch): the nb picked rows brow[q] become
+// N[bpiv[q]] = sum_u S[q][u] * (picked row u), and every row i that is not
+// picked (cur[i] < 0) gets row_i ^= sum_c row_i[jb + c] * N[c] (the panel
+// bytes at jb are read here, so the caller updates the chunk holding them
+// last).  N stays in registers; the multiply-by-q matrices are broadcast
+// from the table.
+template <int NB>
+__attribute__((target("avx512f,avx512bw,gfni"))) inline void panel_update(
+    uint8_t* const* rows, size_t k, size_t o, size_t w, size_t jb, const int32_t* brow, const int* bpiv,
+    const uint8_t (*S)[NB], int nb, const int16_t* cur) {
+  const Tables& t = T();
+  const __mmask64 km = (__mmask64)(~0ULL >> (64 - w));
+  __m512i P[NB];
+  alignas(64) __m512i Nm[NB];
+  for (int q = 0; q < nb; q++) P[q] = _mm512_maskz_loadu_epi8(km, rows[brow[q]] + o);
+  for (int c = 0; c < NB; c++) Nm[c] = _mm512_setzero_si512();
+  for (int q = 0; q < nb; q++) {
+    __m512i acc = _mm512_setzero_si512();
+    for (int u = 0; u < nb; u++)
+      if (S[q][u])
+        acc = _mm512_xor_si512(acc, _mm512_gf2p8affine_epi64_epi8(P[u], _mm512_set1_epi64((long long)t.affine[S[q][u]]), 0));
+    Nm[bpiv[q]] = acc;
+  }
+  __m512i N[NB];
+#pragma GCC unroll 16
+  for (int c = 0; c < NB; c++) N[c] = Nm[c];
+  const uint64_t* aff = t.affine;
+  for (size_t i = 0; i < k; i++) {
+    if (cur[i] >= 0) continue;
+    uint8_t* row = rows[i];
+    const uint8_t* qi = row + jb;
+    uint8_t* dst = row + o;
+    __m512i d0 = _mm512_maskz_loadu_epi8(km, dst), d1 = _mm512_setzero_si512();
+#pragma GCC unroll 16
+    for (int c = 0; c < NB; c += 2) {
+      const __m512i a0 = _mm512_gf2p8affine_epi64_epi8(N[c], _mm512_set1_epi64((long long)aff[qi[c]]), 0);
+      const __m512i a1 = _mm512_gf2p8affine_epi64_epi8(N[c + 1], _mm512_set1_epi64((long long)aff[qi[c + 1]]), 0);
+      if (c & 2) d1 = _mm512_ternarylogic_epi64(d1, a0, a1, 0x96);
+      else d0 = _mm512_ternarylogic_epi64(d0, a0, a1, 0x96);
+    }
+    _mm512_mask_storeu_epi8(dst, km, _mm512_xor_si512(d0, d1));
+  }
+  for (int q = 0; q < nb; q++) _mm512_mask_storeu_epi8(rows[brow[q]] + o, km, Nm[bpiv[q]]);
+}
 #endif
 
 // dst[0..n) ^= q * src[0..n)

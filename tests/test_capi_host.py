@@ -386,3 +386,31 @@ def test_systematic_full_batch_solve(seed):
     rows += [rng.integers(0, 256, k, dtype=np.uint8) for _ in range(int(rng.integers(0, 4)))]
     R = np.ascontiguousarray(np.stack(rows))
     _batch_vs_rows(k, R, [R.shape[0]])
+
+
+@pytest.mark.parametrize("seed", range(36))
+def test_full_batch_solve(seed):
+    # one batched AddPiece of >= k coded rows on a fresh decoder (k >= 224):
+    # DecoderCore inverts the first k vectors by blocked Gauss-Jordan
+    # (decoder_core.cpp solve_full_batch) instead of taking kodr's route; the
+    # state, counters and T must equal row-by-row AddPiece -- for dense rows,
+    # {0,1,2}-valued rows (zero diagonals, panels whose first candidate rows are
+    # dependent), and singular batches (duplicates, low rank: kodr's route)
+    rng = np.random.default_rng(6100 + seed)
+    k = int(rng.choice([224, 231, 256]))
+    n = k + int(rng.integers(0, 4))
+    kind = seed % 6
+    if kind in (0, 1):
+        R = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    elif kind == 2:
+        R = rng.integers(0, 3, (n, k), dtype=np.uint8)
+    elif kind == 3:  # panel-local dependence: rows 0..16 agree on the first 16 columns up to scale
+        R = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        R[1:17, :16] = oracle.matmul(rng.integers(0, 256, (16, 1), dtype=np.uint8), R[:1, :16])[1]
+    elif kind == 4:  # singular: a duplicate among the first k
+        R = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        R[int(rng.integers(1, k))] = R[0]
+    else:  # singular: rank k - 3
+        B = rng.integers(0, 256, (k - 3, k), dtype=np.uint8)
+        R = oracle.matmul(rng.integers(0, 256, (n, k - 3), dtype=np.uint8), B)[1]
+    _batch_vs_rows(k, np.ascontiguousarray(R), [n])
