@@ -168,6 +168,15 @@ int rlnc_encoder_seed(rlnc_encoder* enc, uint64_t seed);
  * of >= 9 coded pieces read, so that cost is paid once up front instead of by
  * the first large batch.  Optional; idempotent.  Async on the ctx stream. */
 int rlnc_encoder_prepare(rlnc_encoder* enc);
+/* Compact residency (no kodr counterpart): keep only the bit-sliced copy of
+ * the generation and release the plain rows -- half the HBM per resident
+ * generation.  Every product then runs on the bit-sliced kernel (batches of
+ * fewer than 9 pieces are slower than on the plain rows: DESIGN.md),
+ * systematic pieces are converted back per call, rlnc_encoder_device_pieces
+ * returns NULL and grouped launches take one launch per generation.
+ * Idempotent; synchronizes the ctx stream.  RLNC_ERR_INVALID_ARGUMENT when
+ * the bit-sliced path is unavailable for this shape or device. */
+int rlnc_encoder_compact(rlnc_encoder* enc);
 /* Many generations in one launch: coded pieces for each of n_enc resident
  * generations (full/encoder.go:61-71 once per generation), all encoders on one
  * ctx with equal piece count k and piece size L.  d_vectors: n_enc blocks of
@@ -192,6 +201,8 @@ int rlnc_recoder_destroy(rlnc_recoder* rec);
 /* as rlnc_encoder_prepare: build the held rows' bit-sliced twin up front
  * (NewFullRLNCRecoder*, full/recoder.go:52-70).  Optional; async. */
 int rlnc_recoder_prepare(rlnc_recoder* rec);
+/* as rlnc_encoder_compact, for the held coded pieces */
+int rlnc_recoder_compact(rlnc_recoder* rec);
 size_t rlnc_recoder_piece_count(const rlnc_recoder* rec);        /* n held coded pieces */
 size_t rlnc_recoder_coded_piece_len(const rlnc_recoder* rec);    /* k + L */
 /* `count` CodedPiece() calls (full/recoder.go:27-46): r = count x n caller

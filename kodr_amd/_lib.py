@@ -63,11 +63,13 @@ SIGNATURES = {
     "rlnc_encoder_coded_wire_device": (_int, [_vp, _sz, _vp, _sz]),
     "rlnc_encoder_seed": (_int, [_vp, ctypes.c_uint64]),
     "rlnc_encoder_prepare": (_int, [_vp]),
+    "rlnc_encoder_compact": (_int, [_vp]),
     "rlnc_encoder_group_coded_pieces_device": (_int, [_vpp, _sz, _vp, _sz, _vp, _sz]),
     "rlnc_recoder_create": (_int, [_vp, _u8p, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_create_device": (_int, [_vp, _vp, _sz, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_destroy": (_int, [_vp]),
     "rlnc_recoder_prepare": (_int, [_vp]),
+    "rlnc_recoder_compact": (_int, [_vp]),
     "rlnc_recoder_piece_count": (_sz, [_vp]),
     "rlnc_recoder_coded_piece_len": (_sz, [_vp]),
     "rlnc_recoder_coded_pieces": (_int, [_vp, _u8p, _sz, _u8p]),

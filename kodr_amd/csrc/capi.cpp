@@ -105,6 +105,7 @@ struct rlnc_encoder {
   DevBuf pieces;             // k x pitch, zero padded
   DevBuf pieces_bs;          // bit-sliced twin of pieces, built on first large batch
   bool bs_valid = false;
+  bool compact = false;      // rlnc_encoder_compact: only the twin is resident
   DevBuf vecs, out;          // staging for host-pointer calls
 };
 
@@ -114,6 +115,7 @@ struct rlnc_recoder {
   DevBuf flat;               // n x pitch wire rows
   DevBuf flat_bs;            // bit-sliced twin, built on first large batch
   bool bs_valid = false;
+  bool compact = false;      // rlnc_recoder_compact: only the twin is resident
   DevBuf r, out;
 };
 
@@ -292,11 +294,40 @@ bool resident_uses_bs(rlnc_ctx* ctx, size_t M, size_t K, size_t ldx, size_t ncol
 
 // Y = A (x) X for a resident, immutable X: small M through gf_gemm on the
 // plain rows, larger M through gf_gemm_bs on a bit-sliced twin built once.
+// A compact X (plain == nullptr: only the twin is resident) takes gf_gemm_bs
+// for every M.
 int gemm_resident(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* plain,
                   DevBuf& twin, bool& twin_valid, size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+  if (!plain) return gemm_bs(ctx, dA, lda, M, K, twin.p, ldx, dY, ldy, ncols);
   if (!resident_uses_bs(ctx, M, K, ldx, ncols)) return gemm(ctx, dA, lda, M, K, plain, ldx, dY, ldy, ncols);
   TRY(build_twin(ctx, plain, twin, twin_valid, K, ldx, ncols));
   return gemm_bs(ctx, dA, lda, M, K, twin.p, ldx, dY, ldy, ncols);
+}
+
+// Keep only the bit-sliced twin of a resident X (K rows at pitch ldx): half
+// the HBM per generation.  Needs the bit-sliced path on this device.
+int compact_resident(rlnc_ctx* ctx, DevBuf& plain, DevBuf& twin, bool& twin_valid, bool& compact, size_t K,
+                     size_t ldx, size_t ncols) {
+  if (compact) return RLNC_OK;
+  if ((ldx % 32) || !kodr_amd::bs_ready(ctx->device) || !bs_chunk_rows(1, std::max<size_t>(K, 1), ldx, ncols)) {
+    g_last_error = "compact residency needs the bit-sliced kernel for this shape";
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  TRY(build_twin(ctx, plain.p, twin, twin_valid, K, ldx, ncols));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  plain.release();
+  compact = true;
+  return RLNC_OK;
+}
+
+// plain rows [r0, r0 + n) of a compact X into dst (pitch dpitch, device):
+// the bit-sliced layout is its own inverse
+int uncompact_rows(rlnc_ctx* ctx, const DevBuf& twin, size_t ldx, size_t r0, size_t n, size_t ncols, DevBuf& scratch,
+                   uint8_t* dst, size_t dpitch) {
+  TRY(scratch.reserve(n * ldx));
+  HIPC(kodr_amd::bitslice_rows(twin.p + r0 * ldx, scratch.p, ldx, n, ncols, ctx->stream));
+  HIPC(hipMemcpy2DAsync(dst, dpitch, scratch.p, ldx, ncols, n, hipMemcpyDeviceToDevice, ctx->stream));
+  return RLNC_OK;
 }
 
 int encoder_alloc(rlnc_ctx* ctx, int kind, size_t k, size_t L, rlnc_encoder** out) {
@@ -613,7 +644,7 @@ size_t rlnc_encoder_decodable_len(const rlnc_encoder* e) { return e ? e->k * (e-
 size_t rlnc_encoder_coded_piece_len(const rlnc_encoder* e) { return e ? e->k + e->L : 0; }
 size_t rlnc_encoder_padding(const rlnc_encoder* e) { return e ? e->padding : 0; }
 const uint8_t* rlnc_encoder_device_pieces(const rlnc_encoder* e, size_t* pitch) {
-  if (!e) return nullptr;
+  if (!e || e->compact) return nullptr;
   if (pitch) *pitch = e->pitch;
   return e->pieces.p;
 }
@@ -637,7 +668,14 @@ int rlnc_encoder_coded_pieces(rlnc_encoder* e, uint8_t* vectors, size_t count, u
       memcpy(out + r * clen, vectors + r * k, k);
     }
     // consecutive piece ids: one strided copy of rows id0 .. id0+n-1
-    HIPC(e->ctx->stage.d2h(out + k, clen, e->pieces.p + id0 * e->pitch, e->pitch, L, n, st));
+    const uint8_t* src = e->pieces.p + id0 * e->pitch;
+    if (e->compact) {
+      TRY(e->out.reserve(n * e->pitch));
+      TRY(e->vecs.reserve(n * e->pitch));
+      TRY(uncompact_rows(e->ctx, e->pieces_bs, e->pitch, id0, n, L, e->vecs, e->out.p, e->pitch));
+      src = e->out.p;
+    }
+    HIPC(e->ctx->stage.d2h(out + k, clen, src, e->pitch, L, n, st));
     e->sys_next += n;
     i = n;
   }
@@ -670,8 +708,14 @@ int rlnc_encoder_prepare(rlnc_encoder* e) {
   if (!e) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(e->ctx));
   // any batch of >= kBsMinRows pieces that takes the bit-sliced kernel reads the twin
-  if (!resident_uses_bs(e->ctx, std::max<size_t>(e->k, 64), e->k, e->pitch, e->L)) return RLNC_OK;
+  if (e->compact || !resident_uses_bs(e->ctx, std::max<size_t>(e->k, 64), e->k, e->pitch, e->L)) return RLNC_OK;
   return build_twin(e->ctx, e->pieces.p, e->pieces_bs, e->bs_valid, e->k, e->pitch, e->L);
+}
+
+int rlnc_encoder_compact(rlnc_encoder* e) {
+  if (!e) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(e->ctx));
+  return compact_resident(e->ctx, e->pieces, e->pieces_bs, e->bs_valid, e->compact, e->k, e->pitch, e->L);
 }
 
 int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
@@ -688,8 +732,9 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
   const size_t vstride = count * k, ostride = count * out_pitch;
   // one launch streams up to kGemmGroupMax generations where the product runs on
   // gf_gemm in one row chunk; otherwise one product per generation
-  const bool grouped = !resident_uses_bs(ctx, count, k, e0->pitch, L) && k * e0->pitch < kMaxDescBytes &&
-                       (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
+  bool grouped = !resident_uses_bs(ctx, count, k, e0->pitch, L) && k * e0->pitch < kMaxDescBytes &&
+                 (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
+  for (size_t i = 0; i < n_enc && grouped; i++) grouped = !encs[i]->compact;  // the grouped launch reads plain rows
   if (!grouped) {
     for (size_t i = 0; i < n_enc; i++)
       TRY(rlnc_encoder_coded_pieces_device(encs[i], d_vectors + i * vstride, count, d_out + i * ostride, out_pitch));
@@ -726,7 +771,9 @@ int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wir
   HIPC(kodr_amd::fill_vectors(d_wire, wire_pitch, count, k, e->seed, e->drawn, n_sys, e->sys_next, st));
   // the systematic pieces are the pieces themselves (e_id x P = P_id): one
   // strided copy of rows sys_next.., no GF product
-  if (n_sys)
+  if (n_sys && e->compact)
+    TRY(uncompact_rows(e->ctx, e->pieces_bs, e->pitch, e->sys_next, n_sys, L, e->out, d_wire + k, wire_pitch));
+  else if (n_sys)
     HIPC(hipMemcpy2DAsync(d_wire + k, wire_pitch, e->pieces.p + e->sys_next * e->pitch, e->pitch, L, n_sys,
                           hipMemcpyDeviceToDevice, st));
   // the coded rows' vectors are read in place as the coefficient matrix
@@ -814,8 +861,14 @@ int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t n, s
 int rlnc_recoder_prepare(rlnc_recoder* r) {
   if (!r) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(r->ctx));
-  if (!resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->pitch, r->clen)) return RLNC_OK;
+  if (r->compact || !resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->pitch, r->clen)) return RLNC_OK;
   return build_twin(r->ctx, r->flat.p, r->flat_bs, r->bs_valid, r->n, r->pitch, r->clen);
+}
+
+int rlnc_recoder_compact(rlnc_recoder* r) {
+  if (!r) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(r->ctx));
+  return compact_resident(r->ctx, r->flat, r->flat_bs, r->bs_valid, r->compact, r->n, r->pitch, r->clen);
 }
 
 int rlnc_recoder_destroy(rlnc_recoder* r) {
