@@ -179,6 +179,9 @@ class EncoderBase {
   size_t DecodableLen() const { return rlnc_encoder_decodable_len(h_); }
   size_t CodedPieceLen() const { return rlnc_encoder_coded_piece_len(h_); }
   size_t Padding() const { return rlnc_encoder_padding(h_); }
+  // extension (no kodr counterpart): keep only the bit-sliced copy of the
+  // generation in HBM (rlnc_encoder_compact)
+  Err Compact() { return check(rlnc_encoder_compact(h_)); }
   kodr_internals::CodedPiece CodedPiece() {
     if (queue_.empty()) refill();
     kodr_internals::CodedPiece p = std::move(queue_.front());
@@ -260,6 +263,26 @@ class DecoderBase {  // full/decoder.go == systematic/decoder.go
   }
   rlnc_decoder* handle() const { return h_; }
 
+  // Extensions (no kodr counterpart): pieces decoded before full
+  // rank.  SetEager(true): AddPiece materializes what it decoded.
+  Err SetEager(bool eager) {
+    return check(rlnc_decoder_set_policy(h_, eager ? RLNC_DECODE_EAGER : RLNC_DECODE_LAZY));
+  }
+  std::vector<bool> DecodedMask() const {
+    const size_t k = PieceCount();
+    std::vector<uint8_t> m(k ? k : 1);
+    rlnc_decoder_decoded_mask(h_, m.data());
+    return std::vector<bool>(m.begin(), m.begin() + k);
+  }
+  std::pair<kodr_internals::Piece, Err> GetDecodedPiece(size_t i) {
+    kodr_internals::Piece out(PieceLength() ? PieceLength() : 1);
+    Err e = check(rlnc_decoder_get_decoded(h_, i, out.data(), 0));
+    out.resize(PieceLength());
+    if (e != Err::None) return {{}, e};
+    return {out, Err::None};
+  }
+  size_t PieceCount() const { return rlnc_decoder_required(h_) + rlnc_decoder_useful(h_); }
+
  private:
   rlnc_decoder* h_ = nullptr;
 };
@@ -295,6 +318,7 @@ class FullRLNCRecoder {  // full/recoder.go:8-11
   FullRLNCRecoder(const FullRLNCRecoder&) = delete;
   FullRLNCRecoder& operator=(const FullRLNCRecoder&) = delete;
   // full/recoder.go:27-46 (error return kept for signature parity; never set)
+  Err Compact() { return detail::check(rlnc_recoder_compact(h_)); }  // extension: rlnc_recoder_compact
   std::pair<kodr_internals::CodedPiece, Err> CodedPiece() {
     if (queue_.empty()) {
       const size_t n = rlnc_recoder_piece_count(h_), clen = rlnc_recoder_coded_piece_len(h_);

@@ -82,6 +82,11 @@ class _Encoder:
                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return vec.reshape(count, k), out.reshape(count, clen)
 
+    def compact(self):
+        """Extension (rlnc_encoder_compact): keep only the bit-sliced copy of
+        the generation in HBM; device_pieces() is then (None, pitch)."""
+        errors.check(lib().rlnc_encoder_compact(self._h))
+
     def seed(self, seed):
         """Reseed the device-side vector stream of coded_wire_device."""
         errors.check(lib().rlnc_encoder_seed(self._h, ctypes.c_uint64(seed)))
@@ -139,6 +144,10 @@ class _Recoder:
                 self._h, rv.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), count,
                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return out.reshape(count, clen)
+
+    def compact(self):
+        """Extension (rlnc_recoder_compact): keep only the bit-sliced copy."""
+        errors.check(lib().rlnc_recoder_compact(self._h))
 
     def CodedPiece(self):
         """full/recoder.go:27-46 -> CodedPiece(Vector = r x C, Piece = sum r_i P_i)."""
@@ -224,3 +233,25 @@ class _Decoder:
         out = np.empty(max(L * n, 1), dtype=np.uint8)
         errors.check(lib().rlnc_decoder_get_pieces(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))))
         return [out[i * L:(i + 1) * L].tobytes() for i in range(n)]
+
+    # extensions (no kodr counterpart): pieces decoded before full rank
+    def set_policy(self, eager):
+        """EAGER (True): every AddPiece materializes the pieces it decoded."""
+        errors.check(lib().rlnc_decoder_set_policy(self._h, 1 if eager else 0))
+
+    def decoded_mask(self):
+        m = np.zeros(max(self._k, 1), dtype=np.uint8)
+        lib().rlnc_decoder_decoded_mask(self._h, m.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+        return m[:self._k].astype(bool)
+
+    def GetDecodedPiece(self, i):
+        """Original piece i if it is decoded now (a systematic piece on
+        arrival, any piece at full rank), else ErrPieceNotDecodedYet."""
+        L = self.PieceLength()
+        out = np.empty(max(L, 1), dtype=np.uint8)
+        errors.check(lib().rlnc_decoder_get_decoded(self._h, i, ctypes.c_void_p(out.ctypes.data), 0))
+        return out[:L].tobytes()
+
+    def bind_output(self, d_out, pitch):
+        """Decoded pieces land at row j of the device buffer d_out (None unbinds)."""
+        errors.check(lib().rlnc_decoder_bind_output(self._h, None if d_out is None else ctypes.c_void_p(d_out), pitch))

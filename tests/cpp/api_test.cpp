@@ -109,6 +109,30 @@ int main() {
     EXPECT(dec->GetPiece(4).second == ErrPieceOutOfBound);
     EXPECT(dec->GetPiece(0).second == ErrPieceNotDecodedYet);
   }
+  {  // extensions: compact residency, progressive decode of a systematic stream
+    std::vector<Piece> pieces;
+    for (int i = 0; i < 48; i++) pieces.push_back(gen(2048));
+    auto [enc, err] = systematic::NewSystematicRLNCEncoder(pieces);
+    EXPECT(err == Err::None && enc->Compact() == Err::None);
+    auto dec = systematic::NewSystematicRLNCDecoder(48);
+    EXPECT(dec->SetEager(true) == Err::None);
+    size_t sent = 0;
+    while (true) {
+      auto p = enc->CodedPiece();
+      const bool sys = sent++ < 48;
+      if (sys && sent % 5 == 0) continue;  // lose every fifth systematic piece
+      if (dec->AddPiece(p) == ErrAllUsefulPiecesReceived) break;
+      if (sys) {  // a systematic piece is readable on arrival
+        auto m = dec->DecodedMask();
+        EXPECT(m[sent - 1]);
+        auto [d, e] = dec->GetDecodedPiece(sent - 1);
+        EXPECT(e == Err::None && d == pieces[sent - 1]);
+        if (sent % 5 == 4) EXPECT(dec->GetDecodedPiece(sent).second == ErrPieceNotDecodedYet);
+      }
+    }
+    EXPECT(dec->GetPieces().first == pieces);
+    EXPECT(dec->GetDecodedPiece(48).second == ErrPieceOutOfBound);
+  }
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ok", failures);
   return failures ? 1 : 0;
 }

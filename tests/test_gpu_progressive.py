@@ -196,3 +196,32 @@ def test_bound_output_in_place(gpu_ctx, policy):
     assert st == 0 and np.array_equal(out, P[7])
     gpu_ctx.synchronize()
     gpu_ctx.free(dout)
+
+
+def test_python_mirror_extensions(gpu_ctx):
+    """The Python mirror's extensions: compact encoder, EAGER decoder,
+    decoded_mask / GetDecodedPiece while a systematic stream arrives."""
+    from kodr_amd import systematic
+    rng = np.random.default_rng(44)
+    k, L = 32, 1500
+    pieces = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for _ in range(k)]
+    enc = systematic.NewSystematicRLNCEncoder(pieces, ctx=gpu_ctx)
+    enc.compact()
+    assert enc.device_pieces()[0] is None
+    dec = systematic.NewSystematicRLNCDecoder(k, ctx=gpu_ctx)
+    dec.set_policy(True)
+    lost = {3, 17, 30}
+    sent = 0
+    while not dec.IsDecoded():
+        p = enc.CodedPiece()
+        i = sent
+        sent += 1
+        if i < k and i in lost:
+            continue
+        dec.AddPiece(p)
+        if i < k:
+            assert dec.decoded_mask()[i] and dec.GetDecodedPiece(i) == pieces[i]
+            with pytest.raises(errors.ErrPieceNotDecodedYet):
+                dec.GetDecodedPiece(30)
+    assert dec.decoded_mask().all()
+    assert [dec.GetDecodedPiece(j) for j in range(k)] == pieces == dec.GetPieces()
