@@ -2,7 +2,9 @@
 // kodr_internals/matrix/decoder_state.go unless stated otherwise.
 #include "decoder_core.hpp"
 
+#include <stdio.h>
 #include <stdlib.h>
+#include <time.h>
 #include <string.h>
 
 #include <algorithm>
@@ -296,12 +298,15 @@ bool DecoderCore::solve_systematic_batch(const uint8_t* vecs, size_t pitch) {
 //     pivot yet, in index order, each reduced against the rows picked so far
 //     (Gauss-Jordan on [panel | tracking] vectors, so the tracking half ends
 //     as S, the inverse of the picked rows' panel block);
-//  B: per 64-byte column chunk, right to left (the panel's own chunk last, so
-//     every row's panel bytes are still the multipliers Q): the new pivot
-//     rows S x (picked rows), and every other row ^= Q[row] x (new pivot rows).
-// Columns left of the panel never change (zero in every picked row), and T
-// column t stays zero in every row until row t is picked (each unpicked row's
-// own identity entry aside), so a row's bytes in play are [jb, k + tmax).  A
+//  B: per 64-byte column chunk: the new pivot rows S x (picked rows), and
+//     every other row ^= Q[row] x (new pivot rows), Q = the row's panel bytes.
+// Columns left of the panel never change (zero in every picked row), the
+// panel's own columns end as 0 in every other row and as the identity in the
+// picked ones (not stored: nothing reads them again, and the final rows'
+// coefficient halves are written as I at the end), and T column t stays zero
+// in every row until row t is picked (each unpicked row's own identity entry
+// aside), so a row's bytes in play are [jb + nb, k + tmax): k bytes when the
+// picked rows are the lowest unpicked ones, 4 full chunks at k = 256.  A
 // panel with too few independent rows means C is singular: nothing is kept
 // and add_many takes kodr's route.  One thread: the matrix is ~160 KB, and a
 // spin-barrier thread pool splitting its 64-byte column chunks over cores
@@ -309,9 +314,17 @@ bool DecoderCore::solve_systematic_batch(const uint8_t* vecs, size_t pitch) {
 // one) moved more cache lines between cores per panel than it saved.
 namespace {
 
+double now_us() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 constexpr int kFullNB = 16;
-// Below this the 4-row panels of add_panel are faster on the box's EPYC
-// (tools/full_solve_time.sh: k = 192 route 40 us vs 48 blocked; k = 256 103 vs 94).
+// Below this the 4-row panels of add_panel are as fast or faster on the box's
+// EPYC (tools/full_solve_time.sh, profiles/r02/elim/: k = 192 route 40 us vs
+// 48 blocked in the first version; k = 256 105 vs 79-81 now, 14 us of it the
+// panels' pivot picking, 63 us the row updates).
 constexpr size_t kFullMinK = 224;
 
 struct FullSolve {
@@ -363,11 +376,10 @@ struct FullSolve {
   }
 
   void phase_b(size_t jb) {
-    const size_t end = k + tmax, nch = (end - jb + 63) / 64;
-    for (size_t ch = nch; ch-- > 0;) {
-      const size_t o = jb + ch * 64, w = std::min<size_t>(64, end - o);
-      hostgf::panel_update<kFullNB>(rows.data(), k, o, w, jb, brow, bpiv, S, nb, cur.data());
-    }
+    const size_t beg = jb + nb, end = k + tmax;
+    for (size_t o = beg; o < end; o += 64)
+      hostgf::panel_update<kFullNB>(rows.data(), k, o, std::min<size_t>(64, end - o), jb, brow, bpiv, S, nb,
+                                    cur.data());
   }
 };
 
@@ -391,15 +403,25 @@ bool DecoderCore::solve_full_batch(const uint8_t* vecs, size_t pitch) {
   F.cur.assign(k, -1);
   F.used.assign(k, 0);
   F.pivrow.assign(k, -1);
+  static const bool timing = getenv("KODR_FULL_SOLVE") && atoi(getenv("KODR_FULL_SOLVE")) == 2;
+  double ta = 0, tb = 0;
   for (size_t jb = 0; jb < k; jb += kFullNB) {
+    const double t0 = timing ? now_us() : 0;
     if (!F.phase_a(jb)) return false;  // C singular; the slots are still free: nothing changed
+    const double t1 = timing ? now_us() : 0;
     F.phase_b(jb);
+    if (timing) {
+      ta += t1 - t0;
+      tb += now_us() - t1;
+    }
   }
-  for (size_t c = 0; c < k; c++)
-    if (F.rows[F.pivrow[c]][c] != 1) return false;  // cannot happen: refuse rather than load a wrong state
+  if (timing) fprintf(stderr, "solve_full_batch k=%zu: panels %.1f us, updates %.1f us\n", k, ta, tb);
   free_.resize(free_.size() - k);
   for (size_t c = 0; c < k; c++) {
-    push_row(F.rows[F.pivrow[c]], -1, 0);
+    uint8_t* row = F.rows[F.pivrow[c]];
+    memset(row, 0, k);  // [I | C^-1]: the panels' columns were not stored
+    row[c] = 1;
+    push_row(row, -1, 0);
     clean_[c] = 1;
     touched_[c] = 0;
   }
