@@ -322,10 +322,11 @@ double now_us() {
 
 constexpr int kFullNB = 16;
 // Below this the 4-row panels of add_panel are as fast or faster on the box's
-// EPYC (tools/full_solve_time.sh, profiles/r02/elim/: k = 192 route 40 us vs
-// 48 blocked in the first version; k = 256 105 vs 79-81 now, 14 us of it the
-// panels' pivot picking, 63 us the row updates).
-constexpr size_t kFullMinK = 224;
+// EPYC (tools/full_solve_mink.sh, profiles/r02/elim/full_solve_min_k.log: equal
+// within 1-3 us at k = 64-192, k = 224 route 55 us vs 68 blocked; k = 256 105
+// vs 79-81, 14 us of it the panels' pivot picking, 63 us the row updates).
+// KODR_FULL_MIN_K overrides it (measurements).
+constexpr size_t kFullMinK = 240;
 
 struct FullSolve {
   size_t k = 0;
@@ -388,7 +389,8 @@ struct FullSolve {
 bool DecoderCore::solve_full_batch(const uint8_t* vecs, size_t pitch) {
   const size_t k = k_;
   static const bool enabled = !getenv("KODR_FULL_SOLVE") || atoi(getenv("KODR_FULL_SOLVE")) != 0;
-  if (!enabled || received_ != 0 || k < kFullMinK || !hostgf::have_gfni512()) return false;
+  static const size_t min_k = getenv("KODR_FULL_MIN_K") ? (size_t)atol(getenv("KODR_FULL_MIN_K")) : kFullMinK;
+  if (!enabled || received_ != 0 || k < min_k || !hostgf::have_gfni512()) return false;
   ensure_tcap(k);
   FullSolve F;
   F.k = k;

@@ -390,14 +390,14 @@ def test_systematic_full_batch_solve(seed):
 
 @pytest.mark.parametrize("seed", range(36))
 def test_full_batch_solve(seed):
-    # one batched AddPiece of >= k coded rows on a fresh decoder (k >= 224):
+    # one batched AddPiece of >= k coded rows on a fresh decoder (k >= 240):
     # DecoderCore inverts the first k vectors by blocked Gauss-Jordan
     # (decoder_core.cpp solve_full_batch) instead of taking kodr's route; the
     # state, counters and T must equal row-by-row AddPiece -- for dense rows,
     # {0,1,2}-valued rows (zero diagonals, panels whose first candidate rows are
     # dependent), and singular batches (duplicates, low rank: kodr's route)
     rng = np.random.default_rng(6100 + seed)
-    k = int(rng.choice([224, 231, 256]))
+    k = int(rng.choice([240, 250, 256]))
     n = k + int(rng.integers(0, 4))
     kind = seed % 6
     if kind in (0, 1):
