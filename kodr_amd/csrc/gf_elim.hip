@@ -45,6 +45,7 @@
 // and published it in LDS (two buffers, alternating).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gf_kernels.hpp"
 
@@ -55,6 +56,7 @@ namespace {
 constexpr int kElimWaves = 16;
 constexpr int kElimRowsPerWave = 16;   // 16 x 16 = 256 rows
 constexpr int kNone = 0x7fffffff;
+constexpr int kElimBlockedMinK = 32;  // below: the per-step kernel (one panel would be most of it)
 
 // LDS: two pivot buffers [2][128] dwords, the pivot choice (three rotating
 // slots, LDS atomic min of the waves' candidates), the pivot column of every
@@ -243,6 +245,252 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_kernel(ElimArgs args)
   if (tid == 0) args.counts[g] = c;
 }
 
+
+// ---- FULL batches, blocked: panels of 16 columns ------------------------
+// The same result as the FULL case above ([I | C^-1], T in arrival order),
+// computed by a blocked Gauss-Jordan whose serial part is one small panel
+// per 16 columns instead of every one of the k steps:
+//  1. panel b (columns jb = 16b ..): its candidates are rows jb .. jb + 15,
+//     all owned by wave b (rows picked so far are exactly rows 0 .. jb - 1, as
+//     long as every panel block is invertible).  Wave b inverts the block
+//     M = C'[rows jb.., cols jb..] by Gauss-Jordan with row pivoting, one
+//     lane per (row, dword) of [M | I]; S = M^-1 (LDS), the candidates' old
+//     rows to LDS.  A singular block stops the kernel (count 0: the host
+//     takes kodr's route for the batch, as for a singular C).
+//  2. all waves: the new pivot rows N = S x (candidate rows), 1-2 dwords per
+//     lane, to LDS.
+//  3. wave b replaces its rows with N (pivot column jb + c -> row of S's
+//     column c); every other row j gets row_j ^= sum_c row_j[jb + c] * N[c]
+//     (multipliers wave-uniform: tables through the scalar cache).
+// Two barriers per panel, k/16 panels.
+struct ElimBlkLds {
+  uint32_t tab[256 * 8];   // per-lane table reads (panel Gauss-Jordan): [256][8] dwords
+  uint32_t prow[16][128];  // the panel's candidate rows before the step
+  uint32_t np[16][128];    // the new pivot rows, by panel column
+  uint32_t pan[16][4];     // the panel block of the candidates (owner wave scratch)
+  uint32_t sd[16][4];      // S[c][u] = byte u % 4 of sd[c][u / 4]
+  int colof[256];          // pivot column of each row
+  int fail;
+};
+
+__device__ __forceinline__ uint32_t sel0(uint32_t x) { return x & 0x07070707u; }
+__device__ __forceinline__ uint32_t sel1(uint32_t x) { return (x >> 3) & 0x07070707u; }
+__device__ __forceinline__ uint32_t sel2(uint32_t x) { return (x >> 6) & 0x03030303u; }
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
+}
+
+template <int DPL>
+__global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimArgs args) {
+  __shared__ ElimBlkLds lds;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = args.k;
+  const int j0 = w * kElimRowsPerWave;
+  const uint8_t* vec = args.vecs[g];
+  const size_t vp = args.vpitch;
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  cu32* tb = (cu32*)args.tables;
+
+  for (int i = tid; i < 256 * 8; i += 64 * kElimWaves) lds.tab[i] = args.tables[i];
+  for (int i = tid; i < 256; i += 64 * kElimWaves) lds.colof[i] = -1;
+  if (tid == 0) lds.fail = 0;
+
+  // rows [C | I] in registers, as gf_elim_kernel
+  uint32_t R[kElimRowsPerWave][DPL];
+#pragma unroll
+  for (int i = 0; i < kElimRowsPerWave; i++) {
+    const int j = j0 + i;
+#pragma unroll
+    for (int h = 0; h < DPL; h++) {
+      uint32_t v = 0;
+      if (j < k) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int col = (h * 64 + lane) * 4 + b;
+          uint32_t byte = 0;
+          if (col < k) byte = vec[(size_t)j * vp + col];
+          else if (col == k + j) byte = 1;
+          v |= byte << (8 * b);
+        }
+      }
+      R[i][h] = v;
+    }
+  }
+  __syncthreads();
+
+  const int npanels = (k + 15) / 16;
+#ifdef KODR_ELIM_TIMING
+  uint64_t tacc[6] = {0, 0, 0, 0, 0, 0};  // owner panel, barrier 1, pivot rows, barrier 2, row update
+  uint64_t tq = __builtin_amdgcn_s_memtime(), tstart = tq;
+#define KODR_STAMP(i)                              \
+  do {                                             \
+    const uint64_t tn = __builtin_amdgcn_s_memtime(); \
+    tacc[i] += tn - tq;                            \
+    tq = tn;                                       \
+  } while (0)
+#else
+#define KODR_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+  for (int pb = 0; pb < npanels; pb++) {
+    const int jb = pb * 16, nb = min(16, k - jb);
+    const int pl0 = jb >> 2;  // lane of the panel's first dword (h = 0)
+    if (w == pb) {
+      // ---- 1. the owner: old rows out, panel block inverted ----
+#pragma unroll
+      for (int i = 0; i < kElimRowsPerWave; i++) {
+#pragma unroll
+        for (int h = 0; h < DPL; h++) lds.prow[i][h * 64 + lane] = R[i][h];
+        if (lane >= pl0 && lane < pl0 + 4) lds.pan[i][lane - pl0] = R[i][0];
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes land first
+      const int t = lane >> 2, d = lane & 3;
+      uint32_t P = lds.pan[t][d], Tr = 0;
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (4 * d + e >= nb) P &= ~(0xffu << (8 * e));  // columns past the panel (the last one)
+      if (t < nb && (t >> 2) == d) Tr = 1u << (8 * (t & 3));
+      if (t >= nb) P = 0;
+      uint32_t used = (0xffffu << nb) & 0xffffu;  // rows past k are not candidates
+      int mycol = -1;
+      bool ok = true;
+      for (int c = 0; c < nb; c++) {
+        const int cd = c >> 2, cb = 8 * (c & 3);
+        const bool nz = (d == cd) && ((P >> cb) & 0xffu) != 0u && !((used >> t) & 1u);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+        if (m == 0) {
+          ok = false;
+          break;
+        }
+        const int pl = __builtin_ctzll(m), tp = pl >> 2;
+        const uint32_t dp = (__builtin_amdgcn_readlane(P, pl) >> cb) & 0xffu;
+        cu32* tinv = tb + kElimInvTables + dp * 8;  // tables of inv(dp) (gf256.go:77-86)
+        const uint4 ti = {tinv[0], tinv[1], tinv[2], tinv[3]};
+        const uint32_t ti2 = tinv[4];
+        if (t == tp) {
+          P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
+          Tr = gmul4(ti, ti2, sel0(Tr), sel1(Tr), sel2(Tr));
+          mycol = c;
+        }
+        const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
+        uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
+        if (t == tp) f = 0u;
+        const uint4 tf = *reinterpret_cast<const uint4*>(&lds.tab[f * 8]);
+        const uint32_t tf2 = lds.tab[f * 8 + 4];
+        P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
+        Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
+        used |= 1u << tp;
+      }
+      if (!ok) {
+        if (lane == 0) lds.fail = 1;
+      } else if (t < nb) {
+        lds.sd[mycol][d] = Tr;
+        if (d == 0) lds.colof[jb + t] = jb + mycol;
+      }
+    }
+    KODR_STAMP(0);
+    __syncthreads();
+    KODR_STAMP(1);
+    if (lds.fail) break;  // uniform
+    // ---- 2. the new pivot rows, spread over the workgroup ----
+#pragma unroll
+    for (int r = 0; r < DPL; r++) {
+      const int idx = tid + r * 64 * kElimWaves;
+      const int c = __builtin_amdgcn_readfirstlane(idx / (64 * DPL)), dw = idx % (64 * DPL);
+      if (c < nb) {
+        uint32_t acc = 0;
+        for (int u4 = 0; u4 < 4; u4++) {  // S[c][4 u4 .. 4 u4 + 3]: one dword, four tables in flight
+          const uint32_t sw = __builtin_amdgcn_readfirstlane(lds.sd[c][u4]);
+          uint32_t x[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) x[e] = lds.prow[4 * u4 + e][dw];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const uint32_t su = (sw >> (8 * e)) & 0xffu;  // 0 past nb (S rows are zero there)
+            const uint4 ts = {tb[su * 8], tb[su * 8 + 1], tb[su * 8 + 2], tb[su * 8 + 3]};
+            const uint32_t ts2 = tb[su * 8 + 4];
+            acc ^= gmul4(ts, ts2, sel0(x[e]), sel1(x[e]), sel2(x[e]));
+          }
+        }
+        lds.np[c][dw] = acc;
+      }
+    }
+    KODR_STAMP(2);
+    __syncthreads();
+    KODR_STAMP(3);
+    // ---- 3. rows: the owner's become the pivot rows, the others drop the panel ----
+    if (w == pb) {
+#pragma unroll
+      for (int i = 0; i < kElimRowsPerWave; i++)
+        if (i < nb) {
+          const int c = __builtin_amdgcn_readfirstlane(lds.colof[jb + i]) - jb;
+#pragma unroll
+          for (int h = 0; h < DPL; h++) R[i][h] = lds.np[c][h * 64 + lane];
+        }
+    } else if (j0 < k) {
+      // one panel column c at a time: its pivot row's selectors, then every
+      // row's multiplier table (the row's panel byte c: wave-uniform) read
+      // from LDS one row ahead, so no row waits for its own table
+      for (int c = 0; c < nb; c++) {
+        uint32_t s0[DPL], s1[DPL], s2[DPL];
+#pragma unroll
+        for (int h = 0; h < DPL; h++) {
+          const uint32_t x = lds.np[c][h * 64 + lane];
+          s0[h] = sel0(x);
+          s1[h] = sel1(x);
+          s2[h] = sel2(x);
+        }
+        const int ql = pl0 + (c >> 2), qs = 8 * (c & 3);
+        auto fetch = [&](int i, uint4& t, uint32_t& t2) {
+          const uint32_t f = (__builtin_amdgcn_readlane(R[i][0], ql) >> qs) & 0xffu;
+          t = *reinterpret_cast<const uint4*>(&lds.tab[f * 8]);
+          t2 = lds.tab[f * 8 + 4];
+        };
+        uint4 ta, tn;
+        uint32_t ta2, tn2;
+        fetch(0, ta, ta2);
+#pragma unroll
+        for (int i = 0; i < kElimRowsPerWave; i++) {
+          if (i + 1 < kElimRowsPerWave) fetch(i + 1, tn, tn2);
+#pragma unroll
+          for (int h = 0; h < DPL; h++) R[i][h] ^= gmul4(ta, ta2, s0[h], s1[h], s2[h]);
+          ta = tn;
+          ta2 = tn2;
+        }
+      }
+    }
+    KODR_STAMP(4);
+  }
+#ifdef KODR_ELIM_TIMING
+  tacc[5] = __builtin_amdgcn_s_memtime() - tstart;
+  if (lane == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(args.out + (size_t)g * args.out_gen_stride) + 8 * w;
+    for (int q = 0; q < 6; q++) o[q] = tacc[q];
+  }
+  if (tid == 0) args.counts[g] = 0;
+  return;
+#endif
+#undef KODR_STAMP
+  __syncthreads();
+  const int c = lds.fail ? 0 : k;
+  uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+  if (c) {
+#pragma unroll
+    for (int i = 0; i < kElimRowsPerWave; i++) {
+      const int j = j0 + i;
+      if (j >= k) continue;
+      const int at = lds.colof[j];
+#pragma unroll
+      for (int h = 0; h < DPL; h++)
+        reinterpret_cast<uint32_t*>(out + (size_t)at * args.out_pitch)[h * 64 + lane] = R[i][h];
+    }
+  }
+  if (tid == 0) args.counts[g] = c;
+}
+
 }  // namespace
 
 void elim_tables(uint32_t* host_out) {
@@ -283,6 +531,9 @@ void elim_tables(uint32_t* host_out) {
   for (int i = 0; i < 64; i++)
     host_out[256 * 8 + i] = (uint32_t)inv[4 * i] | ((uint32_t)inv[4 * i + 1] << 8) |
                             ((uint32_t)inv[4 * i + 2] << 16) | ((uint32_t)inv[4 * i + 3] << 24);
+  // tables of inv(f), so a pivot's normalization is one dependent load
+  for (unsigned f = 0; f < 256; f++)
+    for (int q = 0; q < 8; q++) host_out[kElimInvTables + f * 8 + q] = f ? host_out[inv[f] * 8 + q] : 0u;
 }
 
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
@@ -290,7 +541,15 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G > kElimMaxGens || args.k < 2 || args.k > 256 || args.out_pitch % 4 ||
       args.out_pitch < (size_t)(args.k <= 128 ? 256 : 512))
     return hipErrorInvalidValue;
-  if (args.k <= 128)
+  // every batch full (n >= k) and k large enough for panels to pay: blocked
+  bool full = args.k >= kElimBlockedMinK;
+  for (int i = 0; i < G && full; i++) full = args.n[i] >= args.k;
+  if (const char* e = getenv("KODR_ELIM_BLOCKED")) full = full && atoi(e) != 0;  // A/B measurements
+  if (full && args.k <= 128)
+    hipLaunchKernelGGL(gf_elim_blocked_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
+  else if (full)
+    hipLaunchKernelGGL(gf_elim_blocked_kernel<2>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
+  else if (args.k <= 128)
     hipLaunchKernelGGL(gf_elim_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else
     hipLaunchKernelGGL(gf_elim_kernel<2>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);

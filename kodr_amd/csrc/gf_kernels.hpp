@@ -87,7 +87,9 @@ struct ElimArgs {
   int* counts;
   int k;
 };
-constexpr size_t kElimTableWords = 256 * 8 + 64;
+// [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
+constexpr size_t kElimInvTables = 256 * 8 + 64;
+constexpr size_t kElimTableWords = kElimInvTables + 256 * 8;
 void elim_tables(uint32_t* host_out);  // kElimTableWords dwords
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 
