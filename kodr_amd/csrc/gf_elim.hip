@@ -264,7 +264,7 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_kernel(ElimArgs args)
 //     (multipliers wave-uniform: tables through the scalar cache).
 // Two barriers per panel, k/16 panels.
 struct ElimBlkLds {
-  uint32_t tab[256 * 8];   // per-lane table reads (panel Gauss-Jordan): [256][8] dwords
+  uint4 tab[256 * 2];      // the [256][8]-dword tables as 16-byte rows: tab[2f] = T0, T1; tab[2f + 1].x = T2
   uint32_t prow[16][128];  // the panel's candidate rows before the step
   uint32_t np[16][128];    // the new pivot rows, by panel column
   uint32_t pan[16][4];     // the panel block of the candidates (owner wave scratch)
@@ -293,7 +293,8 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
   typedef const __attribute__((address_space(4))) uint32_t cu32;
   cu32* tb = (cu32*)args.tables;
 
-  for (int i = tid; i < 256 * 8; i += 64 * kElimWaves) lds.tab[i] = args.tables[i];
+  for (int i = tid; i < 256 * 2; i += 64 * kElimWaves)
+    lds.tab[i] = make_uint4(args.tables[4 * i], args.tables[4 * i + 1], args.tables[4 * i + 2], args.tables[4 * i + 3]);
   for (int i = tid; i < 256; i += 64 * kElimWaves) lds.colof[i] = -1;
   if (tid == 0) lds.fail = 0;
 
@@ -378,8 +379,8 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
         const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
         uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
         if (t == tp) f = 0u;
-        const uint4 tf = *reinterpret_cast<const uint4*>(&lds.tab[f * 8]);
-        const uint32_t tf2 = lds.tab[f * 8 + 4];
+        const uint4 tf = lds.tab[2 * f];  // one ds_read_b128 + one ds_read_b32
+        const uint32_t tf2 = lds.tab[2 * f + 1].x;
         P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
         Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
         used |= 1u << tp;
@@ -446,19 +447,28 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
         const int ql = pl0 + (c >> 2), qs = 8 * (c & 3);
         auto fetch = [&](int i, uint4& t, uint32_t& t2) {
           const uint32_t f = (__builtin_amdgcn_readlane(R[i][0], ql) >> qs) & 0xffu;
-          t = *reinterpret_cast<const uint4*>(&lds.tab[f * 8]);
-          t2 = lds.tab[f * 8 + 4];
+          t = lds.tab[2 * f];
+          t2 = lds.tab[2 * f + 1].x;
         };
-        uint4 ta, tn;
-        uint32_t ta2, tn2;
+        // two rows ahead: a row's LDS reads have two rows of arithmetic to land
+        uint4 ta, tb1, tn;
+        uint32_t ta2, tb2, tn2;
         fetch(0, ta, ta2);
+        fetch(1, tb1, tb2);
 #pragma unroll
         for (int i = 0; i < kElimRowsPerWave; i++) {
-          if (i + 1 < kElimRowsPerWave) fetch(i + 1, tn, tn2);
+          if (i + 2 < kElimRowsPerWave) fetch(i + 2, tn, tn2);
 #pragma unroll
-          for (int h = 0; h < DPL; h++) R[i][h] ^= gmul4(ta, ta2, s0[h], s1[h], s2[h]);
-          ta = tn;
-          ta2 = tn2;
+          for (int h = 0; h < DPL; h++) {
+            const uint32_t p0 = __builtin_amdgcn_perm(ta.y, ta.x, s0[h]);
+            const uint32_t p1 = __builtin_amdgcn_perm(ta.w, ta.z, s1[h]);
+            const uint32_t p2 = __builtin_amdgcn_perm(ta2, ta2, s2[h]);
+            R[i][h] = __builtin_amdgcn_bitop3_b32(R[i][h], p0, p1, 0x96) ^ p2;
+          }
+          ta = tb1;
+          ta2 = tb2;
+          tb1 = tn;
+          tb2 = tn2;
         }
       }
     }
