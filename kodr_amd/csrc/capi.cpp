@@ -1193,7 +1193,16 @@ struct BatchCopy {
   bool early = false;
 };
 
-int dec_batch_pre(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch, bool dev, BatchCopy* bc) {
+// With `defer`, a fused copy of device rows is appended there instead of
+// launched (rlnc_decoders_add_pieces_gpu launches all of them at once).
+struct DeferredCopy {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint8_t* dbs;
+  size_t rows, dpitch;
+};
+int dec_batch_pre(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch, bool dev, BatchCopy* bc,
+                  std::vector<DeferredCopy>* defer = nullptr) {
   const size_t k = d->core.piece_count();
   bc->row0 = d->core.received();
   bc->early = d->ctx && (dev || kodr_amd::Staging::is_pinned(rows));
@@ -1213,9 +1222,17 @@ int dec_batch_pre(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pit
     }
   }
   // device rows whose twin starts here: copy and bit-slice in one pass
-  const bool fused = twin && dev && d->bs_rows == row0 && d->L % 32 == 0 &&
-                     kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, d->recv_bs.p + row0 * d->pitch, d->pitch,
-                                                  pre, d->L, d->ctx->stream) == hipSuccess;
+  uint8_t* dbs = twin ? d->recv_bs.p + row0 * d->pitch : nullptr;
+  bool fused = false;
+  if (twin && dev && d->bs_rows == row0 && d->L % 32 == 0) {
+    if (defer && kodr_amd::copy_bitslice_ok(rows + k, pitch, dst, dbs, d->pitch, d->L) && pre <= 0x7fffffff) {
+      defer->push_back({rows + k, dst, dbs, pre, d->pitch});
+      fused = true;
+    } else {
+      fused = kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, dbs, d->pitch, pre, d->L, d->ctx->stream) ==
+              hipSuccess;
+    }
+  }
   if (!fused) {
     if (dev)
       HIPC(kodr_amd::copy_rows(rows + k, pitch, dst, d->pitch, pre, d->L, d->ctx->stream));
@@ -1316,6 +1333,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   // launch); every other decoder takes rlnc_decoder_add_pieces
   std::vector<size_t> gpu;
   std::vector<BatchCopy> bcs(G);
+  std::vector<DeferredCopy> defer;
   for (size_t g = 0; g < G; g++) {
     rlnc_decoder* d = ds[g];
     const bool ok = k >= 2 && k <= 256 && counts[g] >= 2 && d->core.received() == 0;
@@ -1324,8 +1342,22 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       continue;
     }
     if ((status[g] = dec_check(d, k, rows[g] + k, piece_len)) != RLNC_OK) continue;
-    if ((status[g] = dec_batch_pre(d, rows[g], counts[g], pitch, true, &bcs[g])) != RLNC_OK) continue;
+    if ((status[g] = dec_batch_pre(d, rows[g], counts[g], pitch, true, &bcs[g], &defer)) != RLNC_OK) continue;
     gpu.push_back(g);
+  }
+  // the deferred row copies: one launch per kCopyGroupMax decoders (one piece
+  // length, so one pitch)
+  for (size_t c0 = 0; c0 < defer.size(); c0 += kodr_amd::kCopyGroupMax) {
+    const size_t nc = std::min<size_t>(kodr_amd::kCopyGroupMax, defer.size() - c0);
+    kodr_amd::CopyGroup cg = {};
+    for (size_t i = 0; i < nc; i++) {
+      if (defer[c0 + i].dpitch != defer[c0].dpitch) return RLNC_ERR_INVALID_ARGUMENT;  // cannot happen
+      cg.src[i] = defer[c0 + i].src;
+      cg.dst[i] = defer[c0 + i].dst;
+      cg.dbs[i] = defer[c0 + i].dbs;
+      cg.rows[i] = (int)defer[c0 + i].rows;
+    }
+    HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len, ctx->stream));
   }
   if (gpu.empty()) return RLNC_OK;
   TRY(ctx_elim_tables(ctx));
@@ -1350,8 +1382,17 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
     a.k = (int)k;
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
-    HIPC(ctx->stage.d2h(host.data(), hdr + nc * ostride, ctx->elim_out.p, hdr + nc * ostride, hdr + nc * ostride,
-                        1, ctx->stream));
+    // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
+    // back (one 2D copy: the generations' rows are evenly strided), else the
+    // whole states
+    const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
+    if (tonly) {
+      HIPC(ctx->stage.d2h(host.data(), hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
+      HIPC(ctx->stage.d2h(host.data() + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
+    } else {
+      HIPC(ctx->stage.d2h(host.data(), hdr + nc * ostride, ctx->elim_out.p, hdr + nc * ostride,
+                          hdr + nc * ostride, 1, ctx->stream));
+    }
 #ifdef KODR_ELIM_TIMING
     if (const char* dump = getenv("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
       if (FILE* fp = fopen(dump, "wb")) {
@@ -1366,7 +1407,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       const size_t g = gpu[c0 + i];
       rlnc_decoder* d = ds[g];
       size_t c = (size_t)std::max(cnt[i], 0);
-      if (c && !d->core.load_rref(host.data() + hdr + i * ostride, opitch, c)) c = 0;
+      if (c && tonly && !(c == k && d->core.load_inverse(host.data() + hdr + i * k * k, k))) c = 0;
+      if (c && !tonly && !d->core.load_rref(host.data() + hdr + i * ostride, opitch, c)) c = 0;
       // the rest of the batch (past a row off its diagonal, or past k) through
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;

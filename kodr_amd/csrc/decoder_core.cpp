@@ -766,6 +766,27 @@ bool DecoderCore::load_rref(const uint8_t* state, size_t pitch, size_t c) {
   return true;
 }
 
+bool DecoderCore::load_inverse(const uint8_t* tinv, size_t pitch) {
+  const size_t k = k_;
+  if (received_ != 0 || k < 2) return false;
+  ensure_tcap(k);
+  for (size_t i = 0; i < k; i++) {
+    uint8_t* row = free_.back();
+    free_.pop_back();
+    memset(row, 0, k);
+    row[i] = 1;
+    memcpy(row + k, tinv + i * pitch, k);
+    memset(row + 2 * k, 0, tcap_ - k);
+    push_row(row, -1, 0);
+    clean_[i] = 1;
+    touched_[i] = 0;
+  }
+  received_ = k;
+  useful_ = k;
+  all_clean_ = true;
+  return true;
+}
+
 size_t DecoderCore::decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const {
   row_of->assign(k_, -1);
   scale->assign(k_, 0);

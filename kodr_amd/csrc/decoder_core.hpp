@@ -41,6 +41,10 @@ class DecoderCore {
   // Later add() / add_many() calls continue exactly as if those c pieces had
   // been added one by one.  Returns false (and changes nothing) otherwise.
   bool load_rref(const uint8_t* state, size_t pitch, size_t c);
+  // A fresh decoder takes the state kodr reaches after k pieces whose vectors
+  // C are independent: [I | C^-1], given as C^-1 (k rows of k bytes at `pitch`,
+  // columns in arrival order).  Returns false (and changes nothing) otherwise.
+  bool load_inverse(const uint8_t* tinv, size_t pitch);
 
   bool is_decoded() const { return useful_ >= k_; }   // full/decoder.go:32-34
   size_t required() const { return k_ - useful_; }    // full/decoder.go:38-40

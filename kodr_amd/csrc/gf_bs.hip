@@ -113,6 +113,26 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
   t[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// copy_bitslice_kernel over several row sets at once (blockIdx.y = set)
+__global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
+                                                                   int nblk) {
+  const int y = blockIdx.y;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(i / (size_t)nblk), b = (int)(i % (size_t)nblk);
+  if (r >= g.rows[y]) return;
+  const uint4* q = reinterpret_cast<const uint4*>(g.src[y] + (size_t)r * spitch + (size_t)b * kBsBlock);
+  const size_t off = (size_t)r * dpitch + (size_t)b * kBsBlock;
+  const uint4 a = q[0], c = q[1];
+  uint4* p = reinterpret_cast<uint4*>(g.dst[y] + off);
+  p[0] = a;
+  p[1] = c;
+  uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  bitslice32(d);
+  uint4* t = reinterpret_cast<uint4*>(g.dbs[y] + off);
+  t[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  t[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+
 // The bodies' only home: this kernel exports the absolute address of body
 // (0, 0) and every body's offset from it (out[i] for body i = copy * 256 + c,
 // out[1024] lo, out[1025] hi) and never runs them; gf_bs_kernel jumps here.
@@ -547,6 +567,29 @@ hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, u
   if (rows > 0x7fffffff || nblk > 0x7fffffff) return hipErrorInvalidValue;
   hipLaunchKernelGGL(copy_bitslice_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src,
                      spitch, dst, dst_bs, dpitch, (int)rows, (int)nblk);
+  return hipGetLastError();
+}
+
+bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, const uint8_t* dst_bs, size_t dpitch,
+                      size_t ncols) {
+  return ncols && ncols % kBsBlock == 0 && dpitch % kBsBlock == 0 && dpitch >= ncols && (uintptr_t)src % 16 == 0 &&
+         spitch % 16 == 0 && (uintptr_t)dst % 16 == 0 && (uintptr_t)dst_bs % 16 == 0 && ncols / kBsBlock <= 0x7fffffff;
+}
+
+hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
+                                      hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (n > kCopyGroupMax) return hipErrorInvalidValue;
+  int maxr = 0;
+  for (int i = 0; i < n; i++) {
+    if (g.rows[i] < 0 || !copy_bitslice_ok(g.src[i], spitch, g.dst[i], g.dbs[i], dpitch, ncols))
+      return hipErrorInvalidValue;
+    maxr = g.rows[i] > maxr ? g.rows[i] : maxr;
+  }
+  const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk;
+  if (!total) return hipSuccess;
+  hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)((total + 255) / 256), (unsigned)n), dim3(256), 0,
+                     stream, g, spitch, dpitch, (int)nblk);
   return hipGetLastError();
 }
 

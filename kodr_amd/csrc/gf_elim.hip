@@ -546,15 +546,20 @@ void elim_tables(uint32_t* host_out) {
     for (int q = 0; q < 8; q++) host_out[kElimInvTables + f * 8 + q] = f ? host_out[inv[f] * 8 + q] : 0u;
 }
 
+bool gf_elim_blocked(const ElimArgs& args, int G) {
+  // every batch full (n >= k) and k large enough for panels to pay
+  bool full = args.k >= kElimBlockedMinK;
+  for (int i = 0; i < G && full; i++) full = args.n[i] >= args.k;
+  if (const char* e = getenv("KODR_ELIM_BLOCKED")) full = full && atoi(e) != 0;  // A/B measurements
+  return full;
+}
+
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
   if (G > kElimMaxGens || args.k < 2 || args.k > 256 || args.out_pitch % 4 ||
       args.out_pitch < (size_t)(args.k <= 128 ? 256 : 512))
     return hipErrorInvalidValue;
-  // every batch full (n >= k) and k large enough for panels to pay: blocked
-  bool full = args.k >= kElimBlockedMinK;
-  for (int i = 0; i < G && full; i++) full = args.n[i] >= args.k;
-  if (const char* e = getenv("KODR_ELIM_BLOCKED")) full = full && atoi(e) != 0;  // A/B measurements
+  const bool full = gf_elim_blocked(args, G);
   if (full && args.k <= 128)
     hipLaunchKernelGGL(gf_elim_blocked_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full)

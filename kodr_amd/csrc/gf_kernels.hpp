@@ -91,6 +91,9 @@ struct ElimArgs {
 constexpr size_t kElimInvTables = 256 * 8 + 64;
 constexpr size_t kElimTableWords = kElimInvTables + 256 * 8;
 void elim_tables(uint32_t* host_out);  // kElimTableWords dwords
+// true when gf_elim takes the blocked kernel for this launch: every count is
+// then k (the state is [I | C^-1]: only T = C^-1 needs reading back) or 0
+bool gf_elim_blocked(const ElimArgs& args, int G);
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 
 // ---- bit-sliced path (gf_bs.hip) ----
@@ -107,6 +110,20 @@ hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t ro
 // hipErrorInvalidValue: the caller copies and bit-slices in two passes).
 hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, uint8_t* dst_bs, size_t dpitch,
                               size_t rows, size_t ncols, hipStream_t stream);
+// copy_bitslice_rows for up to kCopyGroupMax row sets of one shape (ncols,
+// pitches) in one launch: set i = rows[i] rows from src[i] to dst[i], dbs[i].
+// The same alignment rules; copy_bitslice_ok checks one set.
+constexpr int kCopyGroupMax = 64;
+struct CopyGroup {
+  const uint8_t* src[kCopyGroupMax];
+  uint8_t* dst[kCopyGroupMax];
+  uint8_t* dbs[kCopyGroupMax];
+  int rows[kCopyGroupMax];
+};
+bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, const uint8_t* dst_bs, size_t dpitch,
+                      size_t ncols);
+hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
+                                      hipStream_t stream);
 
 // byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);
