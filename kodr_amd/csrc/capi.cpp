@@ -1385,7 +1385,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
     // back (one 2D copy: the generations' rows are evenly strided), else the
     // whole states
+#ifdef KODR_ELIM_TIMING
+    const bool tonly = false;  // the kernel's stamps sit in the state rows
+#else
     const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
+#endif
     if (tonly) {
       HIPC(ctx->stage.d2h(host.data(), hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
       HIPC(ctx->stage.d2h(host.data() + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));

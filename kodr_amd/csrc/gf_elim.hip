@@ -560,6 +560,8 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
       args.out_pitch < (size_t)(args.k <= 128 ? 256 : 512))
     return hipErrorInvalidValue;
   const bool full = gf_elim_blocked(args, G);
+  // (a panel step with DPP/readlane broadcasts instead of ds_bpermute measured
+  // slower: 520 vs 493 us at k = 256, profiles/r02/elim/elim_gj_ab.log)
   if (full && args.k <= 128)
     hipLaunchKernelGGL(gf_elim_blocked_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full)
