@@ -203,3 +203,52 @@ def test_gpu_elimination_c2_round_trip(gpu_ctx):
     gpu_ctx.synchronize()
     gpu_ctx.free(dW)
     gpu_ctx.free(dDec)
+
+
+@pytest.mark.parametrize("k", [32, 48])
+def test_gpu_elimination_many_decoders(gpu_ctx, k):
+    """More decoders than one launch takes (kElimMaxGens = 64, and as many
+    grouped row copies): full dense batches (blocked kernel), {0,1,2}-valued
+    ones (zero diagonals, panel blocks that are singular while C is not: the
+    host route), a panel-local dependence, and a few short batches; every
+    decoder ends as rlnc_decoder_add_pieces leaves it, pieces included."""
+    rng = np.random.default_rng(4242 + k)
+    L = 96
+    G = 70
+    pitch = ((k + L + 15) // 16) * 16
+    gens, bufs, hosts, gpus = [], [], [], []
+    for gi in range(G):
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        n = k + int(rng.integers(0, 3)) if gi % 9 else int(rng.integers(2, k))
+        if gi % 5 == 1:
+            V = rng.integers(0, 3, (n, k), dtype=np.uint8)
+        else:
+            V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        if gi % 7 == 3 and n > 17:  # rows 1..16 equal row 0 on the first 16 columns, up to scale
+            V[1:17, :16] = oracle.matmul(rng.integers(0, 256, (16, 1), dtype=np.uint8), V[:1, :16])[1]
+        rows = np.zeros((n, pitch), np.uint8)
+        rows[:, :k], rows[:, k:k + L] = V, oracle.encode(P, V)
+        d = gpu_ctx.alloc(rows.nbytes)
+        gpu_ctx.h2d(d, rows)
+        gens.append((P, V))
+        bufs.append(d)
+        hosts.append(Dec(gpu_ctx, k))
+        gpus.append(Dec(gpu_ctx, k))
+    counts = (ctypes.c_size_t * G)(*[V.shape[0] for _, V in gens])
+    rows_p = (ctypes.c_void_p * G)(*bufs)
+    decs = (ctypes.c_void_p * G)(*[g.h.value for g in gpus])
+    consumed = (ctypes.c_size_t * G)()
+    status = (ctypes.c_int * G)()
+    errors.check(_lib.lib().rlnc_decoders_add_pieces_gpu(decs, G, rows_p, counts, pitch, L, consumed, status))
+    for gi in range(G):
+        c = ctypes.c_size_t()
+        st = _lib.lib().rlnc_decoder_add_pieces(hosts[gi].h, ctypes.c_void_p(bufs[gi]), counts[gi], pitch, L, 1,
+                                                ctypes.byref(c))
+        assert (status[gi], consumed[gi]) == (st, c.value), gi
+        _same(hosts[gi], gpus[gi])
+        if hosts[gi].state()[3]:
+            s1, a = gpus[gi].get_all()
+            assert s1 == 0 and np.array_equal(a, gens[gi][0]), gi
+    gpu_ctx.synchronize()
+    for d in bufs:
+        gpu_ctx.free(d)
