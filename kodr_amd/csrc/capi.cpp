@@ -1360,6 +1360,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len, ctx->stream));
   }
   if (gpu.empty()) return RLNC_OK;
+  // full batches first: launches of full batches only take the blocked kernel
+  std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return counts[g] >= k; });
   TRY(ctx_elim_tables(ctx));
   const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
   const size_t chunk = std::min<size_t>(gpu.size(), kodr_amd::kElimMaxGens);

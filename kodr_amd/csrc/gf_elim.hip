@@ -280,6 +280,57 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, int src_lane) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(src_lane << 2, (int)v);
 }
 
+// The panel block's Gauss-Jordan, by one wave (all 64 lanes active): the
+// candidates' panel dwords pan[t][d] (written by this wave) -> S in sd, the
+// pivot column of each candidate row jb + t in colof, or fail.
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+__device__ __forceinline__ void panel_gj(ElimBlkLds& lds, int jb, int nb, cu32* tb, int lane) {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes land first
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t P = lds.pan[t][d], Tr = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e++)
+    if (4 * d + e >= nb) P &= ~(0xffu << (8 * e));  // columns past the panel (the last one)
+  if (t < nb && (t >> 2) == d) Tr = 1u << (8 * (t & 3));
+  if (t >= nb) P = 0;
+  uint32_t used = (0xffffu << nb) & 0xffffu;  // rows past k are not candidates
+  int mycol = -1;
+  bool ok = true;
+  for (int c = 0; c < nb; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const bool nz = (d == cd) && ((P >> cb) & 0xffu) != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) {
+      ok = false;
+      break;
+    }
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t dp = (__builtin_amdgcn_readlane(P, pl) >> cb) & 0xffu;
+    cu32* tinv = tb + kElimInvTables + dp * 8;  // tables of inv(dp) (gf256.go:77-86)
+    const uint4 ti = {tinv[0], tinv[1], tinv[2], tinv[3]};
+    const uint32_t ti2 = tinv[4];
+    if (t == tp) {
+      P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
+      Tr = gmul4(ti, ti2, sel0(Tr), sel1(Tr), sel2(Tr));
+      mycol = c;
+    }
+    const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
+    uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
+    if (t == tp) f = 0u;
+    const uint4 tf = lds.tab[2 * f];  // one ds_read_b128 + one ds_read_b32
+    const uint32_t tf2 = lds.tab[2 * f + 1].x;
+    P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
+    Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
+    used |= 1u << tp;
+  }
+  if (!ok) {
+    if (lane == 0) lds.fail = 1;
+  } else if (t < nb) {
+    lds.sd[mycol][d] = Tr;
+    if (d == 0) lds.colof[jb + t] = jb + mycol;
+  }
+}
+
 template <int DPL>
 __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimArgs args) {
   __shared__ ElimBlkLds lds;
@@ -347,50 +398,7 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
         for (int h = 0; h < DPL; h++) lds.prow[i][h * 64 + lane] = R[i][h];
         if (lane >= pl0 && lane < pl0 + 4) lds.pan[i][lane - pl0] = R[i][0];
       }
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's own LDS writes land first
-      const int t = lane >> 2, d = lane & 3;
-      uint32_t P = lds.pan[t][d], Tr = 0;
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (4 * d + e >= nb) P &= ~(0xffu << (8 * e));  // columns past the panel (the last one)
-      if (t < nb && (t >> 2) == d) Tr = 1u << (8 * (t & 3));
-      if (t >= nb) P = 0;
-      uint32_t used = (0xffffu << nb) & 0xffffu;  // rows past k are not candidates
-      int mycol = -1;
-      bool ok = true;
-      for (int c = 0; c < nb; c++) {
-        const int cd = c >> 2, cb = 8 * (c & 3);
-        const bool nz = (d == cd) && ((P >> cb) & 0xffu) != 0u && !((used >> t) & 1u);
-        const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
-        if (m == 0) {
-          ok = false;
-          break;
-        }
-        const int pl = __builtin_ctzll(m), tp = pl >> 2;
-        const uint32_t dp = (__builtin_amdgcn_readlane(P, pl) >> cb) & 0xffu;
-        cu32* tinv = tb + kElimInvTables + dp * 8;  // tables of inv(dp) (gf256.go:77-86)
-        const uint4 ti = {tinv[0], tinv[1], tinv[2], tinv[3]};
-        const uint32_t ti2 = tinv[4];
-        if (t == tp) {
-          P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
-          Tr = gmul4(ti, ti2, sel0(Tr), sel1(Tr), sel2(Tr));
-          mycol = c;
-        }
-        const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
-        uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
-        if (t == tp) f = 0u;
-        const uint4 tf = lds.tab[2 * f];  // one ds_read_b128 + one ds_read_b32
-        const uint32_t tf2 = lds.tab[2 * f + 1].x;
-        P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
-        Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
-        used |= 1u << tp;
-      }
-      if (!ok) {
-        if (lane == 0) lds.fail = 1;
-      } else if (t < nb) {
-        lds.sd[mycol][d] = Tr;
-        if (d == 0) lds.colof[jb + t] = jb + mycol;
-      }
+      panel_gj(lds, jb, nb, tb, lane);
     }
     KODR_STAMP(0);
     __syncthreads();
@@ -501,6 +509,7 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
   if (tid == 0) args.counts[g] = c;
 }
 
+
 }  // namespace
 
 void elim_tables(uint32_t* host_out) {
@@ -562,6 +571,9 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   const bool full = gf_elim_blocked(args, G);
   // (a panel step with DPP/readlane broadcasts instead of ds_bpermute measured
   // slower: 520 vs 493 us at k = 256, profiles/r02/elim/elim_gj_ab.log)
+  // (a row-per-lane layout of the same algorithm -- one LDS gather per
+  // multiplier serving 64 rows, pivot rows as scalars -- measured slower too:
+  // 536 vs 493 us at k = 256, profiles/r02/elim/elim_rows_ab.log)
   if (full && args.k <= 128)
     hipLaunchKernelGGL(gf_elim_blocked_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full)
