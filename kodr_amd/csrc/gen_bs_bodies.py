@@ -48,6 +48,9 @@ PG = RING + 8 * P  # program chunk: 8 rows x 8 targets, lane 8j + m (absolute lo
 PGN = PG + 1       # the next chunk, in flight from LDS
 VMAX = PGN + 1     # first VGPR not used by the asm
 NCOPY = 4
+# body start alignment in bytes (0: packed back to back); the instruction
+# fetch after each s_setpc starts at the body's first byte
+ALIGN = int(os.environ.get("KODR_BS_ALIGN", "0"))
 # SGPRs: T[0..4] = s[60:69] (T[0] entry, T[r+1] the tail of copy r), the
 # second half's targets s[70:77], the stub s[78:79], this row's return
 # address s[80:81], the 8 rows' return addresses s[82:97]
@@ -122,6 +125,8 @@ def body_offsets():
     offs, off = [], 0
     for _r in range(NCOPY):
         for c in range(256):
+            if ALIGN:
+                off = (off + ALIGN - 1) // ALIGN * ALIGN
             offs.append(off)
             off += body_bytes(c)
     return offs, off
@@ -383,6 +388,8 @@ def main():
     n_inst = 0
     for r in range(NCOPY):
         for c in range(256):
+            if ALIGN:
+                bodies.append(f".p2align {ALIGN.bit_length() - 1}")
             bodies.append(f".Lbs_b{r}_{c}_%=:")
             lines = body_lines(c, r)
             n_inst += len(lines) - 1
@@ -390,7 +397,7 @@ def main():
     out += emit("KODR_BS_BODIES", bodies)
     offs, total = body_offsets()
     out.append(f"#define KODR_BS_CODE_BYTES {total}")
-    out.append(f"#define KODR_BS_COPY_BYTES {total // NCOPY}u")
+    out.append(f"#define KODR_BS_COPY_BYTES {offs[256]}u")
     out.append("static const uint32_t kBsBodyOffsets[%d] = {" % len(offs))
     for i in range(0, len(offs), 16):
         out.append("  " + ", ".join(str(o) for o in offs[i:i + 16]) + ",")
