@@ -559,6 +559,10 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
     return launch<4, 8, 2, 32, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   if (mode == 2 && g.mt == 8 && g.kw == 4 && g.s == 1)
     return launch<8, 4, 1, 64, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 1 && g.mt == 1 && g.kw == 16 && g.s == 2)
+    return launch<1, 16, 2, 16, 8, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
+  if (mode == 2 && g.mt == 1 && g.kw == 16 && g.s == 2)
+    return launch<1, 16, 2, 16, 8, 2>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
 #endif
   (void)mode;
   // grouped launches stream G generations once each per launch: nt loads
