@@ -130,7 +130,10 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32, help="coded pieces per encode pass")
-    ap.add_argument("--gens", type=int, default=16, help="rotating resident generations (HBM-cold)")
+    ap.add_argument("--gens", type=int, default=16, help="resident generations (512 MiB: HBM-cold)")
+    ap.add_argument("--per-generation", action="store_true",
+                    help="one launch per generation per step (rounds 1-2 headline) instead of one grouped launch "
+                         "over all resident generations")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
@@ -189,14 +192,26 @@ def main():
     ctx.synchronize()
     construct_ms = (time.perf_counter() - tc0) * 1e3 / G
     del datas
-    nvec = 64
-    V = rng.integers(0, 256, (nvec, B, k), dtype=np.uint8)
+    # A step: B coded pieces of every resident generation (full/encoder.go:61-71
+    # B times per generation, vectors drawn per piece), as ONE grouped launch
+    # (rlnc_encoder_group_coded_pieces_device: the launch and the kernel's ramp
+    # and tail are paid once per G generations, each generation read once).
+    # --per-generation: one launch per generation, rotating over the G.
+    grouped = not args.per_generation
+    per_step = G if grouped else 1            # generations per step
+    nvec = 8 if grouped else 64
+    V = rng.integers(0, 256, (nvec, per_step, B, k), dtype=np.uint8)
     dV = ctx.alloc(V.nbytes)
     ctx.h2d(dV, V)
-    dOut = ctx.alloc(B * L)
+    dOut = ctx.alloc(per_step * B * L)
+    enc_arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
 
     def step(i):
-        errors.check(L_.rlnc_encoder_coded_pieces_device(encs[i % G], dV + (i % nvec) * B * k, B, dOut, L))
+        dv = dV + (i % nvec) * per_step * B * k
+        if grouped:
+            errors.check(L_.rlnc_encoder_group_coded_pieces_device(enc_arr, G, dv, B, dOut, L))
+        else:
+            errors.check(L_.rlnc_encoder_coded_pieces_device(encs[i % G], dv, B, dOut, L))
 
     def barrier():
         ctx.synchronize()
@@ -206,7 +221,8 @@ def main():
 
     # W warmup steps, but never fewer than one pass over the G generations, so
     # no generation is first touched inside the timed region
-    for i in range(max(args.warmup, G)):
+    n_warm = max(args.warmup, 1 if grouped else G)
+    for i in range(n_warm):
         step(i)
     barrier()
     e0, e1 = ctx.event(), ctx.event()
@@ -222,7 +238,7 @@ def main():
     t_max = kdist.max_over_ranks(t_local, device="cuda")
 
     unit_bytes = setbytes(k, L)
-    value = kdist.aggregate_rate(args.steps * B, unit_bytes, t_max, world)
+    value = kdist.aggregate_rate(args.steps * per_step * B, unit_bytes, t_max, world)
     t_launch = t_local / args.steps
     # Roofline of the dominant kernel, per launch (one launch = one step):
     #  hbm:   the bytes a launch must move -- the generation once, B vectors
@@ -231,10 +247,10 @@ def main():
     #         piece, so it is not an HBM byte count: B pieces share one read.)
     #  issue: GF MACs per second against the VALU floor of the bit-sliced
     #         method, the bound that binds at B >= 9 (Roofline).
-    algo_bytes = B * unit_bytes
-    compulsory = k * L + B * k + B * L
+    algo_bytes = per_step * B * unit_bytes
+    compulsory = per_step * (k * L + B * k + B * L)
     achieved = compulsory / t_launch / 1e9
-    macs = B * k * L
+    macs = per_step * B * k * L
     bs = B >= 9
 
     extras = {"construct_ms_per_generation": round(construct_ms, 3)}
@@ -268,22 +284,29 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded uniform random bytes and coding vectors)",
             "config": {"workload": "Full RLNC encode, 32 MiB generation / 256 pieces (BASELINE configs[1]); "
-                                   "the decode leg (configs[2]) is extras.c2_decode",
-                       "piece_count": k, "piece_size": L, "coded_pieces_per_step": B,
+                                   + (f"a step = {B} coded pieces of each of the {G} resident generations in one "
+                                      "grouped launch" if grouped else
+                                      f"a step = {B} coded pieces of one generation (rotating over {G})")
+                                   + "; the decode leg (configs[2]) is extras.c2_decode",
+                       "piece_count": k, "piece_size": L, "coded_pieces_per_generation_per_step": B,
+                       "generations_per_step": per_step, "coded_pieces_per_step": per_step * B,
                        "resident_generations": G, "parallelism": f"generation-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(B, k, L),
+                         "traffic": pmc_traffic(B, k, L, per_step),
                          "kernel": "gf_bs_kernel" if bs else "gf_gemm_kernel",  # capi.cpp kBsMinRows
+                         "traffic_source": pmc_traffic_file(B, k, L, per_step),
                          "hbm_bytes_per_launch": compulsory,
                          "avg_launch_us": round(t_launch * 1e6, 3),
+                         "warmup_launches": n_warm, "generations_per_launch": per_step,
                          "issue": {"achieved_gf_macs_per_s": float(f"{macs / t_launch:.4g}"),
                                    "peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
                                    "frac": round(macs / t_launch / VALU_FLOOR_MACS_PER_S, 4) if bs else None,
                                    "gf_macs_per_launch": macs},
                          "kodr_setbytes_per_launch": algo_bytes,
-                         "note": "achieved/frac: the launch's compulsory HBM bytes (generation once + B vectors + "
-                                 "B pieces) / launch time / 8 TB/s; traffic: PMC-measured HBM bytes per launch "
+                         "note": "achieved/frac: the launch's compulsory HBM bytes (per generation: the generation "
+                                 "once + B vectors + B pieces) / launch time / 8 TB/s; traffic: PMC-measured HBM "
+                                 "bytes per launch "
                                  "(profiles/, FETCH_SIZE x2 + WRITE_SIZE); issue: GF MACs/s against the "
                                  "bit-sliced method's VALU floor (8 XOR3 + 26/8 table instructions per "
                                  "coefficient per 2 KiB at 2.3 cycles per wave instruction on 1024 SIMDs), "
@@ -298,11 +321,16 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(B, k, L):
+def pmc_traffic_file(B, k, L, G=1):
+    name = f"pmc_traffic_B{B}_k{k}_L{L}.json" if G == 1 else f"pmc_traffic_G{G}_B{B}_k{k}_L{L}.json"
+    return "profiles/" + name
+
+
+def pmc_traffic(B, k, L, G=1):
     """HBM bytes per launch of this exact configuration, from the committed
-    rocprofv3 --pmc summary (tools/pmc_traffic.sh: separate FETCH_SIZE and
+    rocprofv3 --pmc summary (tools/profile_bench.sh: separate FETCH_SIZE and
     WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM)."""
-    path = os.path.join(ROOT, "profiles", f"pmc_traffic_B{B}_k{k}_L{L}.json")
+    path = os.path.join(ROOT, pmc_traffic_file(B, k, L, G))
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -556,21 +584,23 @@ def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
     from kodr_amd import device as kdev
     G = len(encs)
     arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
-    res = {"generations_per_launch": G, "kernel": "gf_gemm_kernel (grouped)"}
+    res = {"generations_per_launch": G}
     e0, e1 = ctx.event(), ctx.event()
-    for count in (1, 2, 4, 8):
+    for count in (1, 2, 4, 8, 16, 32, 64):
+        iters_c = iters if count <= 8 else 10
         V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
         dV, dO = ctx.alloc(V.nbytes), ctx.alloc(G * count * L)
         ctx.h2d(dV, V)
         for i in range(5):
             errors.check(L_.rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, L))
         ctx.record(e0)
-        for i in range(iters):
+        for i in range(iters_c):
             errors.check(L_.rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, L))
         ctx.record(e1)
-        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters
+        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters_c
         hbm = G * (k * L + count * (k + L))
-        res[str(count)] = {"us_per_launch": round(t * 1e6, 2), "us_per_generation": round(t / G * 1e6, 3),
+        res[str(count)] = {"kernel": "gf_bs_kernel (grouped)" if count >= 9 else "gf_gemm_kernel (grouped)",
+                           "us_per_launch": round(t * 1e6, 2), "us_per_generation": round(t / G * 1e6, 3),
                            "coded_MBps": round(G * count * setbytes(k, L) / t / 1e6, 1),
                            "hbm_GBps": round(hbm / t / 1e9, 1),
                            "hbm_frac": round(hbm / t / 1e9 / HBM_PEAK_GBS, 4)}

@@ -735,6 +735,24 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
   bool grouped = !resident_uses_bs(ctx, count, k, e0->pitch, L) && k * e0->pitch < kMaxDescBytes &&
                  (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
   for (size_t i = 0; i < n_enc && grouped; i++) grouped = !encs[i]->compact;  // the grouped launch reads plain rows
+  // larger batches: one bit-sliced launch per kGemmGroupMax generations over
+  // their twins, when the product is a single row chunk
+  bool grouped_bs = !grouped && resident_uses_bs(ctx, count, k, e0->pitch, L) &&
+                    bs_chunk_rows(count, k, e0->pitch, L) >= k && (out_pitch % 16) == 0;
+  if (grouped_bs) {
+    for (size_t i = 0; i < n_enc; i++)
+      if (!encs[i]->compact)
+        TRY(build_twin(ctx, encs[i]->pieces.p, encs[i]->pieces_bs, encs[i]->bs_valid, k, e0->pitch, L));
+    const uint8_t* xs[kodr_amd::kGemmGroupMax];
+    for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
+      const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
+      for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces_bs.p;
+      const kodr_amd::GemmGroupArgs grp{(int)n, xs, vstride, ostride};
+      HIPC(kodr_amd::gf_gemm_bs(d_vectors + g0 * vstride, k, count, k, xs[0], e0->pitch, d_out + g0 * ostride,
+                                out_pitch, L, ctx->device, ctx->stream, false, &grp));
+    }
+    return RLNC_OK;
+  }
   if (!grouped) {
     for (size_t i = 0; i < n_enc; i++)
       TRY(rlnc_encoder_coded_pieces_device(encs[i], d_vectors + i * vstride, count, d_out + i * ostride, out_pitch));

@@ -158,11 +158,19 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ uint32_t* g_bs_prog = nullptr;  // MODE 14's program scratch (tuning builds only)
 #endif
 
-template <int KW, int MODE = 0>
+// Products of one shape over several resident generations in one launch
+// (GRP): blockIdx.y = generation g reads X = x[g], A + g * a_stride and
+// writes Y + g * y_stride.
+struct BsGroupK {
+  const uint8_t* x[kGemmGroupMax];
+  size_t a_stride, y_stride;
+};
+
+template <int KW, int MODE = 0, bool GRP = false>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
-    const uint32_t* __restrict__ tgt, uint32_t thi, int accum) {
+    const uint32_t* __restrict__ tgt, uint32_t thi, int accum, const BsGroupK grp) {
   // LDS: [0, 16 KiB) per-row XOR sums [8 rows x 8 planes][64 lanes];
   // [16, 17 KiB) the body target table (absolute lo words of copy 0; copy r
   // is r * KODR_BS_COPY_BYTES further); then each wave's program: per input
@@ -177,6 +185,12 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       reinterpret_cast<uint32_t*>(Y)[1] = (uint32_t)(pc >> 32);
     }
     return;
+  }
+  if constexpr (GRP) {
+    const int g = blockIdx.y;
+    A += (size_t)g * grp.a_stride;
+    X = grp.x[g];
+    Y += (size_t)g * grp.y_stride;
   }
   uint32_t* red = lds;
   uint32_t* tgt_l = lds + 64 * 64;
@@ -500,7 +514,7 @@ hipError_t bs_init(int dev, const BsDevice** out) {
     // where gf_bs_kernel runs means the export is wrong, and jumping there
     // would fault
     hipLaunchKernelGGL((gf_bs_kernel<1, 0>), dim3(1), dim3(64), 0, 0, nullptr, 0, 0, 0, nullptr, 0,
-                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u, 0);
+                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u, 0, BsGroupK{});
     if ((e = hipGetLastError()) == hipSuccess) e = hipDeviceSynchronize();
     uint32_t kpc[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpy(kpc, buf, sizeof(kpc), hipMemcpyDeviceToHost);
@@ -534,10 +548,21 @@ hipError_t bs_init(int dev, const BsDevice** out) {
 template <int KW, int MODE = 0>
 hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, int ldx, uint8_t* Y,
                      size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes, const BsDevice* bd,
-                     hipStream_t st, int accum) {
+                     hipStream_t st, int accum, const GemmGroupArgs* group) {
   const int nb = (ncx + 7) / 8 * 8 * nrg;
-  hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
-                     ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum);
+  BsGroupK g{};
+  if (group) {
+    for (int i = 0; i < group->n; i++) g.x[i] = group->x[i];
+    g.a_stride = group->a_stride;
+    g.y_stride = group->y_stride;
+    // gridDim.x is a multiple of 8, so the XCD order of each generation's
+    // blocks is the single-generation one
+    hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A, lda, M,
+                       K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+  } else {
+    hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
+                       ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+  }
   return hipGetLastError();
 }
 
@@ -620,11 +645,11 @@ size_t bs_lds_bytes(int kw, int rpw) {
 
 }  // namespace
 
-BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
+BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups) {
   BsPlan p;
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
   p.nrg = (int)((M + kBsRows - 1) / kBsRows);
-  const long tasks = (long)p.ncx * p.nrg;
+  const long tasks = (long)p.ncx * p.nrg * std::max(groups, 1);
   constexpr long P = kBsChunk;  // rows per wave: whole program chunks
   const long kpad = ((long)K + P - 1) / P * P;
   // cost model in row-units: rounds of resident waves x (rows per wave + the
@@ -653,12 +678,14 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols) {
 }
 
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
-                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream, bool accumulate) {
-  if (M == 0 || ncols == 0) return hipSuccess;
+                      uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream, bool accumulate,
+                      const GemmGroupArgs* group) {
+  if (M == 0 || ncols == 0 || (group && group->n <= 0)) return hipSuccess;
+  if (group && group->n > kGemmGroupMax) return hipErrorInvalidValue;
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
     return hipErrorInvalidValue;
-  BsPlan p = plan_gemm_bs(M, K, ncols);
+  BsPlan p = plan_gemm_bs(M, K, ncols, group ? group->n : 1);
   if (!p.ok) return hipErrorInvalidValue;
 #ifdef KODR_TUNE_MODES
   if (const char* env = getenv("KODR_BS_KW")) {  // force the waves per workgroup
@@ -691,7 +718,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
   bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream, \
-                          accumulate ? 1 : 0)
+                          accumulate ? 1 : 0, group)
 #ifdef KODR_TUNE_MODES
 #define KODR_BS_CASE(KW_)                                                                         \
   case KW_:                                                                                       \

@@ -137,11 +137,14 @@ struct BsPlan {
   size_t lds_bytes = 0;  // per workgroup: row sums, offset table, programs
   bool ok = false;       // false when K is too large for the LDS program
 };
-BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols);
+// groups: independent products of this shape in one launch (grid rows)
+BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups = 1);
 
-// Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.
+// Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.  group:
+// up to kGemmGroupMax products of this shape in one launch (X = group->x[i],
+// A + i * a_stride, Y + i * y_stride; dXbs unused).
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
                       uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream,
-                      bool accumulate = false);
+                      bool accumulate = false, const GemmGroupArgs* group = nullptr);
 
 }  // namespace kodr_amd

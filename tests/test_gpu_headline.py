@@ -7,7 +7,8 @@ full/recoder.go:27-46):
   the sweep's), every byte of every piece;
 - the grouped multi-generation launch (rlnc_encoder_group_coded_pieces_device,
   the north-star leg): every generation's pieces, small shapes, more than one
-  launch's worth of generations, the bit-sliced fallback, C2-sized generations;
+  launch's worth of generations, the grouped bit-sliced launch (count >= 9),
+  C2-sized generations;
 - a prepared recoder at C2 (the bench's recode leg).
 """
 import ctypes
@@ -121,11 +122,13 @@ def group_run(ctx, gens, count, V, out_pitch=None, expect=0):
 
 @pytest.mark.parametrize("G,k,L,count", [(1, 16, 4096, 1), (3, 16, 4096 + 16, 2), (5, 100, 8192 + 48, 1),
                                          (8, 256, 65536, 4), (40, 32, 1024, 1), (33, 64, 2048, 8),
-                                         (6, 64, 4096, 12), (4, 20, 1000, 3)])
+                                         (6, 64, 4096, 12), (4, 20, 1000, 3), (35, 64, 2048, 9),
+                                         (5, 100, 8192 + 48, 40), (3, 300, 4096, 17)])
 def test_grouped_encode_vs_oracle(gpu_ctx, G, k, L, count):
-    # (40, ...) and (33, ...) span two launches of <= 32 generations; count 12
-    # takes the per-generation (bit-sliced) fallback; L = 1000 is not a
-    # multiple of 16 (ragged last chunk, padded pitch)
+    # (40, ...) and (33, ...) span two launches of <= 32 generations; count >= 9
+    # takes the grouped bit-sliced launch ((35, ...) over two launches, k = 100
+    # and 300 with a ragged last program chunk); L = 1000 is not a multiple of
+    # 16 (ragged last chunk, padded pitch)
     rng = np.random.default_rng(G * 1000 + k + count)
     gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
     V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
@@ -143,6 +146,40 @@ def test_grouped_encode_c2_generations(gpu_ctx):
     got = group_run(gpu_ctx, gens, 1, V)
     for g in range(4):
         assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
+def test_grouped_bitsliced_c2_generations(gpu_ctx, c2_generation):
+    # 32 coded pieces of each of 3 generations of 32 MiB / 256 in one
+    # bit-sliced launch (the headline's batch, grouped); one generation is
+    # compact (twin only) and one prepared, one builds its twin in the call
+    rng = np.random.default_rng(0x6B32)
+    gens = [c2_generation, rng.integers(0, 256, (256, 131072), dtype=np.uint8),
+            rng.integers(0, 256, (256, 131072), dtype=np.uint8)]
+    G, count, k, L = 3, 32, 256, 131072
+    V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+    V[1, 0] = 0
+    V[2, 3] = 0
+    V[2, 3, 255] = 1
+    encs = [make_encoder(gpu_ctx, P, prepare=(i == 1)) for i, P in enumerate(gens)]
+    errors.check(_lib.lib().rlnc_encoder_compact(encs[0]))
+    arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    dV, dO = gpu_ctx.alloc(V.nbytes), gpu_ctx.alloc(G * count * L + 64)
+    try:
+        gpu_ctx.h2d(dV, V)
+        gpu_ctx.h2d(dO + G * count * L, np.full(64, 0xA5, np.uint8))
+        errors.check(_lib.lib().rlnc_encoder_group_coded_pieces_device(arr, G, dV, count, dO, L))
+        gpu_ctx.synchronize()
+        got = gpu_ctx.d2h(dO, G * count * L + 64)
+    finally:
+        gpu_ctx.free(dV)
+        gpu_ctx.free(dO)
+        for e in encs:
+            _lib.lib().rlnc_encoder_destroy(e)
+    assert (got[G * count * L:] == 0xA5).all()
+    got = got[:G * count * L].reshape(G, count, L)
+    for g in range(G):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+    assert not got[1, 0].any() and np.array_equal(got[2, 3], gens[2][255])
 
 
 def test_grouped_encode_rejects_mixed_shapes(gpu_ctx):

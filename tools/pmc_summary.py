@@ -12,6 +12,8 @@ import sys
 
 out, B = sys.argv[1], int(sys.argv[2])
 KERNEL = sys.argv[3] if len(sys.argv) > 3 else ("gf_bs_kernel" if B >= 16 else "gf_gemm_kernel")
+# the library's one-workgroup probe launch of the same template is not a product
+MIN_GRID = int(sys.argv[4]) if len(sys.argv) > 4 else 64 * 64
 
 
 def rows(pattern):
@@ -20,11 +22,13 @@ def rows(pattern):
 
 
 dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows("trace/**/*kernel_trace.csv")
-       if KERNEL in r["Kernel_Name"]]
+       if KERNEL in r["Kernel_Name"] and int(r.get("Grid_Size_X", MIN_GRID)) >= MIN_GRID]
 fetch = [float(r["Counter_Value"]) for r in rows("fetch/**/*counter_collection.csv")
-         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"
+         and int(r.get("Grid_Size", MIN_GRID)) >= MIN_GRID]
 write = [float(r["Counter_Value"]) for r in rows("write/**/*counter_collection.csv")
-         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"]
+         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"
+         and int(r.get("Grid_Size", MIN_GRID)) >= MIN_GRID]
 res = {
     "batch": B,
     "kernel": KERNEL,

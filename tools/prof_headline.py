@@ -40,7 +40,7 @@ def main():
     # the headline group: the first (kernel, grid) group of the headline
     # kernel with at least the warmup + timed launches (the library's one-off
     # probe launch of the same template comes earlier, on a one-wave grid)
-    nwarm = max(a.warm, a.gens)
+    nwarm = line["roofline"].get("warmup_launches", max(a.warm, a.gens))
     head_key = next(k for k, v in groups.items()
                     if (kname + "<" in k[0] or k[0].endswith(kname)) and len(v) >= nwarm + a.steps)
     first = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
