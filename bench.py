@@ -219,11 +219,19 @@ def main():
             dist.barrier()
         ctx.synchronize()
 
-    # W warmup steps, but never fewer than one pass over the G generations, so
-    # no generation is first touched inside the timed region
-    n_warm = max(args.warmup, 1 if grouped else G)
-    for i in range(n_warm):
-        step(i)
+    # W warmup steps, but never fewer than one pass over the G generations (no
+    # generation is first touched inside the timed region) and never less than
+    # WARM_S of back-to-back work: after a load step the MI355X's clocks dip
+    # for ~30 ms (a grouped launch goes 242 -> 338 -> 230 us,
+    # profiles/r02/warm/), so the timed steps start at the sustained rate
+    # whatever --warmup says
+    n_warm = 0
+    tw0 = time.perf_counter()
+    while n_warm < max(args.warmup, 1 if grouped else G) or (time.perf_counter() - tw0 < WARM_S and n_warm < 20000):
+        step(n_warm)
+        n_warm += 1
+        if n_warm % 8 == 0:
+            ctx.synchronize()      # keep the host's clock on the device's work
     barrier()
     e0, e1 = ctx.event(), ctx.event()
     t0 = time.perf_counter()
@@ -319,6 +327,9 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+WARM_S = 0.08
 
 
 def pmc_traffic_file(B, k, L, G=1):
