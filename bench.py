@@ -556,6 +556,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["c2_decode"]["roundtrip_ok"] = bool(np.array_equal(a, b))
     ctx.free(dWire)
     ctx.free(dDec)
+    out["c2_decode_grouped"] = c2_decode_grouped(ctx, L_, errors, encs, k, L)
     out["north_star_grouped_encode"] = grouped_encode(ctx, L_, errors, encs, k, L, rng)
     out["c2_recode"] = recode_c2(ctx, L_, errors, encs[0], k, L, rng)
     out["c5_encode_recode_one_gpu"] = c5_one_gpu(ctx, L_, errors, encs[:8], k, L, rng)
@@ -698,6 +699,64 @@ def c5_one_gpu(ctx, L_, errors, encs, k, L, rng, reps=3):
             "coded_plus_recoded_MBps": round(units / best / 1e6, 1),
             "note": "per generation: k encoded + k recoded pieces, kodr SetBytes units for both; host wall time, "
                     "recoder construction (D2D copy of the received rows + twin) included"}
+
+
+def c2_decode_grouped(ctx, L_, errors, encs, k, L, reps=3):
+    """BASELINE configs[2] over many generations: each of the G resident
+    generations' encoders writes k + 2 coded wire rows (device-drawn vectors),
+    then G fresh decoders take them in ONE batched AddPiece call
+    (rlnc_decoders_add_pieces_gpu: one elimination launch) and ONE grouped
+    GetPieces call (rlnc_decoders_get_pieces_device: one bit-sliced launch).
+    Wall time per generation, decoder construction outside the timed region
+    (as kodr's decoder bench, benches/full/decoder_test.go); outputs checked
+    against the generations' resident pieces."""
+    import ctypes
+    import numpy as np
+    G, n, W = len(encs), k + 2, k + L
+    wires = []
+    for g, e in enumerate(encs):
+        L_.rlnc_encoder_seed(e, 1000 + g)
+        dw = ctx.alloc(n * W)
+        errors.check(L_.rlnc_encoder_coded_wire_device(e, n, dw, W))
+        wires.append(dw)
+    dO = ctx.alloc(G * k * L)
+    best, ok = None, True
+    for rep in range(reps):
+        decs = []
+        for g in range(G):
+            h = ctypes.c_void_p()
+            errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+            decs.append(h)
+        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+        errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, (ctypes.c_void_p * G)(*wires),
+                                                     (ctypes.c_size_t * G)(*([n] * G)), W, L, cons, sts))
+        t1 = time.perf_counter()
+        errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, dO, L))
+        ctx.synchronize()
+        t2 = time.perf_counter()
+        ok = ok and all(s_ in (0, 3) for s_ in sts) and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
+        for x in decs:
+            L_.rlnc_decoder_destroy(x)
+        if best is None or t2 - t0 < best[0]:
+            best = (t2 - t0, t1 - t0, t2 - t1)
+    pitch = ctypes.c_size_t()
+    for g in (0, G - 1):
+        dp = L_.rlnc_encoder_device_pieces(encs[g], ctypes.byref(pitch))
+        a = ctx.d2h(dO + g * k * L, k * L)
+        b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
+        ok = ok and bool(np.array_equal(a, b))
+    for d in wires:
+        ctx.free(d)
+    ctx.free(dO)
+    t, ta, tg = best
+    return {"generations": G, "ms": round(t * 1e3, 3), "add_ms": round(ta * 1e3, 3), "get_ms": round(tg * 1e3, 3),
+            "us_per_generation": round(t / G * 1e6, 1),
+            "MBps_decodable_len": round(G * k * (k + L) / t / 1e6, 1),
+            "gf_macs_per_s": float(f"{G * k * k * L / t:.4g}"), "roundtrip_ok": ok,
+            "note": "wall time of one batched AddPiece + one grouped GetPieces over G generations"}
 
 
 def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):

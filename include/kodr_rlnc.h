@@ -268,6 +268,16 @@ int rlnc_decoder_get_piece(rlnc_decoder* dec, size_t index, uint8_t* out);
 int rlnc_decoder_get_pieces(rlnc_decoder* dec, uint8_t* out);
 /* GetPieces into device memory: useful rows of L bytes at out_pitch (async) */
 int rlnc_decoder_get_pieces_device(rlnc_decoder* dec, uint8_t* d_out, size_t out_pitch);
+/* GetPieces of G decoded generations (one context, one piece_count and
+ * piece_len) into device memory: d_out holds G blocks of piece_count rows at
+ * out_pitch (decoder g's first row at g*piece_count*out_pitch).  When every
+ * decoder received the same number of pieces and none holds a systematic
+ * (unit) row, ONE bit-sliced launch per 16 decoders applies their T x R
+ * products (the host stages the next 16 transforms while it runs); other
+ * decoders take rlnc_decoder_get_pieces_device one by one.  Same bytes
+ * either way.  RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED if any decoder is
+ * not decoded (nothing is written).  Async on the ctx stream. */
+int rlnc_decoders_get_pieces_device(rlnc_decoder* const* decs, size_t G, uint8_t* d_out, size_t out_pitch);
 /* introspection of the mirrored decoder state (decoder_state.go:192-200):
  * coefficient matrix (useful x piece_count) and the transform T
  * (useful x received) with coded rows == T x received pieces */

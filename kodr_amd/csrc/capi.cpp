@@ -1523,6 +1523,79 @@ int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_p
   return dec_apply(d, rows, d->hT.data(), d_out, out_pitch);  // T is staged; no host buffer outlives the call
 }
 
+// GetPieces of G decoded generations, kGroupGetChunk decoders per launch:
+// when a chunk's transforms are all coded-only (no unit row), the received
+// counts agree and the product takes the bit-sliced kernel, the chunk's T
+// are staged in one upload and applied by ONE gf_bs_kernel launch (grid row =
+// decoder); otherwise that chunk goes decoder by decoder.  Launches are
+// asynchronous, so the host's T preparation for chunk c + 1 overlaps chunk
+// c's kernel; the T upload itself sits in the stream between launches
+// (~25 us per chunk, profiles/r02/group_get/), hence chunks of 16.
+constexpr size_t kGroupGetChunk = 16;
+
+int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* d_out, size_t out_pitch) {
+  if (!ds || !G || !d_out || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_decoder* d0 = ds[0];
+  for (size_t g = 0; g < G; g++) {
+    rlnc_decoder* d = ds[g];
+    if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+    if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
+    if (!d->ctx) return RLNC_ERR_NO_DEVICE;
+    if (d->ctx != d0->ctx || d->L != d0->L || d->core.piece_count() != d0->core.piece_count())
+      return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  const size_t L = d0->L, rows = d0->core.rank(), recv = d0->core.received(), pitch = d0->pitch;
+  if (out_pitch < L || out_pitch % 16) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(d0->ctx));
+  rlnc_ctx* ctx = d0->ctx;
+  const size_t ostride = rows * out_pitch, tsz = rows * recv;
+  const bool bs = G > 1 && rows >= kBsMinRows && !few_narrow_rows(rows, recv, L) && (pitch % 32) == 0 &&
+                  bs_chunk_rows(rows, std::max<size_t>(recv, 1), pitch, L) >= recv && kodr_amd::bs_ready(ctx->device);
+  if (!bs) {
+    for (size_t g = 0; g < G; g++) TRY(rlnc_decoder_get_pieces_device(ds[g], d_out + g * ostride, out_pitch));
+    return RLNC_OK;
+  }
+  TRY(d0->tmat.reserve(G * tsz));
+  std::vector<uint8_t> hT(kGroupGetChunk * tsz);
+  const uint8_t* xs[kGroupGetChunk];
+  for (size_t g0 = 0; g0 < G; g0 += kGroupGetChunk) {
+    const size_t n = std::min(kGroupGetChunk, G - g0);
+    bool grouped = n > 1;
+    for (size_t i = 0; i < n && grouped; i++) {
+      rlnc_decoder* d = ds[g0 + i];
+      grouped = d->core.received() == recv && d->core.rank() == rows && d->pitch == pitch;
+      if (!grouped) break;
+      uint8_t* t = hT.data() + i * tsz;
+      d->core.copy_transform(t, recv);
+      for (size_t r = 0; r < rows && grouped; r++, t += recv) {  // a unit row is a copy: per-decoder route
+        size_t nz = 0, last = 0;
+        for (size_t j = 0; j < recv && nz < 2; j++)
+          if (t[j]) nz++, last = j;
+        grouped = !(nz == 1 && t[last] == 1);
+      }
+    }
+    if (!grouped) {
+      for (size_t i = 0; i < n; i++)
+        TRY(rlnc_decoder_get_pieces_device(ds[g0 + i], d_out + (g0 + i) * ostride, out_pitch));
+      continue;
+    }
+    for (size_t i = 0; i < n; i++) {
+      rlnc_decoder* d = ds[g0 + i];
+      TRY(dec_extend_twin(d));
+      d->last_gf_rows = rows;
+      d->last_copy_rows = 0;
+      d->last_bs = true;
+      xs[i] = d->recv_bs.p;
+    }
+    uint8_t* dT = d0->tmat.p + g0 * tsz;
+    HIPC(ctx->stage.h2d(dT, n * tsz, hT.data(), n * tsz, n * tsz, 1, ctx->stream));
+    const kodr_amd::GemmGroupArgs grp{(int)n, xs, tsz, ostride};
+    HIPC(kodr_amd::gf_gemm_bs(dT, recv, rows, recv, xs[0], pitch, d_out + g0 * ostride, out_pitch, L, ctx->device,
+                              ctx->stream, false, &grp));
+  }
+  return RLNC_OK;
+}
+
 int rlnc_decoder_apply_stats(const rlnc_decoder* d, size_t* gf_rows, size_t* copy_rows) {
   if (!d || !gf_rows || !copy_rows) return RLNC_ERR_INVALID_ARGUMENT;
   *gf_rows = d->last_gf_rows;
