@@ -560,6 +560,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["north_star_grouped_encode"] = grouped_encode(ctx, L_, errors, encs, k, L, rng)
     out["c2_recode"] = recode_c2(ctx, L_, errors, encs[0], k, L, rng)
     out["c5_encode_recode_one_gpu"] = c5_one_gpu(ctx, L_, errors, encs[:8], k, L, rng)
+    out["c5_encode_recode_one_gpu_grouped"] = c5_one_gpu_grouped(ctx, L_, errors, encs[:8], k, L, rng)
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
     out["batched_decode_elimination"] = batched_elim(ctx, L_, errors, rng)
     out["c1_roundtrip"] = c1_roundtrip(ctx, L_, errors, rng)
@@ -699,6 +700,92 @@ def c5_one_gpu(ctx, L_, errors, encs, k, L, rng, reps=3):
             "coded_plus_recoded_MBps": round(units / best / 1e6, 1),
             "note": "per generation: k encoded + k recoded pieces, kodr SetBytes units for both; host wall time, "
                     "recoder construction (D2D copy of the received rows + twin) included"}
+
+
+def c5_one_gpu_grouped(ctx, L_, errors, encs, k, L, rng, reps=3):
+    """c5_one_gpu with grouped launches: k coded pieces of all 8 generations
+    in ONE encode launch (rlnc_encoder_group_coded_pieces_device, written into
+    the pieces' columns of the wire rows), a recoder per generation on its
+    rows, and k recoded pieces of all 8 in ONE recode launch
+    (rlnc_recoder_group_coded_pieces_device).  The coding vectors are random
+    host bytes uploaded before the timed region, into both the contiguous
+    vector block and the wire rows (64 KiB per generation); the recoded
+    output is checked against the oracle for one generation."""
+    import ctypes
+    import numpy as np
+    clen = k + L
+    pitch = (clen + 255) // 256 * 256
+    G = len(encs)
+    V = rng.integers(0, 256, (G, k, k), dtype=np.uint8)
+    R = rng.integers(0, 256, (G, k, k), dtype=np.uint8)
+    dV, dR = ctx.alloc(V.nbytes), ctx.alloc(R.nbytes)
+    ctx.h2d(dV, V)
+    ctx.h2d(dR, R)
+    dW, dO = ctx.alloc(G * k * pitch), ctx.alloc(G * k * pitch)
+    wire = np.zeros((G * k, pitch), np.uint8)
+    wire[:, :k] = V.reshape(G * k, k)
+    ctx.h2d(dW, wire)
+    del wire
+    earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    best = None
+    for rep in range(reps):
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        errors.check(L_.rlnc_encoder_group_coded_pieces_device(earr, G, dV, k, dW + k, pitch))
+        recs = []
+        for g in range(G):
+            rh = ctypes.c_void_p()
+            errors.check(L_.rlnc_recoder_create_device(ctx.handle, dW + g * k * pitch, k, clen, pitch, k,
+                                                       ctypes.byref(rh)))
+            recs.append(rh)
+        errors.check(L_.rlnc_recoder_group_coded_pieces_device((ctypes.c_void_p * G)(*[r.value for r in recs]), G,
+                                                               dR, k, dO, pitch))
+        ctx.synchronize()
+        t = time.perf_counter() - t0
+        for rh in recs:
+            L_.rlnc_recoder_destroy(rh)
+        best = t if best is None else min(best, t)
+    # generation G-1, recoded rows 0 and k-1: vector part = R x V, and the row
+    # is a codeword of the generation (piece = vector x P), numpy GF(2^8)
+    pp = ctypes.c_size_t()
+    dp = L_.rlnc_encoder_device_pieces(encs[G - 1], ctypes.byref(pp))
+    ok = None
+    if dp:
+        P = ctx.d2h(dp, k * pp.value).reshape(k, pp.value)[:, :L]
+        got = ctx.d2h(dO + (G - 1) * k * pitch, k * pitch).reshape(k, pitch)[:, :clen]
+        ok = True
+        for i in (0, k - 1):
+            vec = _gf_vecmat(R[G - 1, i], V[G - 1])
+            ok = ok and bool(np.array_equal(got[i, :k], vec)) and bool(np.array_equal(got[i, k:], _gf_vecmat(vec, P)))
+    for p_ in (dV, dR, dW, dO):
+        ctx.free(p_)
+    units = G * k * (setbytes(k, L) + (k + 1) * clen)
+    return {"generations": G, "ms": round(best * 1e3, 3), "ms_per_generation": round(best / G * 1e3, 3),
+            "coded_plus_recoded_MBps": round(units / best / 1e6, 1), "recoded_rows_ok": ok,
+            "note": "one grouped encode launch + G recoder constructions (D2D copy + twin) + one grouped recode "
+                    "launch; host wall time; parity of both grouped entry points in tests/test_gpu_headline.py"}
+
+
+def _gf_vecmat(v, M):
+    """v (n bytes) x M (n x w bytes) over GF(2^8), poly 0x11D (gf256.go:15-44),
+    with numpy log/exp tables: a spot check of engine output, not a baseline."""
+    import numpy as np
+    exp = np.zeros(512, np.int32)
+    log = np.zeros(256, np.int32)
+    x = 1
+    for i in range(255):
+        exp[i] = x
+        log[x] = i
+        x <<= 1
+        if x & 0x100:
+            x ^= 0x11D
+    exp[255:510] = exp[:255]
+    acc = np.zeros(M.shape[1], np.int32)
+    for j, c in enumerate(np.asarray(v, np.int32)):
+        if c:
+            row = M[j].astype(np.int32)
+            acc ^= np.where(row != 0, exp[(log[row] + log[c]) % 255], 0)
+    return acc.astype(np.uint8)
 
 
 def c2_decode_grouped(ctx, L_, errors, encs, k, L, reps=3):

@@ -200,6 +200,17 @@ int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t piec
                                size_t coded_piece_len, size_t pitch, size_t pieces_coded_together,
                                rlnc_recoder** out);
 int rlnc_recoder_destroy(rlnc_recoder* rec);
+/* Many recoders in one launch (no kodr counterpart; full/recoder.go:27-46 once
+ * per generation): count recoded pieces of each of n_rec recoders of one ctx
+ * with equal piece_count and coded piece length.  d_r: n_rec blocks of
+ * count x piece_count recoding vectors (recoder i at i*count*piece_count);
+ * d_out: n_rec blocks of count wire rows at out_pitch (recoder i's first row
+ * at i*count*out_pitch).  One launch per 32 recoders (gf_gemm on the plain
+ * rows below 9 pieces, the bit-sliced kernel on the twins from 9), else one
+ * call per recoder; same bytes either way.  Async on the ctx stream. */
+int rlnc_recoder_group_coded_pieces_device(rlnc_recoder* const* recs, size_t n_rec, const uint8_t* d_r,
+                                           size_t count, uint8_t* d_out, size_t out_pitch);
+
 /* as rlnc_encoder_prepare: build the held rows' bit-sliced twin up front
  * (NewFullRLNCRecoder*, full/recoder.go:52-70).  Optional; async. */
 int rlnc_recoder_prepare(rlnc_recoder* rec);

@@ -931,6 +931,53 @@ int rlnc_recoder_coded_pieces_device(rlnc_recoder* r, const uint8_t* d_r, size_t
                        out_pitch, r->clen);
 }
 
+// Recoders of one context and shape (n, clen) at once: count recoded pieces
+// of each (full/recoder.go:27-46 per generation) in one launch per
+// kGemmGroupMax recoders -- gf_gemm on the plain rows below kBsMinRows,
+// gf_bs_kernel on the twins from there -- else one call per recoder.
+int rlnc_recoder_group_coded_pieces_device(rlnc_recoder* const* recs, size_t n_rec, const uint8_t* d_r,
+                                           size_t count, uint8_t* d_out, size_t out_pitch) {
+  if (!recs || (n_rec && (!recs[0] || (count && (!d_r || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!n_rec || !count) return RLNC_OK;
+  rlnc_recoder* r0 = recs[0];
+  const size_t n = r0->n, clen = r0->clen, pitch = r0->pitch;
+  if (out_pitch < clen) return RLNC_ERR_INVALID_ARGUMENT;
+  for (size_t i = 1; i < n_rec; i++)
+    if (!recs[i] || recs[i]->ctx != r0->ctx || recs[i]->n != n || recs[i]->clen != clen) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(r0->ctx));
+  rlnc_ctx* ctx = r0->ctx;
+  const size_t rstride = count * n, ostride = count * out_pitch;
+  const bool bs = resident_uses_bs(ctx, count, n, pitch, clen);
+  bool grouped = (out_pitch % 16) == 0 && n_rec > 1;
+  if (bs) {
+    grouped = grouped && bs_chunk_rows(count, n, pitch, clen) >= n;
+  } else {
+    grouped = grouped && n * pitch < kMaxDescBytes && (pitch % 16) == 0;
+    for (size_t i = 0; i < n_rec && grouped; i++) grouped = !recs[i]->compact;  // gf_gemm reads plain rows
+  }
+  if (!grouped) {
+    for (size_t i = 0; i < n_rec; i++)
+      TRY(rlnc_recoder_coded_pieces_device(recs[i], d_r + i * rstride, count, d_out + i * ostride, out_pitch));
+    return RLNC_OK;
+  }
+  if (bs)
+    for (size_t i = 0; i < n_rec; i++)
+      if (!recs[i]->compact) TRY(build_twin(ctx, recs[i]->flat.p, recs[i]->flat_bs, recs[i]->bs_valid, n, pitch, clen));
+  const uint8_t* xs[kodr_amd::kGemmGroupMax];
+  for (size_t g0 = 0; g0 < n_rec; g0 += kodr_amd::kGemmGroupMax) {
+    const size_t m = std::min<size_t>(kodr_amd::kGemmGroupMax, n_rec - g0);
+    for (size_t i = 0; i < m; i++) xs[i] = bs ? recs[g0 + i]->flat_bs.p : recs[g0 + i]->flat.p;
+    const kodr_amd::GemmGroupArgs grp{(int)m, xs, rstride, ostride};
+    if (bs)
+      HIPC(kodr_amd::gf_gemm_bs(d_r + g0 * rstride, n, count, n, xs[0], pitch, d_out + g0 * ostride, out_pitch, clen,
+                                ctx->device, ctx->stream, false, &grp));
+    else
+      HIPC(kodr_amd::gf_gemm(d_r + g0 * rstride, n, count, n, xs[0], pitch, d_out + g0 * ostride, out_pitch, clen,
+                             ctx->stream, nullptr, false, &grp));
+  }
+  return RLNC_OK;
+}
+
 /* ---- decoder ------------------------------------------------------------ */
 int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
   if (!out) return RLNC_ERR_INVALID_ARGUMENT;

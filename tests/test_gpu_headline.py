@@ -215,3 +215,46 @@ def test_prepared_recoder_c2(gpu_ctx, c2_generation):
     finally:
         _lib.lib().rlnc_recoder_destroy(rh)
     assert np.array_equal(out, oracle.recode(flat, k, R))
+
+
+@pytest.mark.parametrize("G,k,L,n,count,compact", [(3, 32, 4096, 40, 12, False), (5, 16, 2048 + 16, 16, 4, False),
+                                                   (34, 8, 1024, 10, 9, False), (3, 64, 8192, 64, 20, True),
+                                                   (2, 256, 131072, 256, 32, False)])
+def test_grouped_recode_vs_oracle(gpu_ctx, G, k, L, n, count, compact):
+    # rlnc_recoder_group_coded_pieces_device: gf_gemm launch below 9 pieces,
+    # bit-sliced from 9 ((34, ...): two launches; compact: recoder 0 holds
+    # only its twin); every recoded wire row against the oracle's recode
+    rng = np.random.default_rng(G * 31 + k + count)
+    lib = _lib.lib()
+    flats, recs = [], []
+    for g in range(G):
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+        flat = np.ascontiguousarray(np.concatenate([V, oracle.encode(P, V)], axis=1))
+        rh = ctypes.c_void_p()
+        errors.check(lib.rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, n, k, ctypes.byref(rh)))
+        flats.append(flat)
+        recs.append(rh)
+    if compact:
+        errors.check(lib.rlnc_recoder_compact(recs[0]))
+    clen = k + L
+    pitch = (clen + 15) // 16 * 16 + 16
+    R = rng.integers(0, 256, (G, count, n), dtype=np.uint8)
+    arr = (ctypes.c_void_p * G)(*[r.value for r in recs])
+    dR, dO = gpu_ctx.alloc(R.nbytes), gpu_ctx.alloc(G * count * pitch + 64)
+    try:
+        gpu_ctx.h2d(dR, R)
+        gpu_ctx.h2d(dO, np.full(G * count * pitch + 64, 0xA5, np.uint8))
+        errors.check(lib.rlnc_recoder_group_coded_pieces_device(arr, G, dR, count, dO, pitch))
+        gpu_ctx.synchronize()
+        raw = gpu_ctx.d2h(dO, G * count * pitch + 64)
+    finally:
+        gpu_ctx.free(dR)
+        gpu_ctx.free(dO)
+        for r in recs:
+            lib.rlnc_recoder_destroy(r)
+    assert (raw[G * count * pitch:] == 0xA5).all()
+    rows = raw[:G * count * pitch].reshape(G, count, pitch)
+    assert (rows[:, :, clen:] == 0xA5).all(), "wrote past the coded piece"
+    for g in range(G):
+        assert np.array_equal(rows[g, :, :clen], oracle.recode(flats[g], k, R[g])), g
