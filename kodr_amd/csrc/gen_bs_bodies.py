@@ -437,7 +437,9 @@ def main():
     out += emit("KODR_BS_MAIN_SLOAD", main_loop(True, True, ROW_PRIO, None, (), True))
     out += emit("KODR_BS_DUMP", dump_lines())
     # dynamic rows (MODE 20)
-    out += emit("KODR_BS_MAIN_DYN", main_loop_dyn(True))
+    # (a one-row ring only; other ring depths build it empty, and only a
+    # tuning build instantiates MODE 20)
+    out += emit("KODR_BS_MAIN_DYN", main_loop_dyn(True) if P == 1 else [])
     out.append(f"#define KODR_BS_DYN_VMAX {D_VMAX}")
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)
