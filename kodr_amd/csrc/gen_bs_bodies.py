@@ -41,12 +41,22 @@ TL0 = 76           # TL table, 15 registers v[76..90] (singles first, as aligned
 PL = 91            # LDS address of the next program quad
 TH0 = 92           # TH table v[92..106]
 # ring depth (rows in flight per wave): 1 measured 1.5-2.5 % faster than 2 at
-# B = 16-32 (profiles/r01/bs_ring.log), 3 drops to 3 waves per SIMD
+# B = 16-32 in single launches (profiles/r01/bs_ring.log), 2 about 1.7 %
+# faster in grouped launches, whose waves stream 64 rows
+# (profiles/r02/ring_ab/); the kernel carries both (KODR_BS_MAIN: P, the
+# default; KODR_BS_MAIN_P2: two rows).  3 drops to 3 waves per SIMD.
 P = int(os.environ.get("KODR_BS_P", "1"))
 RING = 108         # P row slots x 8 planes: v[108..123]
 PG = RING + 8 * P  # program chunk: 8 rows x 8 targets, lane 8j + m (absolute lo words)
 PGN = PG + 1       # the next chunk, in flight from LDS
 VMAX = PGN + 1     # first VGPR not used by the asm
+
+
+def set_ring(p):
+    """Switch the module's ring depth (and the registers after the ring)."""
+    global P, PG, PGN, VMAX
+    P, PG = p, RING + 8 * p
+    PGN, VMAX = PG + 1, PG + 2
 NCOPY = 4
 # body start alignment in bytes (0: packed back to back); the instruction
 # fetch after each s_setpc starts at the body's first byte
@@ -454,6 +464,18 @@ def main():
     out.append("#define KODR_BS_CLOBBERS_DYN " + ", ".join(dclob) + ', "scc", "memory"')
     out.append("#define KODR_BS_CLOBBERS_SLOAD " + ", ".join(clob + [f'"s{r}"' for r in range(SP, SL + 8)]) +
                ', "scc", "memory"')
+    # the two-row ring variant (grouped launches): main loop, ring operands,
+    # clobbers, register count
+    p0 = P
+    set_ring(2)
+    out += emit("KODR_BS_MAIN_P2", main_loop(True))
+    ops2 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
+    out.append("#define KODR_BS_RING_OPERANDS_P2 " + ", ".join(ops2))
+    clob2 = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, VMAX))]
+    clob2 += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
+    out.append("#define KODR_BS_CLOBBERS_P2 " + ", ".join(clob2) + ', "scc", "memory"')
+    out.append(f"#define KODR_BS_VMAX_P2 {VMAX}")
+    set_ring(p0)
     out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "
                f"row prep {len(table_lines(0))} per row; {total} bytes of bodies")
     print("\n".join(out))

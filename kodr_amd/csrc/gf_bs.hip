@@ -166,7 +166,12 @@ struct BsGroupK {
   size_t a_stride, y_stride;
 };
 
-template <int KW, int MODE = 0, bool GRP = false>
+// RP: rows in flight per wave in the row ring (KODR_BS_P, one, for single
+// launches; two for grouped launches, whose waves stream long row ranges:
+// DESIGN.md, grouped bit-sliced encode).  Both fit 4 waves per SIMD.
+static_assert(512 / KODR_BS_VMAX == 512 / KODR_BS_VMAX_P2, "ring variants differ in occupancy");
+
+template <int KW, int MODE = 0, bool GRP = false, int RP = KODR_BS_P>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
@@ -340,9 +345,9 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
       __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)nrec, 0x00020000);
   // (unconditional: a wave past K reads zeros, and a branch here would make
   // the compiler's waitcnt pass drain these loads at the next LDS write)
-  u32x4 ring[2 * KODR_BS_P];
+  u32x4 ring[2 * RP];
 #pragma unroll
-  for (int i = 0; i < KODR_BS_P; i++) {
+  for (int i = 0; i < RP; i++) {
     ring[2 * i] = __builtin_amdgcn_raw_buffer_load_b128(xr, col, kboff + i * sldx, 0);
     ring[2 * i + 1] = __builtin_amdgcn_raw_buffer_load_b128(xr, col + 16, kboff + i * sldx, 0);
   }
@@ -385,7 +390,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const uint64_t xa = reinterpret_cast<uint64_t>(X);
   const uint32_t xlo = __builtin_amdgcn_readfirstlane((uint32_t)xa);
   const uint32_t xhi = __builtin_amdgcn_readfirstlane((uint32_t)(xa >> 32));
-  const uint32_t roff = kboff + KODR_BS_P * sldx;  // the asm streams from row kb + P
+  const uint32_t roff = kboff + RP * sldx;  // the asm streams from row kb + RP
   // this lane's program word in LDS (chunk lane 8j + m: row j, output row m)
   const uint32_t pl = (uint32_t)(reinterpret_cast<uintptr_t>(wp)) + (uint32_t)lane * 4u;
   const uint32_t sthi = __builtin_amdgcn_readfirstlane(thi);
@@ -393,16 +398,21 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const uint64_t pga = reinterpret_cast<uint64_t>(progw);
   const uint32_t pglo = __builtin_amdgcn_readfirstlane((uint32_t)pga);
   const uint32_t pghi = __builtin_amdgcn_readfirstlane((uint32_t)(pga >> 32));
+#define KODR_BS_ASM_INPUTS                                                                          \
+  [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx), [ngrp] "s"(ngrp),  \
+      [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)reinterpret_cast<uintptr_t>(red) + (uint32_t)lane * 4u), \
+      [pl] "v"(pl), [ydbg] "s"(Y), [pglo] "s"(pglo), [pghi] "s"(pghi)
 #define KODR_BS_ASM2(MAIN, CLOB)                                                                    \
-  asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"                                       \
-               : KODR_BS_RING_OPERANDS                                                              \
-               : [xlo] "s"(xlo), [xhi] "s"(xhi), [nrec] "s"(nrec), [roff] "s"(roff), [ldx] "s"(sldx),  \
-                 [ngrp] "s"(ngrp), [thi] "s"(sthi), [col] "v"(col), [lds] "v"((uint32_t)reinterpret_cast<uintptr_t>(red) + (uint32_t)lane * 4u),   \
-                 [pl] "v"(pl), [ydbg] "s"(Y), [pglo] "s"(pglo), [pghi] "s"(pghi)                   \
-               : CLOB)
+  asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t" : KODR_BS_RING_OPERANDS : KODR_BS_ASM_INPUTS : CLOB)
 #define KODR_BS_ASM(MAIN) KODR_BS_ASM2(MAIN, KODR_BS_CLOBBERS)
   if (nr > 0 && MODE != 5) {
-    if constexpr (MODE == 9) {
+    if constexpr (RP != KODR_BS_P) {
+      static_assert(RP == 2 && MODE == 0, "the two-row ring variant has the plain main loop only");
+      asm volatile(KODR_BS_MAIN_P2 KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS_P2
+                   : KODR_BS_ASM_INPUTS
+                   : KODR_BS_CLOBBERS_P2);
+    } else if constexpr (MODE == 9) {
       if (blockIdx.x == 0 && w == 0) {
         KODR_BS_ASM(KODR_BS_DUMP);
         uint32_t* yd = reinterpret_cast<uint32_t*>(Y) + 64;
@@ -440,6 +450,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   }
 #undef KODR_BS_ASM
 #undef KODR_BS_ASM2
+#undef KODR_BS_ASM_INPUTS
   if constexpr (MODE == 8) stamp[2] = __builtin_amdgcn_s_memtime();
   __syncthreads();
 
@@ -556,9 +567,10 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     g.a_stride = group->a_stride;
     g.y_stride = group->y_stride;
     // gridDim.x is a multiple of 8, so the XCD order of each generation's
-    // blocks is the single-generation one
-    hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A, lda, M,
-                       K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+    // blocks is the single-generation one; the two-row ring (plain loop only)
+    constexpr int rp = MODE == 0 ? 2 : KODR_BS_P;
+    hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
+                       lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
   } else {
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
                        ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
