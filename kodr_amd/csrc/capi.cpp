@@ -1583,10 +1583,12 @@ constexpr size_t kGroupGetChunk = 16;
 int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* d_out, size_t out_pitch) {
   if (!ds || !G || !d_out || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
   rlnc_decoder* d0 = ds[0];
+  for (size_t g = 0; g < G; g++)
+    if (!ds[g]) return RLNC_ERR_INVALID_ARGUMENT;
+  for (size_t g = 0; g < G; g++)  // full/decoder.go:84-86 for any of them before anything else
+    if (!ds[g]->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
   for (size_t g = 0; g < G; g++) {
     rlnc_decoder* d = ds[g];
-    if (!d) return RLNC_ERR_INVALID_ARGUMENT;
-    if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
     if (!d->ctx) return RLNC_ERR_NO_DEVICE;
     if (d->ctx != d0->ctx || d->L != d0->L || d->core.piece_count() != d0->core.piece_count())
       return RLNC_ERR_INVALID_ARGUMENT;

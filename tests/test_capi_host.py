@@ -414,3 +414,26 @@ def test_full_batch_solve(seed):
         B = rng.integers(0, 256, (k - 3, k), dtype=np.uint8)
         R = oracle.matmul(rng.integers(0, 256, (n, k - 3), dtype=np.uint8), B)[1]
     _batch_vs_rows(k, np.ascontiguousarray(R), [n])
+
+
+def test_grouped_entry_points_argument_checks():
+    # the many-generation entry points reject bad arguments before any device
+    # work, and a decoder group reports kodr's GetPieces errors
+    # (full/decoder.go:84-86) or the missing device
+    L = _lib.lib()
+    vp = ctypes.c_void_p
+    assert L.rlnc_encoder_group_coded_pieces_device(None, 1, None, 1, None, 16) == -1
+    assert L.rlnc_recoder_group_coded_pieces_device(None, 1, None, 1, None, 16) == -1
+    assert L.rlnc_decoders_get_pieces_device(None, 1, None, 16) == -1
+    empty = (vp * 1)(None)
+    assert L.rlnc_encoder_group_coded_pieces_device(empty, 0, None, 1, None, 16) == 0
+    assert L.rlnc_recoder_group_coded_pieces_device(empty, 0, None, 1, None, 16) == 0
+    a, b = CoreDecoder(2), CoreDecoder(2)
+    a.add(np.array([1, 0], np.uint8))
+    a.add(np.array([0, 1], np.uint8))
+    buf = ctypes.create_string_buffer(64)
+    both = (vp * 2)(a.h.value, b.h.value)
+    assert L.rlnc_decoders_get_pieces_device(both, 2, buf, 16) == 4   # b: MORE_USEFUL_PIECES_REQUIRED
+    b.add(np.array([1, 1], np.uint8))
+    b.add(np.array([0, 1], np.uint8))
+    assert L.rlnc_decoders_get_pieces_device(both, 2, buf, 16) == -4  # coefficient-side decoders: no device
