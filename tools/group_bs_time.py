@@ -17,7 +17,8 @@ from kodr_amd._lib import lib, _u8p  # noqa: E402
 
 L_ = lib()
 ctx = kdev.Context(0)
-k, L, G, REPS = 256, 131072, 16, 15
+k, L, REPS = 256, 131072, 15
+G = int(os.environ.get("KODR_GROUP_G", "16"))
 rng = np.random.default_rng(3)
 encs = []
 for g in range(G):
