@@ -371,3 +371,31 @@ def test_dynamic_rows_end_to_end_vs_oracle(K, kw):
         for k in range(K):
             exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
         assert np.array_equal(got, exp), (K, kw, m)
+
+
+def test_two_row_ring_end_to_end_vs_oracle():
+    # the grouped launches' loop (KODR_BS_MAIN_P2, gf_bs_kernel RP = 2): the
+    # same interpreter with the ring two rows deep, registers still within
+    # 4 waves per SIMD
+    p0 = gen.P
+    gen.set_ring(2)
+    try:
+        assert gen.VMAX <= 128 and gen.PG == gen.RING + 16
+
+        class _Wave2(_Wave):
+            VEC = (gen.PG, gen.PGN, gen.PL)
+
+        rng = np.random.default_rng(12)
+        for nr in (8, 16, 40):
+            X = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
+            A = rng.integers(0, 256, (8, nr), dtype=np.uint8)
+            A[3, 2], A[6, 0] = 0, 1
+            acc = _Wave2(X, A, nr, gen.main_loop(True)).run()
+            for m in range(8):
+                got = bitslice_np(acc[m].view(np.uint8).copy())
+                exp = np.zeros(32, np.uint8)
+                for k in range(nr):
+                    exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
+                assert np.array_equal(got, exp), (nr, m)
+    finally:
+        gen.set_ring(p0)
