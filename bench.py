@@ -710,7 +710,8 @@ def c5_one_gpu_grouped(ctx, L_, errors, encs, k, L, rng, reps=3):
     (rlnc_recoder_group_coded_pieces_device).  The coding vectors are random
     host bytes uploaded before the timed region, into both the contiguous
     vector block and the wire rows (64 KiB per generation); the recoded
-    output is checked against the oracle for one generation."""
+    output is spot-checked for one generation (two recoded rows: vector part
+    R x V and piece part vector x P, numpy GF(2^8) in _gf_vecmat)."""
     import ctypes
     import numpy as np
     clen = k + L
