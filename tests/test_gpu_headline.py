@@ -123,12 +123,14 @@ def group_run(ctx, gens, count, V, out_pitch=None, expect=0):
 @pytest.mark.parametrize("G,k,L,count", [(1, 16, 4096, 1), (3, 16, 4096 + 16, 2), (5, 100, 8192 + 48, 1),
                                          (8, 256, 65536, 4), (40, 32, 1024, 1), (33, 64, 2048, 8),
                                          (6, 64, 4096, 12), (4, 20, 1000, 3), (35, 64, 2048, 9),
-                                         (5, 100, 8192 + 48, 40), (3, 300, 4096, 17)])
+                                         (5, 100, 8192 + 48, 40), (3, 300, 4096, 17), (5, 16, 4096, 20),
+                                         (3, 24, 65536, 32)])
 def test_grouped_encode_vs_oracle(gpu_ctx, G, k, L, count):
     # (40, ...) and (33, ...) span two launches of <= 32 generations; count >= 9
     # takes the grouped bit-sliced launch ((35, ...) over two launches, k = 100
     # and 300 with a ragged last program chunk); L = 1000 is not a multiple of
-    # 16 (ragged last chunk, padded pitch)
+    # 16 (ragged last chunk, padded pitch); k = 16 / 24 with 20 / 32 pieces:
+    # few narrow rows, the grouped v_perm launch with more than 8 output rows
     rng = np.random.default_rng(G * 1000 + k + count)
     gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
     V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
