@@ -184,8 +184,9 @@ int rlnc_encoder_compact(rlnc_encoder* enc);
  * rows at out_pitch (generation i's first row at i*count*out_pitch).  Every
  * 32 generations take ONE kernel launch: small batches (the streaming regime,
  * count < 9) on the plain rows, larger ones on the bit-sliced twins (built
- * here if rlnc_encoder_prepare was not called); shapes neither kernel takes
- * in one row chunk fall back to one launch per generation.
+ * here if rlnc_encoder_prepare was not called; from 5 pieces when every twin
+ * is already resident); shapes neither kernel takes in one row chunk fall
+ * back to one launch per generation.
  * Full-RLNC semantics.  Async on the ctx stream. */
 int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
                                            size_t count, uint8_t* d_out, size_t out_pitch);

@@ -736,8 +736,20 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
                  (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
   for (size_t i = 0; i < n_enc && grouped; i++) grouped = !encs[i]->compact;  // the grouped launch reads plain rows
   // larger batches: one bit-sliced launch per kGemmGroupMax generations over
-  // their twins, when the product is a single row chunk
-  bool grouped_bs = !grouped && resident_uses_bs(ctx, count, k, e0->pitch, L) &&
+  // their twins, when the product is a single row chunk.  Smaller batches
+  // from kGroupBsMinRows take it too when every twin is already resident
+  // (prepared or compact encoders): one 8-row group per column chunk costs
+  // 6.6-6.9 us per 32 MiB/256 generation at 6-8 pieces against 10-11 us on
+  // gf_gemm, equal at 3-4, gf_gemm ahead at 2 (profiles/r02/group_bs_small/).
+  // KODR_GROUP_BS_MIN overrides it (measurements).
+  constexpr size_t kGroupBsMinRows = 5;
+  static const size_t bs_min =
+      getenv("KODR_GROUP_BS_MIN") ? (size_t)atol(getenv("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
+  bool twins = count >= bs_min && count < kBsMinRows && !few_narrow_rows(count, k, L) && (e0->pitch % 32) == 0 &&
+               kodr_amd::bs_ready(ctx->device);
+  for (size_t i = 0; i < n_enc && twins; i++) twins = encs[i]->compact || encs[i]->bs_valid;
+  if (twins) grouped = false;
+  bool grouped_bs = !grouped && (twins || resident_uses_bs(ctx, count, k, e0->pitch, L)) &&
                     bs_chunk_rows(count, k, e0->pitch, L) >= k && (out_pitch % 16) == 0;
   if (grouped_bs) {
     for (size_t i = 0; i < n_enc; i++)

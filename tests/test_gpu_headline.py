@@ -92,13 +92,13 @@ def test_prepare_matches_lazy_twin(gpu_ctx):
         assert np.array_equal(out[:, k:], ref)
 
 
-def group_run(ctx, gens, count, V, out_pitch=None, expect=0):
+def group_run(ctx, gens, count, V, out_pitch=None, expect=0, prepare=False):
     """Encode `count` pieces of every generation in one grouped call; returns
     (G, count, L) from the device output."""
     G = len(gens)
     k, L = gens[0].shape
     out_pitch = out_pitch or L
-    encs = [make_encoder(ctx, P, prepare=False) for P in gens]
+    encs = [make_encoder(ctx, P, prepare=prepare) for P in gens]
     arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
     dV, dO = ctx.alloc(max(V.nbytes, 1)), ctx.alloc(G * count * out_pitch + 64)
     try:
@@ -135,6 +135,18 @@ def test_grouped_encode_vs_oracle(gpu_ctx, G, k, L, count):
     gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
     V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
     got = group_run(gpu_ctx, gens, count, V, out_pitch=(L + 15) // 16 * 16 + 32)
+    for g in range(G):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
+@pytest.mark.parametrize("G,k,L,count", [(4, 64, 8192, 5), (3, 256, 131072, 8), (34, 32, 4096, 6)])
+def test_grouped_encode_prepared_small_batches(gpu_ctx, G, k, L, count):
+    # prepared encoders (twins resident): 5-8 pieces per generation take the
+    # grouped bit-sliced launch instead of gf_gemm; (34, ...) spans two launches
+    rng = np.random.default_rng(G * 77 + k + count)
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+    got = group_run(gpu_ctx, gens, count, V, out_pitch=L + 32, prepare=True)
     for g in range(G):
         assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
 
