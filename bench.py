@@ -612,7 +612,8 @@ def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
         ctx.record(e1)
         t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters_c
         hbm = G * (k * L + count * (k + L))
-        res[str(count)] = {"kernel": "gf_bs_kernel (grouped)" if count >= 9 else "gf_gemm_kernel (grouped)",
+        # prepared encoders: the bit-sliced launch from 5 pieces (capi.cpp kGroupBsMinRows)
+        res[str(count)] = {"kernel": "gf_bs_kernel (grouped)" if count >= 5 else "gf_gemm_kernel (grouped)",
                            "us_per_launch": round(t * 1e6, 2), "us_per_generation": round(t / G * 1e6, 3),
                            "coded_MBps": round(G * count * setbytes(k, L) / t / 1e6, 1),
                            "hbm_GBps": round(hbm / t / 1e9, 1),
