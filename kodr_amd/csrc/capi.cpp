@@ -718,6 +718,14 @@ int rlnc_encoder_compact(rlnc_encoder* e) {
   return compact_resident(e->ctx, e->pieces, e->pieces_bs, e->bs_valid, e->compact, e->k, e->pitch, e->L);
 }
 
+// grouped launches over resident twins: the bit-sliced kernel from this many
+// pieces per generation (see rlnc_encoder_group_coded_pieces_device)
+constexpr size_t kGroupBsMinRows = 5;
+static size_t group_bs_min() {
+  static const size_t v = getenv("KODR_GROUP_BS_MIN") ? (size_t)atol(getenv("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
+  return v;
+}
+
 int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
                                            size_t count, uint8_t* d_out, size_t out_pitch) {
   if (!encs || (n_enc && (!encs[0] || (count && (!d_vectors || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
@@ -742,11 +750,8 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
   // 6.6-6.9 us per 32 MiB/256 generation at 6-8 pieces against 10-11 us on
   // gf_gemm, equal at 3-4, gf_gemm ahead at 2 (profiles/r02/group_bs_small/).
   // KODR_GROUP_BS_MIN overrides it (measurements).
-  constexpr size_t kGroupBsMinRows = 5;
-  static const size_t bs_min =
-      getenv("KODR_GROUP_BS_MIN") ? (size_t)atol(getenv("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
-  bool twins = count >= bs_min && count < kBsMinRows && !few_narrow_rows(count, k, L) && (e0->pitch % 32) == 0 &&
-               kodr_amd::bs_ready(ctx->device);
+  bool twins = count >= group_bs_min() && count < kBsMinRows && !few_narrow_rows(count, k, L) &&
+               (e0->pitch % 32) == 0 && kodr_amd::bs_ready(ctx->device);
   for (size_t i = 0; i < n_enc && twins; i++) twins = encs[i]->compact || encs[i]->bs_valid;
   if (twins) grouped = false;
   bool grouped_bs = !grouped && (twins || resident_uses_bs(ctx, count, k, e0->pitch, L)) &&
@@ -959,7 +964,12 @@ int rlnc_recoder_group_coded_pieces_device(rlnc_recoder* const* recs, size_t n_r
   TRY(set_dev(r0->ctx));
   rlnc_ctx* ctx = r0->ctx;
   const size_t rstride = count * n, ostride = count * out_pitch;
-  const bool bs = resident_uses_bs(ctx, count, n, pitch, clen);
+  // as for encoders: from kGroupBsMinRows pieces on resident twins (prepared
+  // or compact recoders), else from kBsMinRows
+  bool twins = count >= group_bs_min() && count < kBsMinRows && !few_narrow_rows(count, n, clen) &&
+               (pitch % 32) == 0 && kodr_amd::bs_ready(ctx->device);
+  for (size_t i = 0; i < n_rec && twins; i++) twins = recs[i]->compact || recs[i]->bs_valid;
+  const bool bs = twins || resident_uses_bs(ctx, count, n, pitch, clen);
   bool grouped = (out_pitch % 16) == 0 && n_rec > 1;
   if (bs) {
     grouped = grouped && bs_chunk_rows(count, n, pitch, clen) >= n;

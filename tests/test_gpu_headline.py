@@ -233,7 +233,8 @@ def test_prepared_recoder_c2(gpu_ctx, c2_generation):
 
 @pytest.mark.parametrize("G,k,L,n,count,compact", [(3, 32, 4096, 40, 12, False), (5, 16, 2048 + 16, 16, 4, False),
                                                    (34, 8, 1024, 10, 9, False), (3, 64, 8192, 64, 20, True),
-                                                   (2, 256, 131072, 256, 32, False)])
+                                                   (2, 256, 131072, 256, 32, False), (4, 64, 8192, 64, 6, "prepare"),
+                                                   (3, 64, 8192, 64, 7, True)])
 def test_grouped_recode_vs_oracle(gpu_ctx, G, k, L, n, count, compact):
     # rlnc_recoder_group_coded_pieces_device: gf_gemm launch below 9 pieces,
     # bit-sliced from 9 ((34, ...): two launches; compact: recoder 0 holds
@@ -249,7 +250,10 @@ def test_grouped_recode_vs_oracle(gpu_ctx, G, k, L, n, count, compact):
         errors.check(lib.rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, n, k, ctypes.byref(rh)))
         flats.append(flat)
         recs.append(rh)
-    if compact:
+    if compact == "prepare":     # twins resident: 5-8 pieces take the bit-sliced launch
+        for r in recs:
+            errors.check(lib.rlnc_recoder_prepare(r))
+    elif compact:
         errors.check(lib.rlnc_recoder_compact(recs[0]))
     clen = k + L
     pitch = (clen + 15) // 16 * 16 + 16
