@@ -124,6 +124,65 @@ def c1_roundtrip(ctx, L_, errors, rng):
                     "encode rate for this shape (README.md:73)"}
 
 
+class HeadlineStep:
+    """The timed step, shared with tests/test_gpu_headline.py (which runs it
+    once and compares every piece with the oracle, and pins its launch plan).
+
+    G resident generations of k x L (seeded random bytes) are uploaded and
+    prepared (rlnc_encoder_prepare: the bit-sliced twin) at construction,
+    outside the timed loop, as kodr's bench constructs its encoder before
+    b.Loop (benches/full/encoder_test.go:47-56); the cost is reported apart
+    (construct_ms_per_generation).  A step: B coded pieces of every resident
+    generation (full/encoder.go:61-71 B times per generation, vectors drawn
+    per piece) as ONE grouped launch (rlnc_encoder_group_coded_pieces_device:
+    the launch and the kernel's ramp and tail are paid once per G
+    generations, each generation read once); per_generation=True: one
+    launch per generation, rotating over the G.  Vectors rotate over nvec
+    pre-drawn sets (host copy in self.V)."""
+
+    def __init__(self, ctx, L_, errors, k, L, B, G, grouped=True, rng=None, nvec=None, keep_data=False):
+        import ctypes
+        import numpy as np
+        self.ctx, self.L_, self.errors = ctx, L_, errors
+        self.k, self.L, self.B, self.G, self.grouped = k, L, B, G, grouped
+        rng = rng if rng is not None else np.random.default_rng(0x6B6F6472)
+        datas = [rng.integers(0, 256, k * L, dtype=np.uint8) for _ in range(G)]
+        self.encs = []
+        ctx.synchronize()
+        tc0 = time.perf_counter()
+        for g in range(G):
+            h = ctypes.c_void_p()
+            errors.check(L_.rlnc_encoder_create(ctx.handle, 0, datas[g].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                                                k, L, ctypes.byref(h)))
+            errors.check(L_.rlnc_encoder_prepare(h))
+            self.encs.append(h)
+        ctx.synchronize()
+        self.construct_ms = (time.perf_counter() - tc0) * 1e3 / G
+        self.datas = datas if keep_data else None
+        self.per_step = G if grouped else 1            # generations per step
+        self.nvec = nvec or (8 if grouped else 64)
+        self.V = rng.integers(0, 256, (self.nvec, self.per_step, B, k), dtype=np.uint8)
+        self.dV = ctx.alloc(self.V.nbytes)
+        ctx.h2d(self.dV, self.V)
+        self.dOut = ctx.alloc(self.per_step * B * L)
+        self.enc_arr = (ctypes.c_void_p * G)(*[e.value for e in self.encs])
+
+    def step(self, i):
+        k, L, B = self.k, self.L, self.B
+        dv = self.dV + (i % self.nvec) * self.per_step * B * k
+        if self.grouped:
+            self.errors.check(self.L_.rlnc_encoder_group_coded_pieces_device(self.enc_arr, self.G, dv, B, self.dOut, L))
+        else:
+            self.errors.check(self.L_.rlnc_encoder_coded_pieces_device(self.encs[i % self.G], dv, B, self.dOut, L))
+
+    def close(self):
+        for h in self.encs:
+            self.L_.rlnc_encoder_destroy(h)
+        self.encs = []
+        self.ctx.free(self.dV)
+        self.ctx.free(self.dOut)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,53 +224,16 @@ def main():
 
     from kodr_amd import device as kdev
     from kodr_amd import errors
-    from kodr_amd._lib import lib
+    from kodr_amd._lib import last_launch_plan, lib
 
     L_ = lib()
     ctx = kdev.Context(local)
     k, L, B, G = K_PIECES, L_BYTES, args.batch, args.gens
 
-    # G resident generations of 32 MiB (+ B x k vectors per step, rotating).
-    # Construction (upload + the bit-sliced twin, rlnc_encoder_prepare) happens
-    # here, outside the timed loop, as kodr's bench constructs its encoder
-    # before b.Loop (benches/full/encoder_test.go:47-56); its cost is reported
-    # separately (construct_ms_per_generation).
     rng = np.random.default_rng(0x6B6F6472 + rank)
-    import ctypes
-    encs, datas = [], []
-    for g in range(G):
-        datas.append(rng.integers(0, 256, k * L, dtype=np.uint8))
-    ctx.synchronize()
-    tc0 = time.perf_counter()
-    for g in range(G):
-        h = ctypes.c_void_p()
-        errors.check(L_.rlnc_encoder_create(ctx.handle, 0, datas[g].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
-                                            k, L, ctypes.byref(h)))
-        errors.check(L_.rlnc_encoder_prepare(h))
-        encs.append(h)
-    ctx.synchronize()
-    construct_ms = (time.perf_counter() - tc0) * 1e3 / G
-    del datas
-    # A step: B coded pieces of every resident generation (full/encoder.go:61-71
-    # B times per generation, vectors drawn per piece), as ONE grouped launch
-    # (rlnc_encoder_group_coded_pieces_device: the launch and the kernel's ramp
-    # and tail are paid once per G generations, each generation read once).
-    # --per-generation: one launch per generation, rotating over the G.
-    grouped = not args.per_generation
-    per_step = G if grouped else 1            # generations per step
-    nvec = 8 if grouped else 64
-    V = rng.integers(0, 256, (nvec, per_step, B, k), dtype=np.uint8)
-    dV = ctx.alloc(V.nbytes)
-    ctx.h2d(dV, V)
-    dOut = ctx.alloc(per_step * B * L)
-    enc_arr = (ctypes.c_void_p * G)(*[e.value for e in encs])
-
-    def step(i):
-        dv = dV + (i % nvec) * per_step * B * k
-        if grouped:
-            errors.check(L_.rlnc_encoder_group_coded_pieces_device(enc_arr, G, dv, B, dOut, L))
-        else:
-            errors.check(L_.rlnc_encoder_coded_pieces_device(encs[i % G], dv, B, dOut, L))
+    hs = HeadlineStep(ctx, L_, errors, k, L, B, G, grouped=not args.per_generation, rng=rng)
+    encs, dV, dOut = hs.encs, hs.dV, hs.dOut
+    construct_ms, grouped, per_step, step = hs.construct_ms, hs.grouped, hs.per_step, hs.step
 
     def barrier():
         ctx.synchronize()
@@ -240,6 +262,7 @@ def main():
         step(i)
     ctx.record(e1)
     ms_dev = kdev.Context.elapsed_ms(e0, e1)
+    plan = last_launch_plan()      # the timed launch's kernel instance (pinned by tests/test_gpu_headline.py)
     barrier()
     wall = time.perf_counter() - t0
     t_local = ms_dev / 1e3
@@ -259,9 +282,15 @@ def main():
     compulsory = per_step * (k * L + B * k + B * L)
     achieved = compulsory / t_launch / 1e9
     macs = per_step * B * k * L
-    bs = B >= 9
+    bs = plan["kernel"] == 2
 
     extras = {"construct_ms_per_generation": round(construct_ms, 3)}
+    ed = None
+    if rank == 0:
+        try:
+            ed = encode_decode(ctx, L_, errors, encs, k, L)
+        except Exception as e:  # secondary measurement: never lose the headline line
+            ed = {"error": repr(e)[:300]}
     if not args.no_extras and rank == 0:
         extras.update(run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng))
     if world > 1 and not args.no_extras:
@@ -272,10 +301,7 @@ def main():
         if rank == 0:
             extras["c5_encode_relay_recode"] = c5
 
-    for h in encs:
-        L_.rlnc_encoder_destroy(h)
-    ctx.free(dV)
-    ctx.free(dOut)
+    hs.close()
 
     if rank == 0:
         line = {
@@ -291,18 +317,22 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded uniform random bytes and coding vectors)",
-            "config": {"workload": "Full RLNC encode, 32 MiB generation / 256 pieces (BASELINE configs[1]); "
+            "config": {"workload": "Full RLNC ENCODE leg of the metric, 32 MiB generation / 256 pieces (BASELINE "
+                                   "configs[1]); "
                                    + (f"a step = {B} coded pieces of each of the {G} resident generations in one "
                                       "grouped launch" if grouped else
                                       f"a step = {B} coded pieces of one generation (rotating over {G})")
-                                   + "; the decode leg (configs[2]) is extras.c2_decode",
+                                   + "; value counts encode only. The metric's encode+decode round trip (configs[1] "
+                                     "+ configs[2]) is the top-level encode_decode object",
+                       "value_covers": "encode", "encode_decode_in": "encode_decode",
                        "piece_count": k, "piece_size": L, "coded_pieces_per_generation_per_step": B,
                        "generations_per_step": per_step, "coded_pieces_per_step": per_step * B,
                        "resident_generations": G, "parallelism": f"generation-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, k, L, per_step),
-                         "kernel": "gf_bs_kernel" if bs else "gf_gemm_kernel",  # capi.cpp kBsMinRows
+                         "kernel": {1: "gf_gemm_kernel", 2: "gf_bs_kernel"}.get(plan["kernel"], "?"),
+                         "plan": plan,
                          "traffic_source": pmc_traffic_file(B, k, L, per_step),
                          "hbm_bytes_per_launch": compulsory,
                          "avg_launch_us": round(t_launch * 1e6, 3),
@@ -320,6 +350,7 @@ def main():
                                  "coefficient per 2 KiB at 2.3 cycles per wave instruction on 1024 SIMDs), "
                                  "the bound that binds at B >= 9 (DESIGN.md Roofline)"},
             "cpu_baseline": cpu,
+            "encode_decode": ed,
             "wall_s": round(wall, 4),
         }
         if extras:
@@ -788,6 +819,87 @@ def _gf_vecmat(v, M):
             row = M[j].astype(np.int32)
             acc ^= np.where(row != 0, exp[(log[row] + log[c]) % 255], 0)
     return acc.astype(np.uint8)
+
+
+def encode_decode(ctx, L_, errors, encs, k, L, reps=3):
+    """The metric's encode+decode as one round trip, device-resident, over the
+    G resident 32 MiB/256 generations: k + 2 coded pieces of each as wire rows
+    with device-drawn vectors in ONE grouped call
+    (rlnc_encoder_group_coded_wire_device: one vector launch + one bit-sliced
+    launch), then G fresh decoders take them in ONE batched AddPiece call
+    (rlnc_decoders_add_pieces_gpu: the elimination on the GPU) and ONE grouped
+    GetPieces call (rlnc_decoders_get_pieces_device).  Fresh vectors every
+    repetition; decoders constructed outside the timed region, as
+    kodr's decoder bench does (benches/full/decoder_test.go:46-94).  Wall time
+    of the whole round trip, best of reps; the decoded generations are
+    compared with the resident ones."""
+    import ctypes
+    import numpy as np
+    from kodr_amd import device as kdev
+    G, n, W = len(encs), k + 2, k + L
+    earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    dW = ctx.alloc(G * n * W)
+    dO = ctx.alloc(G * k * L)
+    rows = (ctypes.c_void_p * G)(*[dW + g * n * W for g in range(G)])
+    counts = (ctypes.c_size_t * G)(*([n] * G))
+    e0, e1 = ctx.event(), ctx.event()
+    best, ok = None, True
+    for rep in range(reps + 1):        # rep 0 warms the path (pool buffers, twins of the decoders)
+        decs = []
+        for g in range(G):
+            h = ctypes.c_void_p()
+            errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+            decs.append(h)
+        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ctx.record(e0)
+        errors.check(L_.rlnc_encoder_group_coded_wire_device(earr, G, n, dW, W))
+        ctx.record(e1)
+        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+        errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, rows, counts, W, L, cons, sts))
+        t1 = time.perf_counter()
+        errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, dO, L))
+        ctx.synchronize()
+        t2 = time.perf_counter()
+        t_enc = kdev.Context.elapsed_ms(e0, e1) / 1e3
+        ok = ok and all(s_ in (0, 3) for s_ in sts) and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
+        for x in decs:
+            L_.rlnc_decoder_destroy(x)
+        if rep and (best is None or t2 - t0 < best[0]):
+            best = (t2 - t0, t_enc, t1 - t0, t2 - t1)
+    pitch = ctypes.c_size_t()
+    for g in (0, G - 1):
+        dp = L_.rlnc_encoder_device_pieces(encs[g], ctypes.byref(pitch))
+        a = ctx.d2h(dO + g * k * L, k * L)
+        b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
+        ok = ok and bool(np.array_equal(a, b))
+    ctx.free(dW)
+    ctx.free(dO)
+    t, t_enc, t_add, t_get = best
+    enc_units = G * n * setbytes(k, L)                 # benches/full/encoder_test.go:53 per coded piece
+    dec_units = G * k * (k + L)                        # DecodableLen per decoded generation
+    apply_macs = G * k * k * L
+    return {
+        "generations": G, "coded_pieces_per_generation": n,
+        "ms": round(t * 1e3, 3), "us_per_generation": round(t / G * 1e6, 1),
+        "payload_MBps": round(G * k * L / t / 1e6, 1),
+        "kodr_units_MBps": round((enc_units + dec_units) / t / 1e6, 1),
+        "encode_us_per_generation": round(t_enc / G * 1e6, 2),
+        "add_us_per_generation": round(t_add / G * 1e6, 1),
+        "get_us_per_generation": round(t_get / G * 1e6, 1),
+        "encode_coded_MBps": round(enc_units / t_enc / 1e6, 1),
+        "decode_apply": {"gf_macs_per_s": float(f"{apply_macs / t_get:.4g}"),
+                         "issue_frac": round(apply_macs / t_get / VALU_FLOOR_MACS_PER_S, 4),
+                         "hbm_GBps": round(G * (k * L + k * L) / t_get / 1e9, 1),
+                         "note": "grouped GetPieces wall time (host T staging included): k x k x L GF MACs per "
+                                 "generation against the bit-sliced VALU floor; hbm = received twin read once + "
+                                 "decoded pieces written"},
+        "roundtrip_ok": ok,
+        "note": "one round trip per generation: k + 2 coded wire rows (grouped encode, HIP events) + one batched "
+                "AddPiece (GPU elimination) + one grouped GetPieces, device-resident, wall time; payload_MBps = "
+                "original bytes through encode and decode per second; kodr_units_MBps = (k+2) x SetBytes "
+                "(encoder bench) + DecodableLen (decoder bench) per generation per second"}
 
 
 def c2_decode_grouped(ctx, L_, errors, encs, k, L, reps=3):

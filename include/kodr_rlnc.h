@@ -191,6 +191,21 @@ int rlnc_encoder_compact(rlnc_encoder* enc);
 int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
                                            size_t count, uint8_t* d_out, size_t out_pitch);
 
+/* Many generations' wire rows in one call: `count` coded pieces of each of
+ * n_enc resident generations (one ctx, equal k and L) as rlnc_encoder_coded_wire_device
+ * would write them -- generation i's rows at d_wire + i*count*wire_pitch, each
+ * `vector ++ piece` (CodedPiece.Flatten, data.go:52-57) with the vector drawn
+ * from that encoder's own device stream (data.go:90-95 replaced as in
+ * rlnc_encoder_coded_wire_device), and a systematic encoder's first k pieces
+ * e_id ++ P_id (systematic/encoder.go:82-109).  When every encoder is at the
+ * same point of its systematic phase and k, wire_pitch and d_wire are
+ * multiples of 16, ONE vector launch and one product launch per 32
+ * generations; otherwise encoder by encoder.  Same bytes and the same
+ * per-encoder stream state either way.  count <= 65535.  Async on the ctx
+ * stream. */
+int rlnc_encoder_group_coded_wire_device(rlnc_encoder* const* encs, size_t n_enc, size_t count, uint8_t* d_wire,
+                                         size_t wire_pitch);
+
 /* ---- recoder: full/recoder.go ------------------------------------------ */
 /* NewFullRLNCRecoderWithFlattenData (full/recoder.go:63-70): flat holds
  * piece_count coded pieces (wire layout), each pieces_coded_together + L bytes */
@@ -330,6 +345,21 @@ int rlnc_decoder_get_decoded(rlnc_decoder* dec, size_t j, uint8_t* out, int is_d
  * Binding drops the pieces materialized before it; GetPiece/GetPieces are
  * unchanged. */
 int rlnc_decoder_bind_output(rlnc_decoder* dec, uint8_t* d_out, size_t pitch);
+
+/* diagnostics: the plan of the last GF product launch made by the calling
+ * thread (any entry point above that multiplies), so tests can pin the exact
+ * kernel instance a benchmark times.  No kodr counterpart. */
+typedef struct rlnc_launch_plan {
+  int kernel;         /* 1 = gf_gemm_kernel (v_perm tables), 2 = gf_bs_kernel (bit-sliced), 0 = none yet */
+  int tile_rows;      /* output rows per workgroup tile (gf_bs_kernel: 8) */
+  int waves;          /* waves per workgroup splitting K (KW) */
+  int lane_groups;    /* gf_gemm_kernel: input rows per wave-step (S); gf_bs_kernel: 1 */
+  int ring;           /* rows (gf_bs) or row-steps (gf_gemm) in flight per wave */
+  int rows_per_wave;  /* input rows per wave (gf_gemm: per K-chunk) */
+  int generations;    /* grid rows: products in one grouped launch, else 1 */
+  int workgroups;     /* workgroups per generation (gridDim.x) */
+} rlnc_launch_plan;
+int rlnc_last_launch_plan(rlnc_launch_plan* out);
 
 /* ---- raw kernel entry: Y = A (x) X over GF(2^8) ------------------------ */
 /* Y[m][j] = XOR_k mul(A[m][k], X[k][j]) for m<M, j<ncols.  A is M x K host

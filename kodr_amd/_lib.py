@@ -65,6 +65,7 @@ SIGNATURES = {
     "rlnc_encoder_prepare": (_int, [_vp]),
     "rlnc_encoder_compact": (_int, [_vp]),
     "rlnc_encoder_group_coded_pieces_device": (_int, [_vpp, _sz, _vp, _sz, _vp, _sz]),
+    "rlnc_encoder_group_coded_wire_device": (_int, [_vpp, _sz, _sz, _vp, _sz]),
     "rlnc_recoder_create": (_int, [_vp, _u8p, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_create_device": (_int, [_vp, _vp, _sz, _sz, _sz, _sz, _vpp]),
     "rlnc_recoder_destroy": (_int, [_vp]),
@@ -104,7 +105,25 @@ SIGNATURES = {
     "rlnc_bitslice_device": (_int, [_vp, _vp, _sz, _sz, _sz]),
     "rlnc_bs_body_offsets": (_int, [_vp, _vp]),
     "rlnc_gf_matmul_bs_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
+    "rlnc_last_launch_plan": (_int, [_vp]),
 }
+
+
+class LaunchPlan(ctypes.Structure):
+    """rlnc_launch_plan (include/kodr_rlnc.h): the last product launch of this thread."""
+    _fields_ = [(n, ctypes.c_int) for n in ("kernel", "tile_rows", "waves", "lane_groups", "ring",
+                                            "rows_per_wave", "generations", "workgroups")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+def last_launch_plan():
+    p = LaunchPlan()
+    rc = lib().rlnc_last_launch_plan(ctypes.byref(p))
+    if rc != 0:
+        raise RuntimeError(f"rlnc_last_launch_plan: {rc}")
+    return p.as_dict()
 
 _lib = None
 _lock = threading.Lock()

@@ -726,22 +726,22 @@ static size_t group_bs_min() {
   return v;
 }
 
-int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
-                                           size_t count, uint8_t* d_out, size_t out_pitch) {
-  if (!encs || (n_enc && (!encs[0] || (count && (!d_vectors || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
-  if (!n_enc || !count) return RLNC_OK;
+namespace {
+
+// count coded pieces of each of n_enc resident generations (one ctx, one
+// k and L): generation i's coefficient rows at dA + i * a_stride (pitch lda),
+// its pieces at dY + i * y_stride (pitch ldy).  One launch streams up to
+// kGemmGroupMax generations where the product runs in one row chunk (small
+// batches on gf_gemm over the plain rows, larger ones on gf_bs_kernel over
+// the twins); otherwise one product per generation.
+int group_encode(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* dA, size_t lda, size_t a_stride,
+                 size_t count, uint8_t* dY, size_t ldy, size_t y_stride) {
   rlnc_encoder* e0 = encs[0];
-  const size_t k = e0->k, L = e0->L;
-  if (out_pitch < L) return RLNC_ERR_INVALID_ARGUMENT;
-  for (size_t i = 1; i < n_enc; i++)
-    if (!encs[i] || encs[i]->ctx != e0->ctx || encs[i]->k != k || encs[i]->L != L) return RLNC_ERR_INVALID_ARGUMENT;
-  TRY(set_dev(e0->ctx));
   rlnc_ctx* ctx = e0->ctx;
-  const size_t vstride = count * k, ostride = count * out_pitch;
-  // one launch streams up to kGemmGroupMax generations where the product runs on
-  // gf_gemm in one row chunk; otherwise one product per generation
+  const size_t k = e0->k, L = e0->L;
+  const bool yal = (ldy % 16) == 0 && ((uintptr_t)dY % 16) == 0 && (y_stride % 16) == 0;
   bool grouped = !resident_uses_bs(ctx, count, k, e0->pitch, L) && k * e0->pitch < kMaxDescBytes &&
-                 (e0->pitch % 16) == 0 && (out_pitch % 16) == 0;
+                 (e0->pitch % 16) == 0 && yal;
   for (size_t i = 0; i < n_enc && grouped; i++) grouped = !encs[i]->compact;  // the grouped launch reads plain rows
   // larger batches: one bit-sliced launch per kGemmGroupMax generations over
   // their twins, when the product is a single row chunk.  Smaller batches
@@ -754,8 +754,8 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
                (e0->pitch % 32) == 0 && kodr_amd::bs_ready(ctx->device);
   for (size_t i = 0; i < n_enc && twins; i++) twins = encs[i]->compact || encs[i]->bs_valid;
   if (twins) grouped = false;
-  bool grouped_bs = !grouped && (twins || resident_uses_bs(ctx, count, k, e0->pitch, L)) &&
-                    bs_chunk_rows(count, k, e0->pitch, L) >= k && (out_pitch % 16) == 0;
+  const bool grouped_bs = !grouped && (twins || resident_uses_bs(ctx, count, k, e0->pitch, L)) &&
+                          bs_chunk_rows(count, k, e0->pitch, L) >= k && yal;
   if (grouped_bs) {
     for (size_t i = 0; i < n_enc; i++)
       if (!encs[i]->compact)
@@ -764,26 +764,51 @@ int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_e
     for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
       const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
       for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces_bs.p;
-      const kodr_amd::GemmGroupArgs grp{(int)n, xs, vstride, ostride};
-      HIPC(kodr_amd::gf_gemm_bs(d_vectors + g0 * vstride, k, count, k, xs[0], e0->pitch, d_out + g0 * ostride,
-                                out_pitch, L, ctx->device, ctx->stream, false, &grp));
+      const kodr_amd::GemmGroupArgs grp{(int)n, xs, a_stride, y_stride};
+      HIPC(kodr_amd::gf_gemm_bs(dA + g0 * a_stride, lda, count, k, xs[0], e0->pitch, dY + g0 * y_stride, ldy, L,
+                                ctx->device, ctx->stream, false, &grp));
     }
     return RLNC_OK;
   }
   if (!grouped) {
-    for (size_t i = 0; i < n_enc; i++)
-      TRY(rlnc_encoder_coded_pieces_device(encs[i], d_vectors + i * vstride, count, d_out + i * ostride, out_pitch));
+    for (size_t i = 0; i < n_enc; i++) {
+      rlnc_encoder* e = encs[i];
+      TRY(gemm_resident(ctx, dA + i * a_stride, lda, count, k, e->compact ? nullptr : e->pieces.p, e->pieces_bs,
+                        e->bs_valid, e->pitch, dY + i * y_stride, ldy, L));
+    }
     return RLNC_OK;
   }
   const uint8_t* xs[kodr_amd::kGemmGroupMax];
   for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
     const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
     for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces.p;
-    const kodr_amd::GemmGroupArgs grp{(int)n, xs, vstride, ostride};
-    HIPC(kodr_amd::gf_gemm(d_vectors + g0 * vstride, k, count, k, xs[0], e0->pitch, d_out + g0 * ostride, out_pitch,
-                           L, ctx->stream, nullptr, false, &grp));
+    const kodr_amd::GemmGroupArgs grp{(int)n, xs, a_stride, y_stride};
+    HIPC(kodr_amd::gf_gemm(dA + g0 * a_stride, lda, count, k, xs[0], e0->pitch, dY + g0 * y_stride, ldy, L,
+                           ctx->stream, nullptr, false, &grp));
   }
   return RLNC_OK;
+}
+
+// encoders of one ctx with equal k and L
+int check_group(rlnc_encoder* const* encs, size_t n_enc) {
+  rlnc_encoder* e0 = encs[0];
+  for (size_t i = 1; i < n_enc; i++)
+    if (!encs[i] || encs[i]->ctx != e0->ctx || encs[i]->k != e0->k || encs[i]->L != e0->L)
+      return RLNC_ERR_INVALID_ARGUMENT;
+  return RLNC_OK;
+}
+
+}  // namespace
+
+int rlnc_encoder_group_coded_pieces_device(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* d_vectors,
+                                           size_t count, uint8_t* d_out, size_t out_pitch) {
+  if (!encs || (n_enc && (!encs[0] || (count && (!d_vectors || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!n_enc || !count) return RLNC_OK;
+  rlnc_encoder* e0 = encs[0];
+  if (out_pitch < e0->L) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(check_group(encs, n_enc));
+  TRY(set_dev(e0->ctx));
+  return group_encode(encs, n_enc, d_vectors, e0->k, count * e0->k, count, d_out, out_pitch, count * out_pitch);
 }
 
 int rlnc_encoder_seed(rlnc_encoder* e, uint64_t seed) {
@@ -827,6 +852,71 @@ int rlnc_encoder_coded_wire_device(rlnc_encoder* e, size_t count, uint8_t* d_wir
   }
   e->sys_next += n_sys;
   e->drawn += count;
+  return RLNC_OK;
+}
+
+int rlnc_encoder_group_coded_wire_device(rlnc_encoder* const* encs, size_t n_enc, size_t count, uint8_t* d_wire,
+                                         size_t wire_pitch) {
+  if (!encs || (n_enc && (!encs[0] || (count && !d_wire)))) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!n_enc || !count) return RLNC_OK;
+  rlnc_encoder* e0 = encs[0];
+  const size_t k = e0->k, L = e0->L, wp = wire_pitch, gstride = count * wire_pitch;
+  if (wp < k + L || count > 65535) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(check_group(encs, n_enc));
+  TRY(set_dev(e0->ctx));
+  rlnc_ctx* ctx = e0->ctx;
+  hipStream_t st = ctx->stream;
+  // every encoder at the same point of its systematic phase (all full
+  // encoders, or systematic ones created together) and 16-byte aligned piece
+  // columns: one vector launch and grouped products; otherwise encoder by
+  // encoder (same bytes, same stream state)
+  auto n_sys_of = [&](const rlnc_encoder* e) -> size_t {
+    return (e->kind == RLNC_SYSTEMATIC && e->sys_next < k) ? std::min(count, k - e->sys_next) : 0;
+  };
+  const size_t n_sys = n_sys_of(e0);
+  bool grouped = (k % 16) == 0 && (wp % 16) == 0 && ((uintptr_t)d_wire % 16) == 0;
+  for (size_t i = 1; i < n_enc && grouped; i++) grouped = n_sys_of(encs[i]) == n_sys;
+  if (!grouped) {
+    for (size_t i = 0; i < n_enc; i++) TRY(rlnc_encoder_coded_wire_device(encs[i], count, d_wire + i * gstride, wp));
+    return RLNC_OK;
+  }
+  // the vectors of every row of every encoder from its own stream
+  // (data.go:90-95 per coded piece; e_id for systematic rows,
+  // systematic/encoder.go:60-68)
+  for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
+    const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
+    kodr_amd::VectorGroup vg = {};
+    for (size_t i = 0; i < n; i++) {
+      const rlnc_encoder* e = encs[g0 + i];
+      vg.v[i] = d_wire + (g0 + i) * gstride;
+      vg.seed[i] = e->seed;
+      vg.row0[i] = e->drawn;
+      vg.n_sys[i] = (int)n_sys;
+      vg.sys_first[i] = (int)e->sys_next;
+    }
+    HIPC(kodr_amd::fill_vectors_grouped(vg, (int)n, wp, count, k, st));
+  }
+  // systematic rows: e_id x P = P_id, strided copies (systematic/encoder.go:83-96)
+  for (size_t i = 0; i < n_enc && n_sys; i++) {
+    rlnc_encoder* e = encs[i];
+    uint8_t* dst = d_wire + i * gstride + k;
+    if (e->compact)
+      TRY(uncompact_rows(ctx, e->pieces_bs, e->pitch, e->sys_next, n_sys, L, e->out, dst, wp));
+    else
+      HIPC(hipMemcpy2DAsync(dst, wp, e->pieces.p + e->sys_next * e->pitch, e->pitch, L, n_sys,
+                            hipMemcpyDeviceToDevice, st));
+  }
+  // coded rows: their vectors are read in place as the coefficient rows
+  // (full/encoder.go:61-71, wire layout data.go:52-57)
+  const size_t nc = count - n_sys;
+  if (nc) {
+    uint8_t* w0 = d_wire + n_sys * wp;
+    TRY(group_encode(encs, n_enc, w0, wp, gstride, nc, w0 + k, wp, gstride));
+  }
+  for (size_t i = 0; i < n_enc; i++) {
+    encs[i]->sys_next += n_sys;
+    encs[i]->drawn += count;
+  }
   return RLNC_OK;
 }
 
@@ -1751,6 +1841,14 @@ int rlnc_decoder_get_decoded(rlnc_decoder* d, size_t j, uint8_t* out, int is_dev
   }
   HIPC(d->ctx->stage.d2h(out, d->L, src, d->pitch, d->L, 1, st));
   HIPC(hipStreamSynchronize(st));
+  return RLNC_OK;
+}
+
+int rlnc_last_launch_plan(rlnc_launch_plan* out) {
+  if (!out) return RLNC_ERR_INVALID_ARGUMENT;
+  const kodr_amd::LaunchPlan& p = kodr_amd::last_launch_plan();
+  *out = rlnc_launch_plan{p.kernel, p.tile_rows, p.waves, p.lane_groups, p.ring, p.rows_per_wave, p.generations,
+                          p.workgroups};
   return RLNC_OK;
 }
 

@@ -571,9 +571,11 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     constexpr int rp = MODE == 0 ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
                        lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+    last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
   } else {
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
                        ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+    last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, KODR_BS_P, rpw, 1, nb};
   }
   return hipGetLastError();
 }

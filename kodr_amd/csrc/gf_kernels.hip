@@ -31,6 +31,11 @@
 
 namespace kodr_amd {
 
+LaunchPlan& last_launch_plan() {
+  static thread_local LaunchPlan p;
+  return p;
+}
+
 namespace {
 
 __device__ __forceinline__ uint32_t xt(uint32_t c) {  // multiply by x (=2) mod 0x11D
@@ -322,6 +327,7 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
   }
   hipLaunchKernelGGL((gf_gemm_kernel<MT, KW, S, RC, P, MODE, AUX>), dim3(nx8 * ny, ng), dim3(64 * KW), lds, stream,
                      A, lda, M, K, X, ldx, Y, ldy, ncols, nx, ny, nbuf, accum, xg, as, ys);
+  last_launch_plan() = LaunchPlan{1, MT, KW, S, P, RC, (int)ng, nx8 * ny};
   return hipGetLastError();
 }
 
@@ -463,7 +469,26 @@ __global__ __launch_bounds__(256) void fill_vectors_kernel(uint8_t* __restrict__
   V[(size_t)r * ldv + j] = b;
 }
 
+// fill_vectors_kernel for several encoders at once (blockIdx.z = encoder)
+__global__ __launch_bounds__(256) void fill_vectors_grouped_kernel(VectorGroup g, size_t ldv, int k) {
+  const int e = blockIdx.z, r = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= k) return;
+  uint8_t b;
+  if (r < g.n_sys[e]) b = (j == g.sys_first[e] + r) ? 1 : 0;
+  else b = (uint8_t)splitmix64(g.seed[e] + ((g.row0[e] + (uint64_t)r) << 32) + (uint64_t)j);
+  g.v[e][(size_t)r * ldv + j] = b;
+}
+
 }  // namespace
+
+hipError_t fill_vectors_grouped(const VectorGroup& g, int n, size_t ldv, size_t rows, size_t k, hipStream_t stream) {
+  if (!rows || !k || n <= 0) return hipSuccess;
+  if (n > kGemmGroupMax || rows > 65535 || k > (1u << 30)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fill_vectors_grouped_kernel, dim3((unsigned)((k + 255) / 256), (unsigned)rows, (unsigned)n),
+                     dim3(256), 0, stream, g, ldv, (int)k);
+  return hipGetLastError();
+}
 
 hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
                         size_t n_sys, size_t sys_first, hipStream_t stream) {

@@ -15,6 +15,15 @@ struct GemmConfig {
 
 GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols);
 
+// What the last product launch of this thread ran (diagnostics behind
+// rlnc_last_launch_plan: tests pin the exact instance the bench times).
+// kernel 1 = gf_gemm_kernel, 2 = gf_bs_kernel.
+struct LaunchPlan {
+  int kernel = 0, tile_rows = 0, waves = 0, lane_groups = 0, ring = 0, rows_per_wave = 0, generations = 0,
+      workgroups = 0;
+};
+LaunchPlan& last_launch_plan();
+
 // A group of independent products of one shape (M, K, ncols, pitches) in one
 // launch: product i reads X = x[i], A + i * a_stride and writes Y + i * y_stride.
 constexpr int kGemmGroupMax = 32;
@@ -69,6 +78,14 @@ hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, siz
 // the rest counter-based pseudo-random bytes of (seed, row0 + r).  rows <= 65535.
 hipError_t fill_vectors(uint8_t* dV, size_t ldv, size_t rows, size_t k, uint64_t seed, uint64_t row0,
                         size_t n_sys, size_t sys_first, hipStream_t stream);
+// the same for n <= kGemmGroupMax encoders in one launch: encoder i writes
+// rows x k bytes at v[i] (pitch ldv) from its own (seed, row0, n_sys, sys_first)
+struct VectorGroup {
+  uint8_t* v[kGemmGroupMax];
+  uint64_t seed[kGemmGroupMax], row0[kGemmGroupMax];
+  int n_sys[kGemmGroupMax], sys_first[kGemmGroupMax];
+};
+hipError_t fill_vectors_grouped(const VectorGroup& g, int n, size_t ldv, size_t rows, size_t k, hipStream_t stream);
 
 // ---- decoder elimination on the GPU (gf_elim.hip) ----
 // One workgroup per decoder: Gauss-Jordan of the first n coding vectors of

@@ -71,6 +71,51 @@ def test_headline_launch_full_compare(gpu_ctx, c2_generation, B):
     assert not ref[0].any() and np.array_equal(ref[1], P[7])
 
 
+def test_bench_headline_step_exact(gpu_ctx):
+    # The bench's timed step itself (bench.HeadlineStep, the object bench.py
+    # times): 16 prepared 32 MiB/256 generations x B = 32 coded pieces in one
+    # grouped call.  The launch must be the instance the bench reports
+    # (gf_bs_kernel, KW = 4 waves per workgroup, the two-row ring, 64 rows per
+    # wave, 16 generations), and every one of the 512 pieces must equal the
+    # oracle's encode (full/encoder.go:61-71).
+    import bench
+    hs = bench.HeadlineStep(gpu_ctx, _lib.lib(), errors, 256, 131072, 32, 16, grouped=True,
+                            rng=np.random.default_rng(0xBE7C), nvec=2, keep_data=True)
+    try:
+        hs.step(1)
+        plan = _lib.last_launch_plan()
+        gpu_ctx.synchronize()
+        got = gpu_ctx.d2h(hs.dOut, 16 * 32 * 131072).reshape(16, 32, 131072)
+    finally:
+        hs.close()
+    assert plan == {"kernel": 2, "tile_rows": 8, "waves": 4, "lane_groups": 1, "ring": 2, "rows_per_wave": 64,
+                    "generations": 16, "workgroups": 256}, plan
+    for g in range(16):
+        P = hs.datas[g].reshape(256, 131072)
+        assert np.array_equal(got[g], oracle.encode(P, hs.V[1, g])), g
+
+
+# grouped bit-sliced launches that plan each KW instance of
+# gf_bs_kernel<KW, 0, true, 2> (capi.cpp plan_gemm_bs): (G, k, L, count) -> KW
+GROUPED_KW_SHAPES = [((2, 8, 4096, 40), 1), ((2, 16, 4096, 40), 2), ((2, 24, 4096, 17), 3),
+                     ((2, 32, 4096, 17), 4), ((2, 40, 4096, 9), 6), ((2, 64, 4096, 9), 8),
+                     ((2, 96, 4096, 9), 16)]
+
+
+@pytest.mark.parametrize("shape,kw", GROUPED_KW_SHAPES)
+def test_grouped_bitsliced_every_kw(gpu_ctx, shape, kw):
+    G, k, L, count = shape
+    rng = np.random.default_rng(kw * 101 + k)
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+    V[0, 0] = 0
+    got = group_run(gpu_ctx, gens, count, V, out_pitch=L + 16, prepare=True)
+    plan = _lib.last_launch_plan()
+    assert (plan["kernel"], plan["waves"], plan["ring"], plan["generations"]) == (2, kw, 2, G), plan
+    for g in range(G):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
 def test_prepare_matches_lazy_twin(gpu_ctx):
     # prepare (eager twin) and the lazy twin of the first large batch give
     # the same bytes; prepare is idempotent
