@@ -112,11 +112,16 @@ struct rlnc_encoder {
 struct rlnc_recoder {
   rlnc_ctx* ctx = nullptr;
   size_t n = 0, k = 0, clen = 0, pitch = 0;
-  DevBuf flat;               // n x pitch wire rows
-  DevBuf flat_bs;            // bit-sliced twin, built on first large batch
+  size_t L = 0, ppitch = 0;  // piece length (clen - k) and the piece twin's pitch
+  DevBuf flat;               // n x pitch wire rows (released when compact)
+  DevBuf flat_bs;            // bit-sliced twin of the wire rows (shapes the split layout cannot take)
   bool bs_valid = false;
-  bool compact = false;      // rlnc_recoder_compact: only the twin is resident
-  DevBuf r, out;
+  DevBuf piece_bs;           // split layout: bit-sliced twin of the piece columns only (pitch ppitch)
+  bool piece_bs_valid = false;
+  DevBuf vecs;               // compact split recoder: the n coding vectors (pitch vpitch)
+  size_t vpitch = 0;
+  bool compact = false;      // rlnc_recoder_compact: only the twin (and, split, the vectors) resident
+  DevBuf r, out, scratch;
 };
 
 struct rlnc_decoder {
@@ -921,24 +926,85 @@ int rlnc_encoder_group_coded_wire_device(rlnc_encoder* const* encs, size_t n_enc
 }
 
 /* ---- recoder ------------------------------------------------------------ */
-static int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_recoder** out) {
+namespace {
+
+// Split layout.  A product of >= kBsMinRows recoded pieces reads a
+// bit-sliced twin of the held pieces' columns only (pitch round_up(L, 256):
+// at 32 MiB/256 exactly the encoder's 64 column chunks of 2 KiB), and the
+// recoded coding vectors r x C (matrix.go:45-69) come from a narrow gf_gemm
+// over the k vector columns.  A twin of the whole wire rows (k + L columns)
+// has a 65th, 256-byte column chunk, which took the bit-sliced launch from
+// one round of workgroups to two (B = 32: 30 us against 19.5 for the same
+// MACs in an encode).  Wire-row twins remain for k not a multiple of 16.
+bool rec_split(const rlnc_recoder* r) {
+  return r->k % 16 == 0 && r->pitch % 16 == 0 && (r->ppitch % 32) == 0 && kodr_amd::bs_ready(r->ctx->device) &&
+         bs_chunk_rows(64, r->n, r->ppitch, r->L) >= r->n;
+}
+
+// the n coding vectors (k columns): the plain wire rows, or a compact recoder's copy
+const uint8_t* rec_vectors(const rlnc_recoder* r, size_t* ld) {
+  *ld = r->compact ? r->vpitch : r->pitch;
+  return r->compact ? r->vecs.p : r->flat.p;
+}
+
+int rec_build_piece_twin(rlnc_recoder* r) {
+  if (r->piece_bs_valid) return RLNC_OK;
+  TRY(r->piece_bs.reserve(std::max<size_t>(r->n * r->ppitch, 1)));
+  HIPC(kodr_amd::bitslice_rows_pitched(r->flat.p + r->k, r->pitch, r->piece_bs.p, r->ppitch, r->n, r->L,
+                                       r->ctx->stream));
+  r->piece_bs_valid = true;
+  return RLNC_OK;
+}
+
+// this product takes the split layout
+bool rec_uses_split(const rlnc_recoder* r, size_t count) {
+  return rec_split(r) && (r->compact || resident_uses_bs(r->ctx, count, r->n, r->ppitch, r->L));
+}
+
+// count recoded wire rows [r x C | sum r_i P_i] (full/recoder.go:32-40) into
+// device rows dY (pitch ldy); dR: count x n recoding vectors
+int rec_product(rlnc_recoder* r, const uint8_t* dR, size_t count, uint8_t* dY, size_t ldy) {
+  rlnc_ctx* ctx = r->ctx;
+  const size_t n = r->n, k = r->k, L = r->L;
+  if (!rec_uses_split(r, count))  // one product over the wire rows
+    return gemm_resident(ctx, dR, n, count, n, r->compact ? nullptr : r->flat.p, r->flat_bs, r->bs_valid, r->pitch,
+                         dY, ldy, r->clen);
+  size_t ldv = 0;
+  const uint8_t* C = rec_vectors(r, &ldv);
+  TRY(gemm(ctx, dR, n, count, n, C, ldv, dY, ldy, k));
+  if (!r->compact) TRY(rec_build_piece_twin(r));
+  uint8_t* yp = dY + k;
+  if ((uintptr_t)yp % 16 == 0 && ldy % 16 == 0) return gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, yp, ldy, L);
+  // piece columns not 16-byte aligned: compute aside, then one strided copy
+  TRY(r->scratch.reserve(count * r->ppitch));
+  TRY(gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, r->scratch.p, r->ppitch, L));
+  HIPC(hipMemcpy2DAsync(yp, ldy, r->scratch.p, r->ppitch, L, count, hipMemcpyDeviceToDevice, ctx->stream));
+  return RLNC_OK;
+}
+
+int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_recoder** out) {
   if (!ctx || !out || n == 0) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(ctx));
   rlnc_recoder* r = new (std::nothrow) rlnc_recoder;
   if (!r) return RLNC_ERR_OUT_OF_MEMORY;
   r->ctx = ctx;
-  for (DevBuf* b : {&r->flat, &r->flat_bs, &r->r, &r->out}) b->bind(ctx->device, ctx->stream);
+  for (DevBuf* b : {&r->flat, &r->flat_bs, &r->piece_bs, &r->vecs, &r->r, &r->out, &r->scratch})
+    b->bind(ctx->device, ctx->stream);
   r->n = n;
   r->k = k;
   r->clen = clen;
+  r->L = clen - k;
   r->pitch = round_up(clen, kPitchAlign);
+  r->ppitch = round_up(std::max<size_t>(r->L, 1), kPitchAlign);
   if (r->pitch >= kMaxDescBytes) {
     delete r;
     return RLNC_ERR_INVALID_ARGUMENT;
   }
-  int s = r->flat.reserve(n * r->pitch);
+  // (32 bytes of slack: the piece twin reads each row's piece columns up to
+  // the next 32-byte block)
+  int s = r->flat.reserve(n * r->pitch + 32);
   if (s == RLNC_OK) {
-    hipError_t he = hipMemsetAsync(r->flat.p, 0, n * r->pitch, ctx->stream);
+    hipError_t he = hipMemsetAsync(r->flat.p, 0, n * r->pitch + 32, ctx->stream);
     if (he != hipSuccess) s = hip_fail(he, "hipMemsetAsync");
   }
   if (s != RLNC_OK) {
@@ -949,6 +1015,8 @@ static int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_re
   *out = r;
   return RLNC_OK;
 }
+
+}  // namespace
 
 int rlnc_recoder_create(rlnc_ctx* ctx, const uint8_t* flat, size_t len, size_t n, size_t together,
                         rlnc_recoder** out) {
@@ -986,24 +1054,39 @@ int rlnc_recoder_create_device(rlnc_ctx* ctx, const uint8_t* d_flat, size_t n, s
 int rlnc_recoder_prepare(rlnc_recoder* r) {
   if (!r) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(r->ctx));
-  if (r->compact || !resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->pitch, r->clen)) return RLNC_OK;
+  if (r->compact) return RLNC_OK;
+  if (rec_split(r))
+    return resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->ppitch, r->L) ? rec_build_piece_twin(r)
+                                                                                       : RLNC_OK;
+  if (!resident_uses_bs(r->ctx, std::max<size_t>(r->n, 64), r->n, r->pitch, r->clen)) return RLNC_OK;
   return build_twin(r->ctx, r->flat.p, r->flat_bs, r->bs_valid, r->n, r->pitch, r->clen);
 }
 
 int rlnc_recoder_compact(rlnc_recoder* r) {
   if (!r) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(r->ctx));
-  return compact_resident(r->ctx, r->flat, r->flat_bs, r->bs_valid, r->compact, r->n, r->pitch, r->clen);
+  if (r->compact) return RLNC_OK;
+  if (!rec_split(r))
+    return compact_resident(r->ctx, r->flat, r->flat_bs, r->bs_valid, r->compact, r->n, r->pitch, r->clen);
+  // split: the piece twin plus a copy of the n coding vectors
+  TRY(rec_build_piece_twin(r));
+  r->vpitch = round_up(r->k, 16);
+  TRY(r->vecs.reserve(r->n * r->vpitch));
+  HIPC(hipMemcpy2DAsync(r->vecs.p, r->vpitch, r->flat.p, r->pitch, r->k, r->n, hipMemcpyDeviceToDevice,
+                        r->ctx->stream));
+  HIPC(hipStreamSynchronize(r->ctx->stream));
+  r->flat.release();
+  r->flat_bs.release();
+  r->bs_valid = false;
+  r->compact = true;
+  return RLNC_OK;
 }
 
 int rlnc_recoder_destroy(rlnc_recoder* r) {
   if (!r) return RLNC_OK;
   (void)hipSetDevice(r->ctx->device);
   (void)hipStreamSynchronize(r->ctx->stream);
-  r->flat.release();
-  r->flat_bs.release();
-  r->r.release();
-  r->out.release();
+  for (DevBuf* b : {&r->flat, &r->flat_bs, &r->piece_bs, &r->vecs, &r->r, &r->out, &r->scratch}) b->release();
   delete r;
   return RLNC_OK;
 }
@@ -1021,9 +1104,7 @@ int rlnc_recoder_coded_pieces(rlnc_recoder* r, const uint8_t* rv, size_t count, 
     TRY(r->r.reserve(B * r->n));
     TRY(r->out.reserve(B * r->pitch));
     HIPC(r->ctx->stage.h2d(r->r.p, r->n, rv + i * r->n, r->n, r->n, B, st));
-    // wire rows in, wire rows out: [r x C | sum r_i P_i] (full/recoder.go:32-40)
-    TRY(gemm_resident(r->ctx, r->r.p, r->n, B, r->n, r->flat.p, r->flat_bs, r->bs_valid, r->pitch, r->out.p,
-                      r->pitch, r->clen));
+    TRY(rec_product(r, r->r.p, B, r->out.p, r->pitch));
     HIPC(r->ctx->stage.d2h(out + i * r->clen, r->clen, r->out.p, r->pitch, r->clen, B, st));
     i += B;
   }
@@ -1033,34 +1114,69 @@ int rlnc_recoder_coded_pieces(rlnc_recoder* r, const uint8_t* rv, size_t count, 
 int rlnc_recoder_coded_pieces_device(rlnc_recoder* r, const uint8_t* d_r, size_t count,
                                      uint8_t* d_out, size_t out_pitch) {
   if (!r || (count && (!d_r || !d_out)) || out_pitch < r->clen) return RLNC_ERR_INVALID_ARGUMENT;
+  if (!count) return RLNC_OK;
   TRY(set_dev(r->ctx));
-  return gemm_resident(r->ctx, d_r, r->n, count, r->n, r->flat.p, r->flat_bs, r->bs_valid, r->pitch, d_out,
-                       out_pitch, r->clen);
+  return rec_product(r, d_r, count, d_out, out_pitch);
 }
 
 // Recoders of one context and shape (n, clen) at once: count recoded pieces
-// of each (full/recoder.go:27-46 per generation) in one launch per
-// kGemmGroupMax recoders -- gf_gemm on the plain rows below kBsMinRows,
-// gf_bs_kernel on the twins from there -- else one call per recoder.
+// of each (full/recoder.go:27-46 per generation).  Split layout (every
+// recoder): one narrow gf_gemm launch for the vector columns and one
+// bit-sliced launch over the piece twins per kGemmGroupMax recoders; else
+// one launch over the wire rows (gf_gemm below kBsMinRows, gf_bs_kernel on
+// the wire-row twins from there); else one call per recoder.  Same bytes.
 int rlnc_recoder_group_coded_pieces_device(rlnc_recoder* const* recs, size_t n_rec, const uint8_t* d_r,
                                            size_t count, uint8_t* d_out, size_t out_pitch) {
   if (!recs || (n_rec && (!recs[0] || (count && (!d_r || !d_out))))) return RLNC_ERR_INVALID_ARGUMENT;
   if (!n_rec || !count) return RLNC_OK;
   rlnc_recoder* r0 = recs[0];
-  const size_t n = r0->n, clen = r0->clen, pitch = r0->pitch;
+  const size_t n = r0->n, clen = r0->clen, pitch = r0->pitch, k = r0->k, L = r0->L;
   if (out_pitch < clen) return RLNC_ERR_INVALID_ARGUMENT;
   for (size_t i = 1; i < n_rec; i++)
     if (!recs[i] || recs[i]->ctx != r0->ctx || recs[i]->n != n || recs[i]->clen != clen) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(r0->ctx));
   rlnc_ctx* ctx = r0->ctx;
   const size_t rstride = count * n, ostride = count * out_pitch;
+  const bool oal = (out_pitch % 16) == 0 && ((uintptr_t)d_out % 16) == 0 && n_rec > 1;
   // as for encoders: from kGroupBsMinRows pieces on resident twins (prepared
   // or compact recoders), else from kBsMinRows
-  bool twins = count >= group_bs_min() && count < kBsMinRows && !few_narrow_rows(count, n, clen) &&
-               (pitch % 32) == 0 && kodr_amd::bs_ready(ctx->device);
-  for (size_t i = 0; i < n_rec && twins; i++) twins = recs[i]->compact || recs[i]->bs_valid;
+  const bool small = count >= group_bs_min() && count < kBsMinRows && !few_narrow_rows(count, n, clen) &&
+                     kodr_amd::bs_ready(ctx->device);
+  // split layout for every recoder: vectors by one grouped gf_gemm, pieces by
+  // one grouped bit-sliced launch (their columns start at k, a multiple of 16)
+  bool split = oal && rec_split(r0);
+  bool twins_split = small;
+  for (size_t i = 0; i < n_rec && (split || twins_split); i++) {
+    twins_split = twins_split && (recs[i]->compact || recs[i]->piece_bs_valid);
+    split = split && (recs[i]->compact == r0->compact);
+  }
+  split = split && (twins_split || rec_uses_split(r0, count));
+  if (split) {
+    for (size_t i = 0; i < n_rec; i++)
+      if (!recs[i]->compact) TRY(rec_build_piece_twin(recs[i]));
+    const uint8_t* xs[kodr_amd::kGemmGroupMax];
+    size_t ldv = 0;
+    (void)rec_vectors(r0, &ldv);
+    for (size_t g0 = 0; g0 < n_rec; g0 += kodr_amd::kGemmGroupMax) {
+      const size_t m = std::min<size_t>(kodr_amd::kGemmGroupMax, n_rec - g0);
+      size_t ld = 0;
+      for (size_t i = 0; i < m; i++) xs[i] = rec_vectors(recs[g0 + i], &ld);
+      const kodr_amd::GemmGroupArgs gv{(int)m, xs, rstride, ostride};
+      HIPC(kodr_amd::gf_gemm(d_r + g0 * rstride, n, count, n, xs[0], ldv, d_out + g0 * ostride, out_pitch, k,
+                             ctx->stream, nullptr, false, &gv));
+      for (size_t i = 0; i < m; i++) xs[i] = recs[g0 + i]->piece_bs.p;
+      const kodr_amd::GemmGroupArgs gp{(int)m, xs, rstride, ostride};
+      HIPC(kodr_amd::gf_gemm_bs(d_r + g0 * rstride, n, count, n, xs[0], r0->ppitch, d_out + g0 * ostride + k,
+                                out_pitch, L, ctx->device, ctx->stream, false, &gp));
+    }
+    return RLNC_OK;
+  }
+  // wire-row products
+  bool twins = small && (pitch % 32) == 0;
+  for (size_t i = 0; i < n_rec && twins; i++) twins = !rec_split(recs[i]) && (recs[i]->compact || recs[i]->bs_valid);
   const bool bs = twins || resident_uses_bs(ctx, count, n, pitch, clen);
-  bool grouped = (out_pitch % 16) == 0 && n_rec > 1;
+  bool grouped = oal;
+  for (size_t i = 0; i < n_rec && grouped; i++) grouped = !rec_uses_split(recs[i], count);
   if (bs) {
     grouped = grouped && bs_chunk_rows(count, n, pitch, clen) >= n;
   } else {

@@ -475,6 +475,14 @@ def main():
     clob2 += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
     out.append("#define KODR_BS_CLOBBERS_P2 " + ", ".join(clob2) + ', "scc", "memory"')
     out.append(f"#define KODR_BS_VMAX_P2 {VMAX}")
+    # direct variant (KW = 1, no cross-wave fold): the accumulators leave the
+    # asm as outputs (early clobber: the prologue zeroes them before it reads
+    # every input) and the C++ epilogue transposes and stores them
+    acc_out = [f'"=&{{v[{ACC + 8 * m}:{ACC + 8 * m + 7}]}}"(acc[{m}])' for m in range(8)]
+    out.append("#define KODR_BS_ACC_OUTPUTS " + ", ".join(acc_out))
+    clob2d = [f'"v{r}"' for r in list(range(ACC + 64, RING)) + list(range(RING + 8 * P, VMAX))]
+    clob2d += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
+    out.append("#define KODR_BS_CLOBBERS_P2_DIRECT " + ", ".join(clob2d) + ', "scc", "memory"')
     set_ring(p0)
     out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "
                f"row prep {len(table_lines(0))} per row; {total} bytes of bodies")

@@ -90,6 +90,23 @@ __global__ __launch_bounds__(256) void bitslice_kernel(const uint8_t* src, uint8
   p[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// bitslice_kernel with separate source and destination pitches (the piece
+// columns of a recoder's wire rows into a twin of their own)
+__global__ __launch_bounds__(256) void bitslice_pitched_kernel(const uint8_t* __restrict__ src, size_t spitch,
+                                                              uint8_t* __restrict__ dst, size_t dpitch, int rows,
+                                                              int nblk) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = (int)(i / (size_t)nblk), b = (int)(i % (size_t)nblk);
+  if (r >= rows) return;
+  const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)r * spitch + (size_t)b * kBsBlock);
+  const uint4 a = q[0], c = q[1];
+  uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  bitslice32(d);
+  uint4* p = reinterpret_cast<uint4*>(dst + (size_t)r * dpitch + (size_t)b * kBsBlock);
+  p[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  p[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+
 // dst row r = src row r (bytes [0, nblk * 32)), and dst_bs row r = its
 // bit-sliced form: one read of the source for both, for the decoder's
 // received rows (plain rows for the GetPiece paths, the twin for T x R).
@@ -148,6 +165,7 @@ __global__ __launch_bounds__(64) void gf_bs_export_kernel(uint32_t* out) {
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
 
 // MODE (tuning builds only, -DKODR_TUNE_MODES): 3 = the row stream, table
 // prep and program reads without dispatching bodies, 4 = as 3 without the
@@ -197,8 +215,13 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     X = grp.x[g];
     Y += (size_t)g * grp.y_stride;
   }
+  // DIRECT (one wave per workgroup in a grouped launch): the wave runs all K
+  // rows of its task, so there is no cross-wave fold; its accumulators leave
+  // the asm in registers and are transposed and stored straight from there
+  // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
+  constexpr bool DIRECT = KW == 1 && GRP && MODE == 0 && RP == 2;
   uint32_t* red = lds;
-  uint32_t* tgt_l = lds + 64 * 64;
+  uint32_t* tgt_l = DIRECT ? lds : lds + 64 * 64;
   uint32_t* prog_l = tgt_l + 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if constexpr (MODE == 20) {
@@ -357,7 +380,8 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     const int i = tid + j * 64 * KW;
     if (i < kTgt) tgt_l[i] = ot[j];
   }
-  for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
+  if constexpr (!DIRECT)
+    for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
   __syncthreads();
   // program: entry e = the target of (output row m0 + e%8, input row kb + e/8):
   // body c in copy (e%8) & 3
@@ -405,6 +429,42 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #define KODR_BS_ASM2(MAIN, CLOB)                                                                    \
   asm volatile(MAIN KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t" : KODR_BS_RING_OPERANDS : KODR_BS_ASM_INPUTS : CLOB)
 #define KODR_BS_ASM(MAIN) KODR_BS_ASM2(MAIN, KODR_BS_CLOBBERS)
+  if constexpr (DIRECT) {
+    u32x8 acc[8];
+    if (nr > 0) {
+      asm volatile(KODR_BS_MAIN_P2 "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
+                   : KODR_BS_ASM_INPUTS
+                   : KODR_BS_CLOBBERS_P2_DIRECT);
+    } else {
+#pragma unroll
+      for (int m = 0; m < kBsRows; m++) acc[m] = u32x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    // rows m0..m0+7 of this lane's 32-byte block: planes -> bytes, store
+    const int cc = (cx * 64 + lane) * kBsBlock;
+#pragma unroll
+    for (int m = 0; m < kBsRows; m++) {
+      const int row = m0 + m;
+      if (row >= M || cc >= ncols) continue;
+      uint32_t d[8] = {acc[m][0], acc[m][1], acc[m][2], acc[m][3], acc[m][4], acc[m][5], acc[m][6], acc[m][7]};
+      bitslice32(d);
+      uint8_t* dst = Y + (size_t)row * ldy + cc;
+      if (cc + kBsBlock <= ncols) {
+        uint4 v0 = make_uint4(d[0], d[1], d[2], d[3]), v1 = make_uint4(d[4], d[5], d[6], d[7]);
+        if (accum) {
+          const uint4 o0 = reinterpret_cast<const uint4*>(dst)[0], o1 = reinterpret_cast<const uint4*>(dst)[1];
+          v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
+          v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
+        }
+        reinterpret_cast<uint4*>(dst)[0] = v0;
+        reinterpret_cast<uint4*>(dst)[1] = v1;
+      } else {
+        for (int i = 0; cc + i < ncols; i++)
+          dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
+      }
+    }
+    return;
+  }
   if (nr > 0 && MODE != 5) {
     if constexpr (RP != KODR_BS_P) {
       static_assert(RP == 2 && MODE == 0, "the two-row ring variant has the plain main loop only");
@@ -632,6 +692,18 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   return hipGetLastError();
 }
 
+hipError_t bitslice_rows_pitched(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows,
+                                 size_t ncols, hipStream_t stream) {
+  if (!rows || !ncols) return hipSuccess;
+  const size_t nblk = (ncols + kBsBlock - 1) / kBsBlock;
+  if ((uintptr_t)src % 16 || spitch % 16 || dpitch % kBsBlock || dpitch < nblk * kBsBlock) return hipErrorInvalidValue;
+  const size_t total = rows * nblk;
+  if (rows > 0x7fffffff || nblk > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bitslice_pitched_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, src,
+                     spitch, dst, dpitch, (int)rows, (int)nblk);
+  return hipGetLastError();
+}
+
 hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,
                          hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;
@@ -652,14 +724,22 @@ constexpr int kBsWavesPerSimd = 512 / ((KODR_BS_VMAX + 7) / 8 * 8);
 constexpr int kBsKw[] = {1, 2, 3, 4, 6, 8, 16};
 constexpr size_t kLdsPerCu = 160 * 1024;
 
-// row sums, the body target table, and KW programs of rpw rows x 8 targets
-size_t bs_lds_bytes(int kw, int rpw) {
-  return (64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4 + 16;  // + the dynamic rows' counter
+// row sums, the body target table, and KW programs of rpw rows x 8 targets;
+// the direct variant (KW = 1 in a grouped launch) has no row sums
+size_t bs_lds_bytes(int kw, int rpw, bool direct = false) {
+  return (direct ? 256 : 64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4 + 16;  // + the dynamic rows' counter
+}
+
+// KODR_BS_DIRECT=0/1: whether grouped launches may plan the direct variant
+// (A/B measurements)
+bool bs_direct_allowed() {
+  static const bool v = getenv("KODR_BS_DIRECT") ? atoi(getenv("KODR_BS_DIRECT")) != 0 : false;
+  return v;
 }
 
 }  // namespace
 
-BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups) {
+BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups, bool grouped) {
   BsPlan p;
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
   p.nrg = (int)((M + kBsRows - 1) / kBsRows);
@@ -672,7 +752,7 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups) {
   for (int kw : kBsKw) {
     if (kw > 4 * kBsWavesPerSimd) continue;  // one workgroup must fit a CU
     const long rpw = ((kpad + kw - 1) / kw + P - 1) / P * P;
-    const size_t lds = bs_lds_bytes(kw, (int)rpw);
+    const size_t lds = bs_lds_bytes(kw, (int)rpw, grouped && kw == 1 && bs_direct_allowed());
     if (lds > kLdsPerCu) continue;
     const long wg_per_cu = std::min<long>((4L * kBsWavesPerSimd) / kw, (long)(kLdsPerCu / lds));
     const long slots = 256L * wg_per_cu * kw;  // waves resident at once
@@ -699,7 +779,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
     return hipErrorInvalidValue;
-  BsPlan p = plan_gemm_bs(M, K, ncols, group ? group->n : 1);
+  BsPlan p = plan_gemm_bs(M, K, ncols, group ? group->n : 1, group != nullptr);
   if (!p.ok) return hipErrorInvalidValue;
 #ifdef KODR_TUNE_MODES
   if (const char* env = getenv("KODR_BS_KW")) {  // force the waves per workgroup

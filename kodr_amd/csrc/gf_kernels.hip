@@ -527,6 +527,17 @@ GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
     while (mt > 1 && nxc * ((M + mt - 1) / mt) < 1024) mt /= 2;
     return {mt, 1, 2, 8};
   }
+  // Narrow products (a recoder's coding-vector columns r x C, ncols = k):
+  // 256-byte column chunks (S = 4) with 16 waves splitting K, output rows
+  // split over row tiles until there are >= 128 workgroups.  The wide-row
+  // tiles below would leave one or two workgroups per 8 output rows running
+  // all of K (M = 32, K = 256, 256 columns: ~25 us).
+  if (ncols <= 1024 && K >= 64) {
+    const size_t nx = (ncols + 255) / 256;
+    int mt = 8;
+    while (mt > 1 && nx * ((M + mt - 1) / mt) < 128) mt /= 2;
+    return {mt, 16, 4, 4};
+  }
   if (K > 256 && M > 8 && M <= 16) return {8, 16, 2, 2};
   if (M <= 1) return {1, 16, 2, 0};
   if (M <= 2) return {2, 16, 2, 0};

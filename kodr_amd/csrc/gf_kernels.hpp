@@ -120,6 +120,10 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 // written.
 hipError_t bitslice_rows(const uint8_t* src, uint8_t* dst, size_t ldx, size_t rows, size_t ncols,
                          hipStream_t stream);
+// the same from src (pitch spitch, 16-byte aligned rows; each row readable up
+// to round_up(ncols, 32) bytes) into dst at pitch dpitch (multiple of 32)
+hipError_t bitslice_rows_pitched(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpitch, size_t rows,
+                                 size_t ncols, hipStream_t stream);
 
 // dst rows = the first ncols bytes of src rows, and dst_bs rows = the same
 // rows bit-sliced (as bitslice_rows), from one read of src.  ncols and dpitch
@@ -155,7 +159,9 @@ struct BsPlan {
   bool ok = false;       // false when K is too large for the LDS program
 };
 // groups: independent products of this shape in one launch (grid rows)
-BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups = 1);
+// grouped: the launch is a grouped one (gf_gemm_bs with group), where one
+// wave per workgroup takes the direct variant (no LDS fold)
+BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups = 1, bool grouped = false);
 
 // Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.  group:
 // up to kGemmGroupMax products of this shape in one launch (X = group->x[i],

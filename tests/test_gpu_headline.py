@@ -12,6 +12,7 @@ full/recoder.go:27-46):
 - a prepared recoder at C2 (the bench's recode leg).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -71,6 +72,15 @@ def test_headline_launch_full_compare(gpu_ctx, c2_generation, B):
     assert not ref[0].any() and np.array_equal(ref[1], P[7])
 
 
+# the launch bench.py times (KODR_BS_DIRECT=1: the direct variant, one wave
+# per workgroup running all 256 rows, A/B runs only)
+HEADLINE_PLAN = ({"kernel": 2, "tile_rows": 8, "waves": 1, "lane_groups": 1, "ring": 2, "rows_per_wave": 256,
+                  "generations": 16, "workgroups": 256}
+                 if os.environ.get("KODR_BS_DIRECT") == "1" else
+                 {"kernel": 2, "tile_rows": 8, "waves": 4, "lane_groups": 1, "ring": 2, "rows_per_wave": 64,
+                  "generations": 16, "workgroups": 256})
+
+
 def test_bench_headline_step_exact(gpu_ctx):
     # The bench's timed step itself (bench.HeadlineStep, the object bench.py
     # times): 16 prepared 32 MiB/256 generations x B = 32 coded pieces in one
@@ -88,8 +98,7 @@ def test_bench_headline_step_exact(gpu_ctx):
         got = gpu_ctx.d2h(hs.dOut, 16 * 32 * 131072).reshape(16, 32, 131072)
     finally:
         hs.close()
-    assert plan == {"kernel": 2, "tile_rows": 8, "waves": 4, "lane_groups": 1, "ring": 2, "rows_per_wave": 64,
-                    "generations": 16, "workgroups": 256}, plan
+    assert plan == HEADLINE_PLAN, plan
     for g in range(16):
         P = hs.datas[g].reshape(256, 131072)
         assert np.array_equal(got[g], oracle.encode(P, hs.V[1, g])), g
@@ -321,3 +330,75 @@ def test_grouped_recode_vs_oracle(gpu_ctx, G, k, L, n, count, compact):
     assert (rows[:, :, clen:] == 0xA5).all(), "wrote past the coded piece"
     for g in range(G):
         assert np.array_equal(rows[g, :, :clen], oracle.recode(flats[g], k, R[g])), g
+
+
+def test_recode_c2_device_split_plan(gpu_ctx, c2_generation):
+    # the bench's c2_recode leg at B = 32 through the device API: the piece
+    # columns take the encoder's launch shape (64 column chunks x 4 row
+    # groups, one round of KW = 16 workgroups) and the vector columns a
+    # narrow gf_gemm; every recoded wire row against the oracle's recode
+    P = c2_generation
+    k, L = P.shape
+    rng = np.random.default_rng(0x2EC0)
+    n, clen = k, k + L
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    flat = np.ascontiguousarray(np.concatenate([V, oracle.encode(P, V)], axis=1))
+    lib = _lib.lib()
+    rh = ctypes.c_void_p()
+    errors.check(lib.rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, n, k, ctypes.byref(rh)))
+    errors.check(lib.rlnc_recoder_prepare(rh))
+    R = rng.integers(0, 256, (32, n), dtype=np.uint8)
+    R[0] = 0
+    R[1] = 0
+    R[1, 5] = 1                  # a unit recoding vector returns held piece 5 itself
+    pitch = (clen + 255) // 256 * 256
+    dR, dO = gpu_ctx.alloc(R.nbytes), gpu_ctx.alloc(32 * pitch)
+    try:
+        gpu_ctx.h2d(dR, R)
+        errors.check(lib.rlnc_recoder_coded_pieces_device(rh, dR, 32, dO, pitch))
+        plan = _lib.last_launch_plan()
+        gpu_ctx.synchronize()
+        got = gpu_ctx.d2h(dO, 32 * pitch).reshape(32, pitch)[:, :clen]
+    finally:
+        gpu_ctx.free(dR)
+        gpu_ctx.free(dO)
+        lib.rlnc_recoder_destroy(rh)
+    assert (plan["kernel"], plan["waves"], plan["workgroups"]) == (2, 16, 256), plan
+    assert np.array_equal(got, oracle.recode(flat, k, R))
+    assert np.array_equal(got[1], flat[5]) and not got[0].any()
+
+
+@pytest.mark.parametrize("k,L,n,counts", [(32, 4096 + 48, 40, (1, 3, 12)), (16, 2048, 16, (2, 9)),
+                                          (20, 1024, 24, (1, 10))])
+def test_compact_recoder_vs_oracle(gpu_ctx, k, L, n, counts):
+    # compact recoders: the split layout (k a multiple of 16: piece twin +
+    # a copy of the coding vectors) for every batch size, and the wire-row
+    # twin for k = 20; device and host entry points against the oracle
+    rng = np.random.default_rng(k * 1000 + L + n)
+    lib = _lib.lib()
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    flat = np.ascontiguousarray(np.concatenate([V, oracle.encode(P, V)], axis=1))
+    clen = k + L
+    rh = ctypes.c_void_p()
+    errors.check(lib.rlnc_recoder_create(gpu_ctx.handle, ptr(flat), flat.size, n, k, ctypes.byref(rh)))
+    errors.check(lib.rlnc_recoder_compact(rh))
+    try:
+        for c in counts:
+            R = rng.integers(0, 256, (c, n), dtype=np.uint8)
+            out = np.empty((c, clen), np.uint8)
+            errors.check(lib.rlnc_recoder_coded_pieces(rh, ptr(R), c, ptr(out)))
+            assert np.array_equal(out, oracle.recode(flat, k, R)), c
+            pitch = (clen + 15) // 16 * 16 + 16
+            dR, dO = gpu_ctx.alloc(R.nbytes), gpu_ctx.alloc(c * pitch)
+            try:
+                gpu_ctx.h2d(dR, R)
+                errors.check(lib.rlnc_recoder_coded_pieces_device(rh, dR, c, dO, pitch))
+                gpu_ctx.synchronize()
+                got = gpu_ctx.d2h(dO, c * pitch).reshape(c, pitch)[:, :clen]
+            finally:
+                gpu_ctx.free(dR)
+                gpu_ctx.free(dO)
+            assert np.array_equal(got, out), c
+    finally:
+        lib.rlnc_recoder_destroy(rh)
