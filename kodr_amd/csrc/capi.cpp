@@ -156,6 +156,18 @@ struct rlnc_decoder {
   std::vector<uint8_t*> hdst;    // per materialized row: its destination
   std::vector<int32_t> drow;     // DecoderCore::decoded() scratch
   std::vector<uint8_t> dscale;
+  // Lazy AddPiece: coding vectors accepted while they cannot complete the
+  // rank are queued and eliminated as one batch (DecoderCore::add_many, the
+  // same state as row-by-row adds) when the state is next observed or could
+  // be complete; device pieces are referenced until the next data flush and
+  // then copied by one gather launch.  Every accessor flushes first, so what a
+  // caller can observe is kodr's state after each AddPiece.
+  bool lazy = true;
+  std::vector<uint8_t> pend_v;           // queued coding vectors, k bytes each
+  size_t npend = 0;
+  std::vector<const uint8_t*> pend_src;  // queued device pieces (borrowed), arrival order
+  size_t pend_row0 = 0;                  // received index of pend_src[0]
+  DevBuf ptab;                           // the gather's source-row table
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -1214,8 +1226,10 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
   if (!d) return RLNC_ERR_OUT_OF_MEMORY;
   d->ctx = ctx;
   if (ctx)
-    for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch})
+    for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch, &d->ptab})
       b->bind(ctx->device, ctx->stream);
+  static const bool lazy = !getenv("KODR_DEC_LAZY") || atoi(getenv("KODR_DEC_LAZY")) != 0;  // A/B knob
+  d->lazy = lazy;
   *out = d;
   return RLNC_OK;
 }
@@ -1233,6 +1247,7 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   d->scratch.release();
   d->recv_bs.release();
   d->prog.release();
+  d->ptab.release();
   delete d;
   return RLNC_OK;
 }
@@ -1284,14 +1299,69 @@ int dec_check(rlnc_decoder* d, size_t vlen, const uint8_t* piece, size_t plen) {
 
 int dec_progress(rlnc_decoder* d, long only);
 
+// the queued coding vectors through kodr's elimination as one batch.  They
+// were queued only while useful + queued < k, and each row raises the row
+// count by at most one, so the rank can complete only at the last of them and
+// add_many accepts all (none is refused as "all useful pieces received").
+void dec_flush_coef(rlnc_decoder* d) {
+  if (!d->npend) return;
+  size_t used = 0;
+  (void)d->core.add_many(d->pend_v.data(), d->core.piece_count(), d->npend, &used);
+  d->npend = 0;
+}
+
+// the queued device pieces into their received rows: one gather launch
+constexpr size_t kPendMax = 1024;
+int dec_flush_data(rlnc_decoder* d) {
+  if (d->pend_src.empty()) return RLNC_OK;
+  const size_t m = d->pend_src.size(), r0 = d->pend_row0;
+  TRY(dec_reserve_rows(d, r0 + m, r0));
+  TRY(d->ptab.reserve(m * sizeof(uint8_t*)));
+  HIPC(d->ctx->stage.h2d(d->ptab.p, m * sizeof(uint8_t*), reinterpret_cast<const uint8_t*>(d->pend_src.data()),
+                         m * sizeof(uint8_t*), m * sizeof(uint8_t*), 1, d->ctx->stream));
+  HIPC(kodr_amd::gather_rows(reinterpret_cast<const uint8_t* const*>(d->ptab.p), d->recv.p + r0 * d->pitch, d->pitch,
+                             m, d->L, d->ctx->stream));
+  d->pend_src.clear();
+  return RLNC_OK;
+}
+
+// everything queued: the state and the received rows are kodr's
+int dec_flush(rlnc_decoder* d) {
+  dec_flush_coef(d);
+  if (d->ctx && !d->pend_src.empty()) {
+    TRY(set_dev(d->ctx));
+    TRY(dec_flush_data(d));
+  }
+  return RLNC_OK;
+}
+
 int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
             bool dev) {
   if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  const size_t k = d->core.piece_count();
+  // the queue could complete the rank: observe the state (full/decoder.go:52-54)
+  if (d->npend && d->core.useful() + d->npend >= k) dec_flush_coef(d);
   if (d->core.is_decoded()) return RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;
   if (!vec) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(dec_check(d, vlen, piece, plen));
-  TRY(d->core.add(vec));
+  const size_t row = d->core.received() + d->npend;  // this piece's arrival index
   d->decoded_ready = false;
+  if (d->lazy && d->policy == RLNC_DECODE_LAZY) {
+    d->pend_v.resize((d->npend + 1) * k);
+    memcpy(d->pend_v.data() + d->npend * k, vec, k);
+    d->npend++;
+    if (!d->ctx) return RLNC_OK;
+    if (dev && (uintptr_t)piece % 16 == 0) {  // borrowed until the next data flush
+      if (d->pend_src.empty()) d->pend_row0 = row;
+      d->pend_src.push_back(piece);
+      if (d->pend_src.size() >= kPendMax) TRY(dec_flush_data(d));
+      return RLNC_OK;
+    }
+    TRY(dec_flush_data(d));
+    return dec_store_pieces(d, row, piece, d->L, 1, dev);
+  }
+  TRY(dec_flush(d));
+  TRY(d->core.add(vec));
   TRY(dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev));
   if (d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
   return RLNC_OK;
@@ -1562,6 +1632,7 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
   const bool dev = is_device != 0;
   if (dev && !d->ctx) return RLNC_ERR_NO_DEVICE;
+  TRY(dec_flush(d));
   TRY(dec_check(d, k, rows + k, piece_len));
   const uint8_t* vecs = rows;
   size_t vpitch = pitch;
@@ -1620,6 +1691,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     consumed[g] = 0;
     status[g] = RLNC_OK;
   }
+  for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(ctx));
   // GPU elimination for fresh decoders with >= 2 rows (kElimMaxGens per
@@ -1743,17 +1815,28 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t cou
   return st;
 }
 
-int rlnc_decoder_is_decoded(const rlnc_decoder* d) { return d && d->core.is_decoded(); }
-size_t rlnc_decoder_required(const rlnc_decoder* d) { return d ? d->core.required() : 0; }
-size_t rlnc_decoder_useful(const rlnc_decoder* d) { return d ? d->core.useful() : 0; }
-size_t rlnc_decoder_received(const rlnc_decoder* d) { return d ? d->core.received() : 0; }
+// The accessors observe kodr's state: queued AddPiece calls are eliminated
+// first (a host-only batch; the handle's observable state does not change).
+}  // extern "C"
+namespace {
+const DecoderCore& dec_state(const rlnc_decoder* d) {
+  dec_flush_coef(const_cast<rlnc_decoder*>(d));
+  return d->core;
+}
+}  // namespace
+extern "C" {
+int rlnc_decoder_is_decoded(const rlnc_decoder* d) { return d && dec_state(d).is_decoded(); }
+size_t rlnc_decoder_required(const rlnc_decoder* d) { return d ? dec_state(d).required() : 0; }
+size_t rlnc_decoder_useful(const rlnc_decoder* d) { return d ? dec_state(d).useful() : 0; }
+size_t rlnc_decoder_received(const rlnc_decoder* d) { return d ? d->core.received() + d->npend : 0; }
 size_t rlnc_decoder_piece_length(const rlnc_decoder* d) {
-  return (d && d->core.received() > 0) ? d->L : 0;  // full/decoder.go:18-25
+  return (d && d->core.received() + d->npend > 0) ? d->L : 0;  // full/decoder.go:18-25
 }
 size_t rlnc_decoder_piece_count(const rlnc_decoder* d) { return d ? d->core.piece_count() : 0; }
 
 int rlnc_decoder_get_piece(rlnc_decoder* d, size_t idx, uint8_t* out) {
   if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   TRY(d->core.piece_available(idx));  // decoder_state.go:222-256
   if (!out) return RLNC_ERR_INVALID_ARGUMENT;
   if (!d->ctx) return RLNC_ERR_NO_DEVICE;
@@ -1775,6 +1858,7 @@ int rlnc_decoder_get_piece(rlnc_decoder* d, size_t idx, uint8_t* out) {
 
 int rlnc_decoder_get_pieces(rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;  // full/decoder.go:84-86
   if (!d->ctx) return RLNC_ERR_NO_DEVICE;
   TRY(set_dev(d->ctx));
@@ -1788,6 +1872,7 @@ int rlnc_decoder_get_pieces(rlnc_decoder* d, uint8_t* out) {
 
 int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_pitch) {
   if (!d || !d_out) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   if (!d->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
   if (!d->ctx) return RLNC_ERR_NO_DEVICE;
   if (out_pitch < d->L || out_pitch % 16) return RLNC_ERR_INVALID_ARGUMENT;
@@ -1813,6 +1898,7 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
   rlnc_decoder* d0 = ds[0];
   for (size_t g = 0; g < G; g++)
     if (!ds[g]) return RLNC_ERR_INVALID_ARGUMENT;
+  for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   for (size_t g = 0; g < G; g++)  // full/decoder.go:84-86 for any of them before anything else
     if (!ds[g]->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
   for (size_t g = 0; g < G; g++) {
@@ -1884,18 +1970,19 @@ int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* d) { return d && d->la
 
 int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
-  d->core.copy_coefficients(out);
+  dec_state(d).copy_coefficients(out);
   return RLNC_OK;
 }
 
 int rlnc_decoder_transform(const rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
-  d->core.copy_transform(out, d->core.received());
+  dec_state(d).copy_transform(out, d->core.received());
   return RLNC_OK;
 }
 
 int rlnc_decoder_bind_output(rlnc_decoder* d, uint8_t* d_out, size_t pitch) {
   if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   if (d_out && (!d->ctx || !d->have_len || pitch < d->L || pitch % 16 || (uintptr_t)d_out % 16))
     return RLNC_ERR_INVALID_ARGUMENT;
   d->out_ext = d_out;
@@ -1911,6 +1998,7 @@ int rlnc_decoder_bind_output(rlnc_decoder* d, uint8_t* d_out, size_t pitch) {
 
 int rlnc_decoder_set_policy(rlnc_decoder* d, int policy) {
   if (!d || (policy != RLNC_DECODE_LAZY && policy != RLNC_DECODE_EAGER)) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   d->policy = policy;
   if (policy == RLNC_DECODE_EAGER && d->ctx && d->have_len) {
     TRY(set_dev(d->ctx));
@@ -1923,7 +2011,7 @@ size_t rlnc_decoder_decoded_mask(const rlnc_decoder* d, uint8_t* mask) {
   if (!d) return 0;
   std::vector<int32_t> row;
   std::vector<uint8_t> sc;
-  const size_t n = d->core.decoded(&row, &sc);
+  const size_t n = dec_state(d).decoded(&row, &sc);
   if (mask)
     for (size_t j = 0; j < row.size(); j++) mask[j] = row[j] >= 0 ? 1 : 0;
   return n;
@@ -1931,6 +2019,7 @@ size_t rlnc_decoder_decoded_mask(const rlnc_decoder* d, uint8_t* mask) {
 
 int rlnc_decoder_get_decoded(rlnc_decoder* d, size_t j, uint8_t* out, int is_device) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(dec_flush(d));
   if (j >= d->core.piece_count()) return RLNC_ERR_PIECE_OUT_OF_BOUND;
   std::vector<int32_t> row;
   std::vector<uint8_t> sc;

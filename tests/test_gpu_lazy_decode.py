@@ -1,0 +1,152 @@
+"""GPU parity of lazy AddPiece (capi.cpp dec_add): coding vectors that cannot
+complete the rank are queued and eliminated as one batch when the state is
+next observed, and device pieces are copied by one gather at the next data
+flush.  kodr's AddPiece (full/decoder.go:50-66, decoder_state.go:15-182) is
+the reference: every call's return code, the counters whenever they are read,
+the coefficient state and the decoded bytes equal the oracle's
+(oracle/kodr_oracle.c, the literal restatement), for streams with dependent,
+zero and systematic rows, misaligned and host pieces mixed in, reads in the
+middle of the stream and a generation larger than the gather's queue.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from kodr_amd import _lib, errors
+
+pytestmark = pytest.mark.gpu
+U8P = _lib._u8p
+
+
+def stream(rng, P, n, kind):
+    k, L = P.shape
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    if kind == "quirky":
+        V[0] = 0                       # first piece all-zero: kodr still counts it
+        V[3] = V[2]                    # duplicate: dependent
+        V[5] = 0
+        V[5, 1] = 7                    # scaled unit rows
+        V[6] = 0
+        V[6, 4] = 1
+        V[9] = V[1] ^ V[1]             # zero row
+    elif kind == "systematic":
+        m = min(n, k)
+        V[:m] = 0
+        V[np.arange(m), np.arange(m)] = 1
+        V[2] = 0                       # a lost systematic piece replaced by a coded one
+        V[2] = rng.integers(0, 256, k, dtype=np.uint8)
+    return V, oracle.encode(P, V)
+
+
+def run(ctx, P, V, C, place, reads=(), check_every=False, oracle_cols=None):
+    """Feed (V, C) piece by piece; place(i) -> 'dev', 'dev_misaligned' or 'host'.
+    reads: indices after which useful()/required() and a GetPiece are read.
+    oracle_cols: feed the oracle only that many bytes of each piece (its
+    coefficient side, all that return codes and counters depend on; the
+    decoded bytes are then checked against P alone)."""
+    lib = _lib.lib()
+    k, L = P.shape
+    n = V.shape[0]
+    pitch = (L + 15) // 16 * 16 + 16
+    dbuf = ctx.alloc(n * pitch + 64)
+    host = np.zeros((n, pitch + 1), np.uint8)
+    for i in range(n):
+        host[i, :L] = C[i]
+    stage = np.zeros(n * pitch + 64, np.uint8)
+    for i in range(n):
+        off = i * pitch + (1 if place(i) == "dev_misaligned" else 0)
+        stage[off:off + L] = C[i]
+    ctx.h2d(dbuf, stage)
+    dh = ctypes.c_void_p()
+    errors.check(lib.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
+    od = oracle.Decoder(k)
+    try:
+        for i in range(n):
+            v = np.ascontiguousarray(V[i])
+            pl = place(i)
+            if pl == "host":
+                st = lib.rlnc_decoder_add_piece(dh, v.ctypes.data_as(U8P), k, host[i].ctypes.data_as(U8P), L)
+            else:
+                off = i * pitch + (1 if pl == "dev_misaligned" else 0)
+                st = lib.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(U8P), k, dbuf + off, L)
+            ost = od.add(V[i], C[i] if oracle_cols is None else C[i][:oracle_cols])
+            assert st == ost, (i, st, ost)
+            if check_every or i in reads:
+                assert lib.rlnc_decoder_useful(dh) == od.useful(), i
+                assert lib.rlnc_decoder_required(dh) == od.required(), i
+                assert bool(lib.rlnc_decoder_is_decoded(dh)) == od.is_decoded(), i
+            if i in reads:
+                out = np.empty(L, np.uint8)
+                for idx in (0, 1):
+                    st_g = lib.rlnc_decoder_get_piece(dh, idx, out.ctypes.data_as(U8P))
+                    ost_g, ref = od.get_piece(idx)
+                    assert st_g == ost_g, (i, idx)
+                    if st_g == 0:
+                        assert np.array_equal(out, ref), (i, idx)
+            assert lib.rlnc_decoder_received(dh) == od.received(), i
+        assert lib.rlnc_decoder_useful(dh) == od.useful()
+        coeffs = np.empty((od.useful(), k), np.uint8)
+        errors.check(lib.rlnc_decoder_coefficients(dh, coeffs.ctypes.data_as(U8P)))
+        assert np.array_equal(coeffs, od.coeffs())
+        if od.is_decoded():
+            out = np.empty((k, L), np.uint8)
+            # the caller may reuse its device buffer once GetPieces has returned
+            errors.check(lib.rlnc_decoder_get_pieces(dh, out.ctypes.data_as(U8P)))
+            ctx.h2d(dbuf, np.full(n * pitch + 64, 0x5A, np.uint8))
+            out2 = np.empty((k, L), np.uint8)
+            errors.check(lib.rlnc_decoder_get_pieces(dh, out2.ctypes.data_as(U8P)))
+            assert np.array_equal(out, P) and np.array_equal(out2, P)
+    finally:
+        lib.rlnc_decoder_destroy(dh)
+        ctx.free(dbuf)
+
+
+@pytest.mark.parametrize("kind", ["coded", "quirky", "systematic"])
+@pytest.mark.parametrize("k,L", [(16, 1024), (64, 4096 + 48), (256, 2048)])
+def test_lazy_device_pieces_vs_oracle(gpu_ctx, kind, k, L):
+    rng = np.random.default_rng(k * 7 + L + len(kind))
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 6, kind)
+    run(gpu_ctx, P, V, C, lambda i: "dev")
+
+
+def test_lazy_mixed_placement_and_reads(gpu_ctx):
+    # device, misaligned device (copied at once) and host pieces interleaved;
+    # counters and a partial GetPiece read in the middle (each read flushes)
+    rng = np.random.default_rng(0x1A2)
+    k, L = 48, 3000
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 5, "quirky")
+    kinds = ["dev", "dev", "dev_misaligned", "host", "dev"]
+    run(gpu_ctx, P, V, C, lambda i: kinds[i % 5], reads=(4, 20, 47, 50))
+
+
+def test_lazy_counters_every_call(gpu_ctx):
+    # reading the counters after every AddPiece observes kodr's state each time
+    rng = np.random.default_rng(0x77)
+    k, L = 32, 512
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 3, "quirky")
+    run(gpu_ctx, P, V, C, lambda i: "dev", check_every=True)
+
+
+def test_lazy_queue_past_gather_limit(gpu_ctx):
+    # k = 1100: more queued device pieces than one gather takes (capi.cpp
+    # kPendMax = 1024), short pieces
+    rng = np.random.default_rng(0x44C)
+    k, L = 1100, 64
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 2, "coded")
+    run(gpu_ctx, P, V, C, lambda i: "dev", oracle_cols=1)
+
+
+def test_lazy_c2_piecewise(gpu_ctx):
+    # BASELINE configs[2] fed one AddPiece call per device piece (the bench's
+    # piecewise leg): k + 2 rows, kodr's return codes, the decoded generation
+    rng = np.random.default_rng(0xC2)
+    k, L = 256, 131072
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 2, "coded")
+    run(gpu_ctx, P, V, C, lambda i: "dev", oracle_cols=1)
