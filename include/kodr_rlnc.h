@@ -252,7 +252,20 @@ int rlnc_decoder_destroy(rlnc_decoder* dec);
  * first piece; a different length is RLNC_ERR_INVALID_ARGUMENT). */
 int rlnc_decoder_add_piece(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                            const uint8_t* piece, size_t piece_len);
-/* same, with the piece bytes already on the device (copied D2D, async) */
+/* same, with the piece bytes already on the device.  Under the LAZY policy
+ * (the default) a 16-byte aligned d_piece is BORROWED: the decoder reads it
+ * on the context stream at its next data flush -- the next GetPiece/GetPieces/
+ * get_decoded/bind_output/set_policy/batched AddPiece call, or once 1024
+ * pieces are queued -- so the caller keeps those bytes unchanged until then
+ * (kodr's own decoder keeps the caller's CodedPiece for good,
+ * decoder_state.go:205-208).  Unaligned pieces, and every piece under EAGER,
+ * are copied D2D in the call (async).
+ * Lazy elimination (both entry points): while the queued rows cannot complete
+ * the rank (useful + queued < piece_count) AddPiece only queues the coding
+ * vector; the queue goes through kodr's elimination as one batch when any
+ * accessor (is_decoded, required, useful, coefficients, GetPiece...) or a
+ * later AddPiece needs the state.  Every return code and every value an
+ * accessor returns is exactly kodr's after the same calls. */
 int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                                   const uint8_t* d_piece, size_t piece_len);
 /* batch AddPiece over `count` wire rows (vector ++ piece, as CodedPiece.Flatten,
@@ -350,7 +363,8 @@ int rlnc_decoder_bind_output(rlnc_decoder* dec, uint8_t* d_out, size_t pitch);
  * thread (any entry point above that multiplies), so tests can pin the exact
  * kernel instance a benchmark times.  No kodr counterpart. */
 typedef struct rlnc_launch_plan {
-  int kernel;         /* 1 = gf_gemm_kernel (v_perm tables), 2 = gf_bs_kernel (bit-sliced), 0 = none yet */
+  int kernel;         /* 1 = gf_gemm_kernel (v_perm tables), 2 = gf_bs_kernel (bit-sliced),
+                         3 = gf_gemv_kernel (one coded piece, register tables), 0 = none yet */
   int tile_rows;      /* output rows per workgroup tile (gf_bs_kernel: 8) */
   int waves;          /* waves per workgroup splitting K (KW) */
   int lane_groups;    /* gf_gemm_kernel: input rows per wave-step (S); gf_bs_kernel: 1 */

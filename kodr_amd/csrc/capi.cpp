@@ -94,6 +94,8 @@ struct rlnc_ctx {
   DevBuf elim_tab;           // gf_elim's field tables (once per context)
   bool elim_tab_ok = false;
   DevBuf elim_out;           // gf_elim's per-generation states and counts
+  std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
+  DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
 };
 
 struct rlnc_encoder {
@@ -453,6 +455,8 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->stage.release();
   ctx->elim_tab.release();
   ctx->elim_out.release();
+  ctx->gtmat[0].release();
+  ctx->gtmat[1].release();
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
@@ -1732,7 +1736,9 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   const size_t chunk = std::min<size_t>(gpu.size(), kodr_amd::kElimMaxGens);
   ctx->elim_out.bind(ctx->device, ctx->stream);
   TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
-  std::vector<uint8_t> host(hdr + chunk * ostride);
+  // only what the kernel wrote is read back: no zero-fill, grown once per context
+  if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
+  uint8_t* const hostp = ctx->elim_host.data();
   for (size_t c0 = 0; c0 < gpu.size(); c0 += chunk) {
     const size_t nc = std::min(chunk, gpu.size() - c0);
     kodr_amd::ElimArgs a = {};
@@ -1758,28 +1764,28 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
 #endif
     if (tonly) {
-      HIPC(ctx->stage.d2h(host.data(), hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
-      HIPC(ctx->stage.d2h(host.data() + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
+      HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
+      HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
     } else {
-      HIPC(ctx->stage.d2h(host.data(), hdr + nc * ostride, ctx->elim_out.p, hdr + nc * ostride,
+      HIPC(ctx->stage.d2h(hostp, hdr + nc * ostride, ctx->elim_out.p, hdr + nc * ostride,
                           hdr + nc * ostride, 1, ctx->stream));
     }
 #ifdef KODR_ELIM_TIMING
     if (const char* dump = getenv("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
       if (FILE* fp = fopen(dump, "wb")) {
-        fwrite(host.data(), 1, hdr + nc * ostride, fp);
+        fwrite(hostp, 1, hdr + nc * ostride, fp);
         fclose(fp);
       }
-      for (size_t i = 0; i < nc; i++) memset(host.data() + i * sizeof(int), 0, sizeof(int));
+      for (size_t i = 0; i < nc; i++) memset(hostp + i * sizeof(int), 0, sizeof(int));
     }
 #endif
-    const int* cnt = reinterpret_cast<const int*>(host.data());
+    const int* cnt = reinterpret_cast<const int*>(hostp);
     for (size_t i = 0; i < nc; i++) {
       const size_t g = gpu[c0 + i];
       rlnc_decoder* d = ds[g];
       size_t c = (size_t)std::max(cnt[i], 0);
-      if (c && tonly && !(c == k && d->core.load_inverse(host.data() + hdr + i * k * k, k))) c = 0;
-      if (c && !tonly && !d->core.load_rref(host.data() + hdr + i * ostride, opitch, c)) c = 0;
+      if (c && tonly && !(c == k && d->core.load_inverse(hostp + hdr + i * k * k, k))) c = 0;
+      if (c && !tonly && !d->core.load_rref(hostp + hdr + i * ostride, opitch, c)) c = 0;
       // the rest of the batch (past a row off its diagonal, or past k) through
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;
@@ -1918,7 +1924,12 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
     for (size_t g = 0; g < G; g++) TRY(rlnc_decoder_get_pieces_device(ds[g], d_out + g * ostride, out_pitch));
     return RLNC_OK;
   }
-  TRY(d0->tmat.reserve(G * tsz));
+  // transforms staged per chunk into two context buffers used in turn
+  // (stream-ordered: chunk c's upload follows chunk c - 2's launch)
+  for (DevBuf& b : ctx->gtmat) {
+    b.bind(ctx->device, ctx->stream);
+    TRY(b.reserve(std::min(G, kGroupGetChunk) * tsz));
+  }
   std::vector<uint8_t> hT(kGroupGetChunk * tsz);
   const uint8_t* xs[kGroupGetChunk];
   for (size_t g0 = 0; g0 < G; g0 += kGroupGetChunk) {
@@ -1950,7 +1961,7 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
       d->last_bs = true;
       xs[i] = d->recv_bs.p;
     }
-    uint8_t* dT = d0->tmat.p + g0 * tsz;
+    uint8_t* dT = ctx->gtmat[(g0 / kGroupGetChunk) & 1].p;
     HIPC(ctx->stage.h2d(dT, n * tsz, hT.data(), n * tsz, n * tsz, 1, ctx->stream));
     const kodr_amd::GemmGroupArgs grp{(int)n, xs, tsz, ostride};
     HIPC(kodr_amd::gf_gemm_bs(dT, recv, rows, recv, xs[0], pitch, d_out + g0 * ostride, out_pitch, L, ctx->device,

@@ -35,8 +35,7 @@ class Staging {
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
     if (width * height <= kUploadSmallMax) {  // coefficients, row tables: a kernel reads the pinned chunk
-      const int b = next_;
-      next_ ^= 1;
+      const int b = take();
       if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
       pack(buf_[b], width, src, spitch, width, height);
       if ((e = upload_small(dev_[b], dst, dpitch, width, height, s)) != hipSuccess) return e;
@@ -57,8 +56,7 @@ class Staging {
     const size_t per = kChunk / width;
     for (size_t r0 = 0; r0 < height; r0 += per) {
       const size_t n = std::min(per, height - r0);
-      const int b = next_;
-      next_ ^= 1;
+      const int b = take();
       if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
       pack(buf_[b], width, src + r0 * spitch, spitch, width, n);
       e = hipMemcpy2DAsync(dst + r0 * dpitch, dpitch, buf_[b], width, width, n, hipMemcpyHostToDevice, s);
@@ -72,17 +70,20 @@ class Staging {
   // Split small download: begin enqueues the copy into a pinned chunk and
   // records its event (work enqueued after it does not delay end); end waits
   // for that event and unpacks into dst.  width * height <= kDownloadSmallMax.
+  // The chunk stays reserved between the two: other staging calls in that
+  // window use the other chunk only.  One ticket at a time.
   hipError_t d2h_small_begin(const uint8_t* src, size_t spitch, size_t width, size_t height, hipStream_t s,
                              int* ticket) {
+    if (reserved_[0] || reserved_[1]) return hipErrorInvalidValue;
     hipError_t e = ensure();
     if (e != hipSuccess) return e;
-    const int b = next_;
-    next_ ^= 1;
+    const int b = take();
     if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
     pending_[b] = false;
     if ((e = download_small(src, spitch, dev_[b], width, height, s)) != hipSuccess) return e;
     if ((e = hipEventRecord(ev_[b], s)) != hipSuccess) return e;
     pending_[b] = true;  // any other use of chunk b waits for the download
+    reserved_[b] = true;
     *ticket = b;
     return hipSuccess;
   }
@@ -90,6 +91,7 @@ class Staging {
     hipError_t e = hipEventSynchronize(ev_[b]);
     if (e != hipSuccess) return e;
     pending_[b] = false;
+    reserved_[b] = false;
     pack(dst, dpitch, buf_[b], width, width, height);
     return hipSuccess;
   }
@@ -123,8 +125,13 @@ class Staging {
     int prev_b = -1;
     for (size_t r0 = 0; r0 < height; r0 += per) {
       const size_t n = std::min(per, height - r0);
-      const int b = next_;
-      next_ ^= 1;
+      const int b = take();
+      if (b == prev_b) {  // one chunk free (the other reserved): unpack before reuse
+        if ((e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
+        pending_[b] = false;
+        pack(dst + prev_r0 * dpitch, dpitch, buf_[b], width, width, prev_n);
+        prev_b = -1;
+      }
       if (pending_[b] && (e = hipEventSynchronize(ev_[b])) != hipSuccess) return e;
       e = hipMemcpy2DAsync(buf_[b], width, src + r0 * spitch, spitch, width, n, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) return e;
@@ -139,6 +146,7 @@ class Staging {
       prev_r0 = r0;
       prev_n = n;
     }
+    if (prev_b < 0) return hipSuccess;
     if ((e = hipEventSynchronize(ev_[prev_b])) != hipSuccess) return e;
     pending_[prev_b] = false;
     pack(dst + prev_r0 * dpitch, dpitch, buf_[prev_b], width, width, prev_n);
@@ -167,6 +175,7 @@ class Staging {
       buf_[b] = nullptr;
       dev_[b] = nullptr;
       pending_[b] = false;
+      reserved_[b] = false;
     }
   }
 
@@ -181,6 +190,13 @@ class Staging {
     }
     return hipSuccess;
   }
+  // the next chunk in turn, skipping one reserved by d2h_small_begin
+  int take() {
+    int b = next_;
+    if (reserved_[b]) b ^= 1;
+    next_ = b ^ 1;
+    return b;
+  }
   static void pack(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width, size_t n) {
     if (dpitch == width && spitch == width) {
       memcpy(dst, src, width * n);
@@ -193,6 +209,7 @@ class Staging {
   uint8_t* dev_[2] = {nullptr, nullptr};  // the same chunks as the device sees them
   hipEvent_t ev_[2] = {nullptr, nullptr};
   bool pending_[2] = {false, false};
+  bool reserved_[2] = {false, false};
   int next_ = 0;
 };
 
