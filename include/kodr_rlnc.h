@@ -170,10 +170,11 @@ int rlnc_encoder_seed(rlnc_encoder* enc, uint64_t seed);
 int rlnc_encoder_prepare(rlnc_encoder* enc);
 /* Compact residency (no kodr counterpart): keep only the bit-sliced copy of
  * the generation and release the plain rows -- half the HBM per resident
- * generation.  Every product then runs on the bit-sliced kernel (batches of
- * fewer than 9 pieces are slower than on the plain rows: DESIGN.md),
- * systematic pieces are converted back per call, rlnc_encoder_device_pieces
- * returns NULL and grouped launches take one launch per generation.
+ * generation.  Every product then runs on the bit-sliced kernel (a batch of
+ * fewer than 9 pieces of one generation is slower than on the plain rows:
+ * DESIGN.md), systematic pieces are converted back per call,
+ * rlnc_encoder_device_pieces returns NULL, and grouped launches take compact
+ * generations from 5 pieces per generation (one launch per generation below).
  * Idempotent; synchronizes the ctx stream.  RLNC_ERR_INVALID_ARGUMENT when
  * the bit-sliced path is unavailable for this shape or device. */
 int rlnc_encoder_compact(rlnc_encoder* enc);

@@ -304,68 +304,83 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
 }
 
 // One coded piece per launch (M = 1: full/encoder.go:61-71 called once), the
-// streaming shape.  A workgroup owns one 512-byte column chunk (two lane
-// groups of 32 lanes x 16 B, each reading its own row per step) and all K
-// rows, split over KW waves of RPW rows; every row load of a wave is issued
-// before anything else.  Unlike gf_gemm_kernel there are no LDS tables and no
-// barrier before the first multiply: each lane builds its row's tables from
-// the coefficient in registers (make_tables), so a step waits only for its
-// own row.  Partial sums: lane groups by v_permlane32_swap, waves through one
-// LDS slot each and a single barrier (no atomics, nothing to zero).
-template <int KW, int RPW>
+// streaming shape.  A workgroup owns one column chunk (S lane groups of 64/S
+// lanes x 16 B, each group reading its own row per step: a 1024/S-byte chunk)
+// and all K rows, split over KW waves of RPW rows; the coefficient and then
+// every row load of a wave are issued before anything else.  Unlike
+// gf_gemm_kernel there are no LDS tables and no barrier before the first
+// multiply: each lane builds the tables of all its rows in registers from the
+// coefficients while the rows are in flight, so a step costs only its
+// multiply once its row lands, and the tail after the last row is short.
+// Partial sums: lane groups by v_permlane16/32_swap, waves through one LDS
+// slot each and a single barrier (no atomics, nothing to zero).
+template <int KW, int RPW, int S>
 __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restrict__ A, int K,
                                                           const uint8_t* __restrict__ X, size_t ldx,
                                                           uint8_t* __restrict__ Y, int ncols, int accum) {
-  static_assert(RPW % 2 == 0, "two rows per step");
-  constexpr int STEPS = RPW / 2;
-  __shared__ uint4 part[KW][32];
+  static_assert(RPW % S == 0 && (S == 2 || S == 4), "S rows per step");
+  constexpr int STEPS = RPW / S;
+  constexpr int GL = 64 / S;              // lanes per group
+  constexpr int CB = GL * kLaneBytes;     // chunk bytes
+  __shared__ uint4 part[KW][GL];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 5, li = lane & 31;
-  const int col = blockIdx.x * 512 + li * kLaneBytes;
+  const int g = lane / GL, li = lane % GL;
+  const int col = blockIdx.x * CB + li * kLaneBytes;
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)K * ldx), 0x00020000);
   const int ildx = (int)ldx;
   const int r0 = w * RPW;
   // lane i < RPW holds the coefficient of row r0 + i (0 past K), requested
-  // first: vmcnt retires in issue order, so step 0 waits for it and its row only
+  // first: vmcnt retires in issue order, so the tables wait for it alone
   const uint32_t cv = (lane < RPW && r0 + lane < K) ? (uint32_t)A[r0 + lane] : 0u;
   __builtin_amdgcn_sched_barrier(0);
   u32x4 ring[STEPS];
 #pragma unroll
-  for (int j = 0; j < STEPS; j++) ring[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (r0 + 2 * j + g) * ildx + col, 0, 0);
+  for (int j = 0; j < STEPS; j++)
+    ring[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (r0 + S * j + g) * ildx + col, 0, 0);
   __builtin_amdgcn_sched_barrier(0);
+  uint4 t01[STEPS];
+  uint32_t t2[STEPS];
+#pragma unroll
+  for (int j = 0; j < STEPS; j++) {
+    uint32_t c = __builtin_amdgcn_readlane(cv, S * j);
+#pragma unroll
+    for (int q = 1; q < S; q++) c = g == q ? __builtin_amdgcn_readlane(cv, S * j + q) : c;
+    make_tables(c, t01[j], t2[j]);
+  }
   uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int j = 0; j < STEPS; j++) {
-    const uint32_t c0 = __builtin_amdgcn_readlane(cv, 2 * j), c1 = __builtin_amdgcn_readlane(cv, 2 * j + 1);
-    uint4 t01;
-    uint32_t t2;
-    make_tables(g ? c1 : c0, t01, t2);
     const u32x4 x = ring[j];
 #pragma unroll
     for (int d = 0; d < 4; d++) {
       const uint32_t s0 = x[d] & 0x07070707u, s1 = (x[d] >> 3) & 0x07070707u, s2 = (x[d] >> 6) & 0x03030303u;
-      const uint32_t a0 = __builtin_amdgcn_perm(t01.y, t01.x, s0);
-      const uint32_t a1 = __builtin_amdgcn_perm(t01.w, t01.z, s1);
-      const uint32_t a2 = __builtin_amdgcn_perm(t2, t2, s2);
+      const uint32_t a0 = __builtin_amdgcn_perm(t01[j].y, t01[j].x, s0);
+      const uint32_t a1 = __builtin_amdgcn_perm(t01[j].w, t01[j].z, s1);
+      const uint32_t a2 = __builtin_amdgcn_perm(t2[j], t2[j], s2);
       acc[d] = __builtin_amdgcn_bitop3_b32(acc[d], a0, a1, 0x96) ^ a2;
     }
   }
 #pragma unroll
   for (int d = 0; d < 4; d++) {
-    const auto r = __builtin_amdgcn_permlane32_swap(acc[d], acc[d], false, false);  // lane ^ 32
+    uint32_t v = acc[d];
+    if (S == 4) {
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // lane ^ 16
+      v = r[0] ^ r[1];
+    }
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);    // lane ^ 32
     acc[d] = r[0] ^ r[1];
   }
   if (g == 0) part[w][li] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
   __syncthreads();
-  if (tid >= 32) return;
+  if (tid >= GL) return;
   uint4 v = part[0][tid];
 #pragma unroll
   for (int q = 1; q < KW; q++) {
     const uint4 p = part[q][tid];
     v = make_uint4(v.x ^ p.x, v.y ^ p.y, v.z ^ p.z, v.w ^ p.w);
   }
-  const int cc = blockIdx.x * 512 + tid * kLaneBytes;
+  const int cc = blockIdx.x * CB + tid * kLaneBytes;
   if (cc >= ncols) return;
   uint8_t* dst = Y + cc;
   if (cc + kLaneBytes <= ncols) {
@@ -650,9 +665,10 @@ static bool env_config(GemmConfig* g) {
   return sscanf(s, "%d,%d,%d,%d", &g->mt, &g->kw, &g->s, &g->p) >= 3;
 }
 
-// KODR_GEMV=0/1: one-row products on gf_gemv_kernel (A/B measurements)
-static bool gemv_enabled() {
-  static const bool v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) != 0 : false;
+// KODR_GEMV=0/2/4: one-row products on gf_gemm_kernel / gf_gemv_kernel with
+// 2 or 4 lane groups (A/B measurements)
+static int gemv_enabled() {
+  static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 0;
   return v;
 }
 
@@ -664,12 +680,17 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   // one coded piece of a generation of up to 256 rows, wide rows: the
   // streaming kernel (row offsets of all 256 lanes' rows fit 31 bits)
   constexpr int kGemvKW = 16, kGemvRPW = 16;
+  const int gemv = gemv_enabled();
   if (M == 1 && !grp && !force && K >= 1 && K <= (size_t)kGemvKW * kGemvRPW && ncols >= 16384 &&
-      (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv_enabled()) {
-    const int nx = (int)((ncols + 511) / 512);
-    hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K, dX,
-                       ldx, dY, (int)ncols, acc);
-    last_launch_plan() = LaunchPlan{3, 1, kGemvKW, 2, kGemvRPW / 2, kGemvRPW, 1, nx};
+      (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv) {
+    const int S = gemv == 4 ? 4 : 2, nx = (int)((ncols + 1024 / S - 1) / (1024 / S));
+    if (S == 4)
+      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 4>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
+                         dX, ldx, dY, (int)ncols, acc);
+    else
+      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
+                         dX, ldx, dY, (int)ncols, acc);
+    last_launch_plan() = LaunchPlan{3, 1, kGemvKW, S, kGemvRPW / S, kGemvRPW, 1, nx};
     return hipGetLastError();
   }
   GemmConfig g = force ? *force : grp ? choose_group_config(M, K, ncols, (size_t)grp->n)
