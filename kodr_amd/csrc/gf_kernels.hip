@@ -665,10 +665,13 @@ static bool env_config(GemmConfig* g) {
   return sscanf(s, "%d,%d,%d,%d", &g->mt, &g->kw, &g->s, &g->p) >= 3;
 }
 
-// KODR_GEMV=0/2/4: one-row products on gf_gemm_kernel / gf_gemv_kernel with
-// 2 or 4 lane groups (A/B measurements)
+// One-row products of 129..256 input rows take gf_gemv_kernel with two lane
+// groups: 8.5 us per 32 MiB/256 coded piece in rocprof against 9.4 on
+// gf_gemm_kernel<1, 16, 2> (profiles/r03/b1/); four lane groups (256-byte
+// chunks, two workgroups per CU) measured 9.4.  KODR_GEMV=0/2/4 selects
+// gf_gemm_kernel / 2 / 4 lane groups (A/B measurements).
 static int gemv_enabled() {
-  static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 0;
+  static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 2;
   return v;
 }
 
@@ -681,7 +684,8 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   // streaming kernel (row offsets of all 256 lanes' rows fit 31 bits)
   constexpr int kGemvKW = 16, kGemvRPW = 16;
   const int gemv = gemv_enabled();
-  if (M == 1 && !grp && !force && K >= 1 && K <= (size_t)kGemvKW * kGemvRPW && ncols >= 16384 &&
+  if (M == 1 && !grp && !force && K > (size_t)kGemvKW * kGemvRPW / 2 && K <= (size_t)kGemvKW * kGemvRPW &&
+      ncols >= 16384 &&
       (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv) {
     const int S = gemv == 4 ? 4 : 2, nx = (int)((ncols + 1024 / S - 1) / (1024 / S));
     if (S == 4)
