@@ -730,10 +730,11 @@ size_t bs_lds_bytes(int kw, int rpw, bool direct = false) {
   return (direct ? 256 : 64 * 64 + 256) * 4 + (size_t)kw * rpw * kBsRows * 4 + 16;  // + the dynamic rows' counter
 }
 
-// KODR_BS_DIRECT=0/1: whether grouped launches may plan the direct variant
-// (A/B measurements)
+// Grouped launches may plan the direct variant (one wave per workgroup, no
+// fold): equal at B = 32-64, 2.4 % faster at B = 256 (profiles/r03/direct_ab/).
+// KODR_BS_DIRECT=0 keeps the folded plans (A/B measurements).
 bool bs_direct_allowed() {
-  static const bool v = getenv("KODR_BS_DIRECT") ? atoi(getenv("KODR_BS_DIRECT")) != 0 : false;
+  static const bool v = getenv("KODR_BS_DIRECT") ? atoi(getenv("KODR_BS_DIRECT")) != 0 : true;
   return v;
 }
 

@@ -72,12 +72,12 @@ def test_headline_launch_full_compare(gpu_ctx, c2_generation, B):
     assert not ref[0].any() and np.array_equal(ref[1], P[7])
 
 
-# the launch bench.py times (KODR_BS_DIRECT=1: the direct variant, one wave
-# per workgroup running all 256 rows, A/B runs only)
-HEADLINE_PLAN = ({"kernel": 2, "tile_rows": 8, "waves": 1, "lane_groups": 1, "ring": 2, "rows_per_wave": 256,
+# the launch bench.py times: the direct variant, one wave per workgroup
+# running all 256 rows (KODR_BS_DIRECT=0, A/B runs only: the folded KW = 4 plan)
+HEADLINE_PLAN = ({"kernel": 2, "tile_rows": 8, "waves": 4, "lane_groups": 1, "ring": 2, "rows_per_wave": 64,
                   "generations": 16, "workgroups": 256}
-                 if os.environ.get("KODR_BS_DIRECT") == "1" else
-                 {"kernel": 2, "tile_rows": 8, "waves": 4, "lane_groups": 1, "ring": 2, "rows_per_wave": 64,
+                 if os.environ.get("KODR_BS_DIRECT") == "0" else
+                 {"kernel": 2, "tile_rows": 8, "waves": 1, "lane_groups": 1, "ring": 2, "rows_per_wave": 256,
                   "generations": 16, "workgroups": 256})
 
 
@@ -85,9 +85,10 @@ def test_bench_headline_step_exact(gpu_ctx):
     # The bench's timed step itself (bench.HeadlineStep, the object bench.py
     # times): 16 prepared 32 MiB/256 generations x B = 32 coded pieces in one
     # grouped call.  The launch must be the instance the bench reports
-    # (gf_bs_kernel, KW = 4 waves per workgroup, the two-row ring, 64 rows per
-    # wave, 16 generations), and every one of the 512 pieces must equal the
-    # oracle's encode (full/encoder.go:61-71).
+    # (HEADLINE_PLAN: gf_bs_kernel, the direct variant with one wave per
+    # workgroup, the two-row ring, 256 rows per wave, 16 generations), and
+    # every one of the 512 pieces must equal the oracle's encode
+    # (full/encoder.go:61-71).
     import bench
     hs = bench.HeadlineStep(gpu_ctx, _lib.lib(), errors, 256, 131072, 32, 16, grouped=True,
                             rng=np.random.default_rng(0xBE7C), nvec=2, keep_data=True)
