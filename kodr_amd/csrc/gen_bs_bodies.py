@@ -57,19 +57,61 @@ def set_ring(p):
     global P, PG, PGN, VMAX
     P, PG = p, RING + 8 * p
     PGN, VMAX = PG + 1, PG + 2
-NCOPY = 4
+# body copies: rows are taken C = NCOPY at a time (copy r for row m = r + C g,
+# M0 index 8 C g), with a stub between groups.  4 (one stub per row) is the
+# shipped build; 3 (2 stubs, 52 KB) and 2 (3 stubs, 35 KB) trade a stub per
+# group for a smaller instruction footprint (A/B builds, KODR_BS_NCOPY)
+NCOPY = int(os.environ.get("KODR_BS_NCOPY", "4"))
+assert NCOPY in (2, 3, 4)
 # body start alignment in bytes (0: packed back to back); the instruction
 # fetch after each s_setpc starts at the body's first byte
 ALIGN = int(os.environ.get("KODR_BS_ALIGN", "0"))
-# SGPRs: T[0..4] = s[60:69] (T[0] entry, T[r+1] the tail of copy r), the
-# second half's targets s[70:77], the stub s[78:79], this row's return
-# address s[80:81], the 8 rows' return addresses s[82:97]
+# SGPRs (NCOPY = 4): T[0..4] = s[60:69] (T[0] entry, T[r+1] the tail of copy
+# r), the second half's targets s[70:77], the stub s[78:79], this row's
+# return address s[80:81], the 8 rows' return addresses s[82:97].  With
+# fewer copies T[0..C] is shorter, the rows after the first group follow it
+# (still ending at s77), the ceil(8/C)-1 stubs start at s78 and the row
+# computes its return address itself (no RET table: SGPRs run out)
 T0 = 60
 H2 = 70
 STUB = 78
 RT = 80
 RET = 82
 CNT = 98
+
+
+def set_ncopy(c):
+    """Switch the module's copy count and the SGPR map that depends on it."""
+    global NCOPY, H2, RT, RET, CNT
+    NCOPY = c
+    H2 = T0 + 2 * (c + 1)
+    assert H2 + 2 * (8 - c) == STUB
+    nst = n_stubs()
+    RT = STUB + 2 * nst
+    RET = RT + 2 if c == 4 else None
+    CNT = RET + 16 if c == 4 else RT + 2
+
+
+def n_stubs():
+    return (8 + NCOPY - 1) // NCOPY - 1
+
+
+def stub_reg(g):
+    """Address register of the stub before row group g (1..)."""
+    return STUB + 2 * (g - 1)
+
+
+def row_target(m):
+    """SGPR pair holding row m's target at dispatch: T[m] in the first group,
+    the H2 block after it."""
+    return T0 + 2 * m if m < NCOPY else H2 + 2 * (m - NCOPY)
+
+
+def stub_label(g, label="stub"):
+    return f"{label}_g{g}" if g > 1 else label
+
+
+set_ncopy(NCOPY)
 GPC = 56           # s_getpc scratch s[56:57]
 SP = 46            # scalar-load variant: program pointer s[46:47]
 SL = 48            # scalar-load variant: the next row's 8 targets s[48:55]
@@ -189,13 +231,12 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
     t = [f"s_setprio {prio(j)}"] if prio else []
     if sload:  # targets staged by the previous row's scalar load; fetch the next row's
         t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(0)"]
-        t += [f"s_mov_b32 s{h(m)}, s{SL + m}" for m in range(4)]
-        t += [f"s_mov_b32 s{H2 + 2 * m}, s{SL + 4 + m}" for m in range(4)]
+        t += [f"s_mov_b32 s{row_target(m)}, s{SL + m}" for m in range(8)]
         t += [f"s_load_dwordx8 s[{SL}:{SL + 7}], s[{SP}:{SP + 1}], 0x0",
               f"s_add_u32 s{SP}, s{SP}, 32", f"s_addc_u32 s{SP + 1}, s{SP + 1}, 0"]
     else:
         t += [f"s_waitcnt vmcnt({2 * (P - 1)}) lgkmcnt(1)"]
-        t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
+        t += [f"v_readlane_b32 s{h(m)}, v{PG}, {8 * j + m}" for m in range(NCOPY)] * (2 if "readlane" in twice else 1)
     t += table_lines(slot) * (2 if "table" in twice else 1)
     b = RING + 8 * slot
     # the row P ahead into this slot (rows past the wave's range read zero)
@@ -204,15 +245,23 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
               f"buffer_load_dwordx4 v[{b + 4}:{b + 7}], %[col], s[40:43], s44 offen offset:16",
               "s_add_u32 s44, s44, s45"]
     if not sload:
-        t += [f"v_readlane_b32 s{H2 + 2 * m}, v{PG}, {8 * j + 4 + m}" for m in range(4)] * (2 if "readlane" in twice else 1)
+        t += [f"v_readlane_b32 s{row_target(m)}, v{PG}, {8 * j + m}"
+              for m in range(NCOPY, 8)] * (2 if "readlane" in twice else 1)
     if dispatch:
+        C = NCOPY
         if half_prio:  # this row's own stub, which sets the second half's priority
+            assert C == 4
             t += [f"s_add_u32 s{h(4)}, s{GPC}, .Lstub{j}_%= - .Lpc_%=",
                   f"s_addc_u32 s{h(4) + 1}, s{GPC + 1}, 0"]
         else:
-            t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{STUB}:{STUB + 1}]"]
-        t += [f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]",
-              "s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
+            t += [f"s_mov_b64 s[{h(C)}:{h(C) + 1}], s[{STUB}:{STUB + 1}]"]
+        if 8 % C:  # the last stub put the return address into T[8 % C]: its hi word back
+            t += [f"s_mov_b32 s{h(8 % C) + 1}, %[thi]"]
+        if RET is not None:
+            t += [f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]"]
+        else:
+            t += [f"s_add_u32 s{RT}, s{GPC}, .Lret{j}_%= - .Lpc_%=", f"s_addc_u32 s{RT + 1}, s{GPC + 1}, 0"]
+        t += ["s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
               f"s_setpc_b64 s[{h(0)}:{h(0) + 1}]",
               f".Lret{j}_%=:",
               "s_set_gpr_idx_off"]
@@ -220,13 +269,22 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
 
 
 def stub_lines(label="stub", prio=None):
-    """Between the two halves of a row: rows 4..7 reuse copies 0..3 at M0
-    index 32, with targets T[1..3] from the second half's registers and T[4]
-    the row's return address."""
+    """Between row groups: group g (rows C g .. C g + n - 1) reuses copies
+    0..n-1 at M0 index 8 C g, with targets T[1..n-1] from the later rows'
+    registers and T[n] the next stub, or the row's return address after the
+    last group (NCOPY = 4: one stub, rows 4..7 at index 32)."""
     h = lambda i: T0 + 2 * i  # noqa: E731
-    t = [f".L{label}_%=:"] + ([f"s_setprio {prio}"] if prio is not None else []) + ["s_add_u32 m0, m0, 32"]
-    t += [f"s_mov_b64 s[{h(m)}:{h(m) + 1}], s[{H2 + 2 * m}:{H2 + 2 * m + 1}]" for m in (1, 2, 3)]
-    t += [f"s_mov_b64 s[{h(4)}:{h(4) + 1}], s[{RT}:{RT + 1}]", f"s_setpc_b64 s[{H2}:{H2 + 1}]"]
+    C, ng = NCOPY, n_stubs() + 1
+    t = []
+    for g in range(1, ng):
+        n = min(C, 8 - C * g)
+        t += [f".L{stub_label(g, label)}_%=:"] + ([f"s_setprio {prio}"] if prio is not None else [])
+        t += [f"s_add_u32 m0, m0, {8 * C}"]
+        t += [f"s_mov_b64 s[{h(i)}:{h(i) + 1}], s[{row_target(C * g + i)}:{row_target(C * g + i) + 1}]"
+              for i in range(1, n)]
+        nxt = stub_reg(g + 1) if g + 1 < ng else RT
+        t += [f"s_mov_b64 s[{h(n)}:{h(n) + 1}], s[{nxt}:{nxt + 1}]",
+              f"s_setpc_b64 s[{row_target(C * g)}:{row_target(C * g) + 1}]"]
     return t
 
 
@@ -239,11 +297,13 @@ def prologue_lines(dispatch=True, sload=False):
            "s_mov_b32 s43, 0x00020000", "s_mov_b32 s44, %[roff]", "s_mov_b32 s45, %[ldx]",
            f"s_getpc_b64 s[{GPC}:{GPC + 1}]", ".Lpc_%=:"]
     if dispatch:
-        for reg, lab in [(STUB, "stub")] + [(RET + 2 * j, f"ret{j}") for j in range(8)]:
+        regs = [(stub_reg(g), stub_label(g)) for g in range(1, n_stubs() + 1)]
+        if RET is not None:
+            regs += [(RET + 2 * j, f"ret{j}") for j in range(8)]
+        for reg, lab in regs:
             pro += [f"s_add_u32 s{reg}, s{GPC}, .L{lab}_%= - .Lpc_%=",
                     f"s_addc_u32 s{reg + 1}, s{GPC + 1}, 0"]
-    pro += [f"s_mov_b32 s{T0 + 2 * i + 1}, %[thi]" for i in range(4)]
-    pro += [f"s_mov_b32 s{H2 + 2 * i + 1}, %[thi]" for i in range(4)]
+    pro += [f"s_mov_b32 s{row_target(m) + 1}, %[thi]" for m in range(8)]
     if sload:  # the wave's program in global memory, one 32-byte row of targets at a time
         pro += [f"s_mov_b32 s{SP}, %[pglo]", f"s_mov_b32 s{SP + 1}, %[pghi]",
                 f"s_load_dwordx8 s[{SL}:{SL + 7}], s[{SP}:{SP + 1}], 0x0",
@@ -371,7 +431,8 @@ def dump_lines():
         t += [f"v_mov_b32 v{ACC}, {src}",
               f"global_store_dword v{ACC + 1}, v{ACC}, %[ydbg] offset:{4 * i}"]
     t += ["s_waitcnt vmcnt(0)"]
-    t += [".Lstub_%=:"] + [f".Lret{j}_%=:" for j in range(8)]   # never jumped to
+    t += [f".L{stub_label(g)}_%=:" for g in range(1, n_stubs() + 1)]   # never jumped to
+    t += [f".Lret{j}_%=:" for j in range(8)]
     return t
 
 
@@ -439,7 +500,7 @@ def main():
     out += emit("KODR_BS_MAIN_NDNL", main_loop(False, False))
     # tuning: the loop without the priority rotation (MODE 10)
     out += emit("KODR_BS_MAIN_NOPRIO", main_loop(True, True, None))
-    out += emit("KODR_BS_MAIN_HALF", main_loop(True, True, ROW_PRIO, lambda j: (j + 2) % 4))
+    out += emit("KODR_BS_MAIN_HALF", main_loop(True, True, ROW_PRIO, lambda j: (j + 2) % 4) if NCOPY == 4 else [])
     # cost probes: the row's target reads or its tables issued twice (same result)
     out += emit("KODR_BS_MAIN_2RL", main_loop(True, True, ROW_PRIO, None, ("readlane",)))
     out += emit("KODR_BS_MAIN_2TB", main_loop(True, True, ROW_PRIO, None, ("table",)))
@@ -449,7 +510,7 @@ def main():
     # dynamic rows (MODE 20)
     # (a one-row ring only; other ring depths build it empty, and only a
     # tuning build instantiates MODE 20)
-    out += emit("KODR_BS_MAIN_DYN", main_loop_dyn(True) if P == 1 else [])
+    out += emit("KODR_BS_MAIN_DYN", main_loop_dyn(True) if P == 1 and NCOPY == 4 else [])
     out.append(f"#define KODR_BS_DYN_VMAX {D_VMAX}")
     red = [f"ds_xor_b32 %[lds], v{ACC + r} offset:{256 * r}" for r in range(64)]
     out += emit("KODR_BS_REDUCE", red)
@@ -460,7 +521,7 @@ def main():
     out.append("#define KODR_BS_CLOBBERS " + ", ".join(clob) + ', "scc", "memory"')
     dclob = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, D_VMAX))]
     dclob += [f'"s{r}"' for r in list(range(40, 46)) + list(range(D_EX, D_TMP + 1)) + [GPC, GPC + 1] +
-              list(range(T0, RET + 2 * D_ROWS))]
+              list(range(T0, (RET or RT) + 2 * D_ROWS))]
     out.append("#define KODR_BS_CLOBBERS_DYN " + ", ".join(dclob) + ', "scc", "memory"')
     out.append("#define KODR_BS_CLOBBERS_SLOAD " + ", ".join(clob + [f'"s{r}"' for r in range(SP, SL + 8)]) +
                ', "scc", "memory"')

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const int e = e0 + tid + j * 64 * KW;
-        if (e < ne) prog_l[e] = tgt_l[c[j]] + (uint32_t)(e & 3) * KODR_BS_COPY_BYTES;
+        if (e < ne) prog_l[e] = tgt_l[c[j]] + (uint32_t)((e & 7) % KODR_BS_NCOPY) * KODR_BS_COPY_BYTES;
       }
     }
     __syncthreads();
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     for (int i = tid; i < 64 * 64; i += 64 * KW) red[i] = 0u;
   __syncthreads();
   // program: entry e = the target of (output row m0 + e%8, input row kb + e/8):
-  // body c in copy (e%8) & 3
+  // body c in copy (e%8) % KODR_BS_NCOPY
   uint32_t* wp = prog_l + w * rpw * kBsRows;
   for (int e0 = 0; e0 < ne; e0 += 64 * 8) {
     if (e0) {
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       const int e = e0 + j * 64 + lane;
-      if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)(e & 3) * KODR_BS_COPY_BYTES;
+      if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)((e & 7) % KODR_BS_NCOPY) * KODR_BS_COPY_BYTES;
     }
   }
 #ifdef KODR_TUNE_MODES

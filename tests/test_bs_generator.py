@@ -137,13 +137,13 @@ class _Wave:
             self.addr[0x1000_0000 + 4 * i] = i
         self.s, self.v = {}, {}
         self.m0, self.idx_on = 0, False
-        # LDS program: per row 8 absolute lo targets, body c in copy m & 3
+        # LDS program: per row 8 absolute lo targets, body c in copy m % NCOPY
         self.lds = {}
         pl = 0x400
         for k in range(nr):
             for m in range(8):
                 c = int(A[m, k])
-                self.lds[pl + 4 * (8 * k + m)] = (self.BASE + offs[(m & 3) * 256 + c]) & 0xFFFFFFFF
+                self.lds[pl + 4 * (8 * k + m)] = (self.BASE + offs[(m % gen.NCOPY) * 256 + c]) & 0xFFFFFFFF
         # the same program in global memory for the scalar-load variant (plus
         # one row of look-ahead past the end, as the kernel's scratch has)
         self.gmem = {0x2000_0000 + a - pl: v for a, v in self.lds.items()}
@@ -398,4 +398,38 @@ def test_two_row_ring_end_to_end_vs_oracle():
                     exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
                 assert np.array_equal(got, exp), (nr, m)
     finally:
+        gen.set_ring(p0)
+
+
+@pytest.mark.parametrize("ncopy", [2, 3])
+@pytest.mark.parametrize("ring", [1, 2])
+def test_fewer_copies_end_to_end_vs_oracle(ncopy, ring):
+    # the A/B builds with fewer body copies (KODR_BS_NCOPY): row groups of
+    # ncopy rows joined by ceil(8/ncopy)-1 stubs, return address computed per
+    # row; SGPRs stay below the kernel's budget
+    c0, p0 = gen.NCOPY, gen.P
+    gen.set_ncopy(ncopy)
+    gen.set_ring(ring)
+    try:
+        assert gen.CNT <= 101 and gen.RET is None
+        offs, total = gen.body_offsets()
+        assert total == 16384 * ncopy
+
+        class _WaveC(_Wave):
+            VEC = (gen.PG, gen.PGN, gen.PL)
+
+        rng = np.random.default_rng(20 + ncopy)
+        for nr in (8, 24):
+            X = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
+            A = rng.integers(0, 256, (8, nr), dtype=np.uint8)
+            A[2, 0], A[7, 1] = 0, 1
+            acc = _WaveC(X, A, nr, gen.main_loop(True)).run()
+            for m in range(8):
+                got = bitslice_np(acc[m].view(np.uint8).copy())
+                exp = np.zeros(32, np.uint8)
+                for k in range(nr):
+                    exp ^= np.array([oracle.gf_mul(int(A[m, k]), int(b)) for b in X[k]], np.uint8)
+                assert np.array_equal(got, exp), (ncopy, nr, m)
+    finally:
+        gen.set_ncopy(c0)
         gen.set_ring(p0)
