@@ -250,9 +250,10 @@ int gemm(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const
   });
 }
 
-// Y = A (x) X over a bit-sliced X (kodr_amd::bitslice_rows), plain Y
+// Y = A (x) X over a bit-sliced X (kodr_amd::bitslice_rows), plain Y; side:
+// the same launch also writes side->y = A (x) side->x (one K chunk only)
 int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
-            size_t ldx, uint8_t* dY, size_t ldy, size_t ncols) {
+            size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, const kodr_amd::BsSide* side = nullptr) {
   if ((ldx % 32) || (ldy % 16) || ldx < ncols || ldy < ncols) {
     g_last_error = "gf_gemm_bs: unsupported layout (pitch a multiple of 32)";
     return RLNC_ERR_INVALID_ARGUMENT;
@@ -263,9 +264,13 @@ int gemm_bs(rlnc_ctx* ctx, const uint8_t* dA, size_t lda, size_t M, size_t K, co
     g_last_error = "gf_gemm_bs: no launch plan for this shape";
     return RLNC_ERR_INVALID_ARGUMENT;
   }
+  if (side && kc < K) {
+    g_last_error = "gf_gemm_bs: a side product needs one K chunk";
+    return RLNC_ERR_INVALID_ARGUMENT;
+  }
   return gemm_k_chunked(K, kc, [&](size_t k0, size_t kn, bool acc) {
     HIPC(kodr_amd::gf_gemm_bs(dA + k0, lda, M, kn, dX + k0 * ldx, ldx, dY, ldy, ncols, ctx->device, ctx->stream,
-                              acc));
+                              acc, nullptr, side));
     return (int)RLNC_OK;
   });
 }
@@ -972,6 +977,11 @@ int rec_build_piece_twin(rlnc_recoder* r) {
   return RLNC_OK;
 }
 
+bool rec_side_enabled() {
+  static const bool v = getenv("KODR_REC_SIDE") ? atoi(getenv("KODR_REC_SIDE")) != 0 : true;
+  return v;
+}
+
 // this product takes the split layout
 bool rec_uses_split(const rlnc_recoder* r, size_t count) {
   return rec_split(r) && (r->compact || resident_uses_bs(r->ctx, count, r->n, r->ppitch, r->L));
@@ -982,20 +992,27 @@ bool rec_uses_split(const rlnc_recoder* r, size_t count) {
 int rec_product(rlnc_recoder* r, const uint8_t* dR, size_t count, uint8_t* dY, size_t ldy) {
   rlnc_ctx* ctx = r->ctx;
   const size_t n = r->n, k = r->k, L = r->L;
+  if (ldy % 16 || (uintptr_t)dY % 16) {  // any pitch: 16-byte aligned rows aside, then one strided copy
+    const size_t sp = round_up(r->clen, 16);
+    TRY(r->scratch.reserve(count * sp));
+    TRY(rec_product(r, dR, count, r->scratch.p, sp));
+    HIPC(hipMemcpy2DAsync(dY, ldy, r->scratch.p, sp, r->clen, count, hipMemcpyDeviceToDevice, ctx->stream));
+    return RLNC_OK;
+  }
   if (!rec_uses_split(r, count))  // one product over the wire rows
     return gemm_resident(ctx, dR, n, count, n, r->compact ? nullptr : r->flat.p, r->flat_bs, r->bs_valid, r->pitch,
                          dY, ldy, r->clen);
   size_t ldv = 0;
   const uint8_t* C = rec_vectors(r, &ldv);
-  TRY(gemm(ctx, dR, n, count, n, C, ldv, dY, ldy, k));
   if (!r->compact) TRY(rec_build_piece_twin(r));
   uint8_t* yp = dY + k;
-  if ((uintptr_t)yp % 16 == 0 && ldy % 16 == 0) return gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, yp, ldy, L);
-  // piece columns not 16-byte aligned: compute aside, then one strided copy
-  TRY(r->scratch.reserve(count * r->ppitch));
-  TRY(gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, r->scratch.p, r->ppitch, L));
-  HIPC(hipMemcpy2DAsync(yp, ldy, r->scratch.p, r->ppitch, L, count, hipMemcpyDeviceToDevice, ctx->stream));
-  return RLNC_OK;
+  // the vector columns as the bit-sliced launch's side product (one launch;
+  // KODR_REC_SIDE=0: a gf_gemm launch of their own, for A/B)
+  const kodr_amd::BsSide sd{C, ldv, dY, ldy, k};
+  if (rec_side_enabled() && kodr_amd::side_ok(sd, n) && bs_chunk_rows(count, n, r->ppitch, L) >= n)
+    return gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, yp, ldy, L, &sd);
+  TRY(gemm(ctx, dR, n, count, n, C, ldv, dY, ldy, k));
+  return gemm_bs(ctx, dR, n, count, n, r->piece_bs.p, r->ppitch, yp, ldy, L);  // k % 16 == 0: yp aligned
 }
 
 int recoder_alloc(rlnc_ctx* ctx, size_t n, size_t clen, size_t k, rlnc_recoder** out) {

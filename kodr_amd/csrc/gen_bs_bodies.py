@@ -16,14 +16,17 @@ output rows).  Then every output plane needs one instruction:
 so a coefficient's body is at most 8 VALU instructions, one per non-empty S_j.
 
 Threaded dispatch.  A wave applies 8 coefficients per input row (output rows
-m = 0..7).  The bodies exist in 4 copies; copy r XORs into accumulator set r
-and ends with s_setpc_b64 to T[r+1] (T[4] for r = 3), so body m jumps straight
-to body m+1: one taken branch per body and no SALU inside it (measured on
-gfx950: 26 SIMD-cycles per 8-XOR body against 43.6 for a s_swappc call and
-return, tools/probe/dispatch.py).  Rows 4..7 reuse copies 0..3 under VGPR
-index mode (SRC0|DST, M0 index 32): a stub between the two halves advances M0
-and moves the second half's targets into T[1..3].  4 copies of 256 bodies are
-about 69 KB, which the instruction cache holds (8 copies thrash it).
+m = 0..7).  The bodies exist in C = NCOPY copies (3); copy r XORs into
+accumulator set r and ends with s_setpc_b64 to T[r+1], so body m jumps
+straight to body m+1: one taken branch per body and no SALU inside it
+(measured on gfx950: 26 SIMD-cycles per 8-XOR body against 43.6 for a
+s_swappc call and return, tools/probe/dispatch.py).  Rows C..7 reuse the
+copies under VGPR index mode (SRC0|DST, M0 index 8C per group): a stub
+between groups advances M0 and moves the next group's targets into T[1..].
+3 copies (48 KB, 2 stubs per row) measured 1-2.5 % faster than 4 (64 KB, 1
+stub) at B = 64-256 and in single launches, equal at grouped B = 32; 2
+copies (32 KB, 3 stubs) in between (profiles/r03/ncopy_ab/).  8 copies
+thrash the instruction cache.
 
 The bodies live in gf_bs_export_kernel, which never runs them: it only exports
 their byte offsets.  Every gf_bs_kernel instance jumps into that one copy with
@@ -58,10 +61,10 @@ def set_ring(p):
     P, PG = p, RING + 8 * p
     PGN, VMAX = PG + 1, PG + 2
 # body copies: rows are taken C = NCOPY at a time (copy r for row m = r + C g,
-# M0 index 8 C g), with a stub between groups.  4 (one stub per row) is the
-# shipped build; 3 (2 stubs, 52 KB) and 2 (3 stubs, 35 KB) trade a stub per
-# group for a smaller instruction footprint (A/B builds, KODR_BS_NCOPY)
-NCOPY = int(os.environ.get("KODR_BS_NCOPY", "4"))
+# M0 index 8 C g), with a stub between groups.  3 (2 stubs per row, 48 KB) is
+# the shipped build; 4 (1 stub, 64 KB) and 2 (3 stubs, 32 KB) are A/B builds
+# (KODR_BS_NCOPY); the tuning loops HALF and DYN exist for 4 only
+NCOPY = int(os.environ.get("KODR_BS_NCOPY", "3"))
 assert NCOPY in (2, 3, 4)
 # body start alignment in bytes (0: packed back to back); the instruction
 # fetch after each s_setpc starts at the body's first byte

@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <mutex>
 
+#include "gf_device.hpp"
 #include "gf_kernels.hpp"
 // generated: bodies, row loop, register map (gen_bs_bodies.py)
 #include "gf_bs_bodies.inc"
@@ -184,6 +185,93 @@ struct BsGroupK {
   size_t a_stride, y_stride;
 };
 
+// Side product of a single launch (BsSideK, ncols > 0): Y2 = A x X2 over
+// plain rows X2 of at most a few hundred columns -- the recoded coding
+// vectors r x C next to the recoded pieces (full/recoder.go:32-40), which
+// as a separate gf_gemm launch cost ~3 us at B = 32.  Output row m is done by
+// workgroup m mod gridDim.x: its waves split K (and the lanes of a wave, in
+// S groups of 64/S lanes x 16 bytes), multiply by v_perm tables
+// (gf_make_tables) and fold through LDS.  In the common case (the block's
+// first row, one column block, K <= kSideSteps x KW x S) the loads are
+// issued in the prologue ahead of the row ring, so the work overlaps the
+// ring's HBM latency; the rest runs after the block's store.
+struct BsSideK {
+  const uint8_t* x;
+  uint8_t* y;
+  uint32_t ldx, ldy;
+  int ncols;  // 0: no side product
+};
+constexpr int kSideSteps = 8;
+
+__device__ __forceinline__ int side_groups(int ncols) { return ncols <= 256 ? 4 : ncols <= 512 ? 2 : 1; }
+
+// sum over the S lane groups (lane ^ 16, lane ^ 32)
+__device__ __forceinline__ void side_lane_fold(uint32_t acc[4], int S) {
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    uint32_t v = acc[d];
+    if (S == 4) {
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      v = r[0] ^ r[1];
+    }
+    if (S >= 2) {
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      v = r[0] ^ r[1];
+    }
+    acc[d] = v;
+  }
+}
+
+// lane li of the first wave: the KW waves' partial sums of 16 bytes at col
+__device__ __forceinline__ void side_store(const uint4* part, int kw, const BsSideK& sd, int m, int col, int li) {
+  uint4 v = part[li];
+  for (int w = 1; w < kw; w++) {
+    const uint4 o = part[w * 64 + li];
+    v = make_uint4(v.x ^ o.x, v.y ^ o.y, v.z ^ o.z, v.w ^ o.w);
+  }
+  if (col >= sd.ncols) return;
+  uint8_t* dst = sd.y + (size_t)m * sd.ldy + col;
+  if (col + 16 <= sd.ncols) {
+    *reinterpret_cast<uint4*>(dst) = v;
+  } else {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+    for (int i = 0; col + i < sd.ncols; i++) dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+// every (row, column block) of the side product this block owns, except the
+// one the prologue did (fast_done)
+template <int KW>
+__device__ void bs_side_rest(const uint8_t* __restrict__ A, int lda, int M, int K, const BsSideK& sd, uint4* part,
+                             bool fast_done) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int S = side_groups(sd.ncols), GL = 64 / S, g = lane / GL, li = lane % GL, CB = GL * 16;
+  for (int m = blockIdx.x; m < M; m += gridDim.x) {
+    for (int c0 = 0; c0 < sd.ncols; c0 += CB) {
+      if (fast_done && m == (int)blockIdx.x && c0 == 0) continue;
+      const int col = c0 + li * 16;
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};
+      for (int k = w * S + g; k < K; k += KW * S) {
+        const uint32_t c = A[(size_t)m * lda + k];
+        const uint4 x = col < sd.ncols ? *reinterpret_cast<const uint4*>(sd.x + (size_t)k * sd.ldx + col)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+        uint4 t01;
+        uint32_t t2;
+        gf_make_tables(c, t01, t2);
+        acc[0] = gf_mul_acc4(acc[0], x.x, t01, t2);
+        acc[1] = gf_mul_acc4(acc[1], x.y, t01, t2);
+        acc[2] = gf_mul_acc4(acc[2], x.z, t01, t2);
+        acc[3] = gf_mul_acc4(acc[3], x.w, t01, t2);
+      }
+      side_lane_fold(acc, S);
+      __syncthreads();  // the previous item's (or the main product's) LDS reads are done
+      if (lane < GL) part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+      __syncthreads();
+      if (tid < GL) side_store(part, KW, sd, m, col, tid);
+    }
+  }
+}
+
 // RP: rows in flight per wave in the row ring (KODR_BS_P, one, for single
 // launches; two for grouped launches, whose waves stream long row ranges:
 // DESIGN.md, grouped bit-sliced encode).  Both fit 4 waves per SIMD.
@@ -193,7 +281,7 @@ template <int KW, int MODE = 0, bool GRP = false, int RP = KODR_BS_P>
 __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / KODR_BS_VMAX))) void gf_bs_kernel(
     const uint8_t* __restrict__ A, int lda, int M, int K, const uint8_t* __restrict__ X, int ldx,
     uint8_t* __restrict__ Y, size_t ldy, int ncols, int rpw, int ncx, int nrg,
-    const uint32_t* __restrict__ tgt, uint32_t thi, int accum, const BsGroupK grp) {
+    const uint32_t* __restrict__ tgt, uint32_t thi, int accum, const BsGroupK grp, const BsSideK side) {
   // LDS: [0, 16 KiB) per-row XOR sums [8 rows x 8 planes][64 lanes];
   // [16, 17 KiB) the body target table (absolute lo words of copy 0; copy r
   // is r * KODR_BS_COPY_BYTES further); then each wave's program: per input
@@ -330,7 +418,14 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const int b = blockIdx.x;
   const int rg = (b >> 3) % nrg;
   const int cx = (b / (8 * nrg)) * 8 + (b & 7);
-  if (cx >= ncx) return;
+  // the side product's partial sums: past the programs (bs_lds_bytes)
+  constexpr bool SIDE = !GRP && MODE == 0;
+  uint4* side_part = reinterpret_cast<uint4*>(lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4);
+  if (cx >= ncx) {
+    if constexpr (SIDE)
+      if (side.ncols > 0) bs_side_rest<KW>(A, lda, M, K, side, side_part, false);
+    return;
+  }
   const int m0 = rg * kBsRows, kb = w * rpw;
   // this wave's input rows: [kb, kb + nr), nr a multiple of the 8-row
   // program chunk (rows >= K read zero and have coefficient 0)
@@ -356,6 +451,29 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   uint32_t c[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
+
+  // side product, this block's first row: its loads go ahead of the ring's
+  // (vmcnt retires in issue order), through buffer descriptors that read
+  // zero past K (and everything when the block has no such row)
+  const int s_S = side_groups(side.ncols), s_GL = 64 / s_S, s_g = lane / s_GL, s_li = lane % s_GL;
+  const bool side_fast = SIDE && side.ncols > 0 && (int)blockIdx.x < M && side.ncols <= s_GL * 16 &&
+                         K <= kSideSteps * KW * s_S;
+  uint4 s_x[kSideSteps];
+  uint32_t s_c[kSideSteps];
+  if constexpr (SIDE) {
+    const __amdgpu_buffer_rsrc_t sxr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)side.x, (short)0, side_fast ? (int)((uint32_t)K * side.ldx) : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t sar = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(A + (size_t)blockIdx.x * lda), (short)0, side_fast ? K : 0, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < kSideSteps; j++) {
+      const uint32_t k = (uint32_t)((j * KW + w) * s_S + s_g);
+      s_c[j] = __builtin_amdgcn_raw_buffer_load_b8(sar, k, 0, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sxr, k * side.ldx + (uint32_t)s_li * 16u, 0, 0);
+      s_x[j] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the ring loads
+  }
 
   const uint32_t col = (uint32_t)(cx * 64 + lane) * kBsBlock;
   // rows past this wave's range read zero, so the look-ahead loads of its
@@ -408,7 +526,26 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #else
   uint32_t* progw = nullptr;
 #endif
+  if constexpr (SIDE) {
+    if (side_fast) {
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < kSideSteps; j++) {
+        uint4 t01;
+        uint32_t t2;
+        gf_make_tables(s_c[j], t01, t2);
+        acc[0] = gf_mul_acc4(acc[0], s_x[j].x, t01, t2);
+        acc[1] = gf_mul_acc4(acc[1], s_x[j].y, t01, t2);
+        acc[2] = gf_mul_acc4(acc[2], s_x[j].z, t01, t2);
+        acc[3] = gf_mul_acc4(acc[3], s_x[j].w, t01, t2);
+      }
+      side_lane_fold(acc, s_S);
+      if (lane < s_GL) side_part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+    }
+  }
   __syncthreads();
+  if constexpr (SIDE)
+    if (side_fast && tid < s_GL) side_store(side_part, KW, side, blockIdx.x, s_li * 16, tid);
 
   const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / kBsChunk));
   const uint64_t xa = reinterpret_cast<uint64_t>(X);
@@ -539,6 +676,9 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
         dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
     }
   }
+  if constexpr (SIDE)
+    if (side.ncols > 0 && (!side_fast || (int)blockIdx.x + (int)gridDim.x < M))
+      bs_side_rest<KW>(A, lda, M, K, side, side_part, side_fast);
   if constexpr (MODE == 8) {  // timeline build: stamps past the M output rows (the caller sizes Y)
     __syncthreads();
     stamp[3] = __builtin_amdgcn_s_memtime();
@@ -585,7 +725,7 @@ hipError_t bs_init(int dev, const BsDevice** out) {
     // where gf_bs_kernel runs means the export is wrong, and jumping there
     // would fault
     hipLaunchKernelGGL((gf_bs_kernel<1, 0>), dim3(1), dim3(64), 0, 0, nullptr, 0, 0, 0, nullptr, 0,
-                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u, 0, BsGroupK{});
+                       reinterpret_cast<uint8_t*>(buf), (size_t)0, -1, 0, 0, 0, nullptr, 0u, 0, BsGroupK{}, BsSideK{});
     if ((e = hipGetLastError()) == hipSuccess) e = hipDeviceSynchronize();
     uint32_t kpc[2] = {0, 0};
     if (e == hipSuccess) e = hipMemcpy(kpc, buf, sizeof(kpc), hipMemcpyDeviceToHost);
@@ -619,7 +759,7 @@ hipError_t bs_init(int dev, const BsDevice** out) {
 template <int KW, int MODE = 0>
 hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, int ldx, uint8_t* Y,
                      size_t ldy, int ncols, int rpw, int ncx, int nrg, size_t lds_bytes, const BsDevice* bd,
-                     hipStream_t st, int accum, const GemmGroupArgs* group) {
+                     hipStream_t st, int accum, const GemmGroupArgs* group, const BsSideK& side) {
   const int nb = (ncx + 7) / 8 * 8 * nrg;
   BsGroupK g{};
   if (group) {
@@ -630,11 +770,11 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     // blocks is the single-generation one; the two-row ring (plain loop only)
     constexpr int rp = MODE == 0 ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
-                       lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+                       lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, BsSideK{});
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
   } else {
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE>), dim3(nb), dim3(64 * KW), lds_bytes, st, A, lda, M, K, X, ldx, Y,
-                       ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g);
+                       ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, side);
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, KODR_BS_P, rpw, 1, nb};
   }
   return hipGetLastError();
@@ -740,6 +880,12 @@ bool bs_direct_allowed() {
 
 }  // namespace
 
+bool side_ok(const BsSide& sd, size_t K) {
+  return sd.x && sd.y && (uintptr_t)sd.x % 16 == 0 && (uintptr_t)sd.y % 16 == 0 && sd.ldx % 16 == 0 &&
+         sd.ldy % 16 == 0 && sd.ldx >= (sd.ncols + 15) / 16 * 16 && sd.ldy >= sd.ncols && K * sd.ldx < ((size_t)1 << 31) &&
+         sd.ldy <= 0xffffffffu && sd.ncols <= 0x7fffffff;
+}
+
 BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups, bool grouped) {
   BsPlan p;
   p.ncx = (int)((ncols + kBsWaveCols - 1) / kBsWaveCols);
@@ -774,9 +920,14 @@ BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups, bool grouped) 
 
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
                       uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream, bool accumulate,
-                      const GemmGroupArgs* group) {
+                      const GemmGroupArgs* group, const BsSide* side) {
   if (M == 0 || ncols == 0 || (group && group->n <= 0)) return hipSuccess;
   if (group && group->n > kGemmGroupMax) return hipErrorInvalidValue;
+  BsSideK sk{};
+  if (side && side->ncols) {
+    if (group || accumulate || !side_ok(*side, K)) return hipErrorInvalidValue;
+    sk = BsSideK{side->x, side->y, (uint32_t)side->ldx, (uint32_t)side->ldy, (int)side->ncols};
+  }
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
     return hipErrorInvalidValue;
@@ -791,6 +942,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     p.lds_bytes = bs_lds_bytes(kw, p.rpw);
   }
 #endif
+  if (sk.ncols && p.lds_bytes + (size_t)p.kw * 64 * 16 > kLdsPerCu) return hipErrorInvalidValue;
   const BsDevice* bd = nullptr;
   hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;
@@ -812,8 +964,9 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   }
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
-  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg, p.lds_bytes, bd, stream, \
-                          accumulate ? 1 : 0, group)
+  bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg,                 \
+                        p.lds_bytes + (sk.ncols ? (size_t)p.kw * 64 * 16 : 0), bd, stream, accumulate ? 1 : 0, \
+                        group, sk)
 #ifdef KODR_TUNE_MODES
 #define KODR_BS_CASE(KW_)                                                                         \
   case KW_:                                                                                       \

@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "gf_device.hpp"
 #include "gf_kernels.hpp"
 
 namespace kodr_amd {
@@ -37,23 +38,6 @@ LaunchPlan& last_launch_plan() {
 }
 
 namespace {
-
-__device__ __forceinline__ uint32_t xt(uint32_t c) {  // multiply by x (=2) mod 0x11D
-  return ((c << 1) ^ ((c & 0x80u) ? 0x1Du : 0u)) & 0xFFu;
-}
-
-// T0 = c*{0..7}, T1 = c*{0..7}<<3, T2 = c*{0..3}<<6, little-endian bytes.
-__device__ __forceinline__ void make_tables(uint32_t c, uint4& t01, uint32_t& t2) {
-  const uint32_t c1 = c, c2 = xt(c1), c4 = xt(c2), c8 = xt(c4);
-  const uint32_t c16 = xt(c8), c32 = xt(c16), c64 = xt(c32), c128 = xt(c64);
-  const uint32_t lo0 = (c1 << 8) | (c2 << 16) | ((c1 ^ c2) << 24);
-  const uint32_t lo1 = (c8 << 8) | (c16 << 16) | ((c8 ^ c16) << 24);
-  t01.x = lo0;
-  t01.y = lo0 ^ (c4 * 0x01010101u);
-  t01.z = lo1;
-  t01.w = lo1 ^ (c32 * 0x01010101u);
-  t2 = (c64 << 8) | (c128 << 16) | ((c64 ^ c128) << 24);
-}
 
 constexpr int kLaneBytes = 16;  // one dwordx4 per lane per row
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -162,7 +146,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
       if (idx < KC * MT) {
         uint4 t01;
         uint32_t t2;
-        make_tables(cf[j], t01, t2);
+        gf_make_tables(cf[j], t01, t2);
         tab01[buf * KC * MT + idx] = t01;
         tab2[buf * KC * MT + idx] = t2;
       }
@@ -346,7 +330,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restr
     uint32_t c = __builtin_amdgcn_readlane(cv, S * j);
 #pragma unroll
     for (int q = 1; q < S; q++) c = g == q ? __builtin_amdgcn_readlane(cv, S * j + q) : c;
-    make_tables(c, t01[j], t2[j]);
+    gf_make_tables(c, t01[j], t2[j]);
   }
   uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll

@@ -163,11 +163,25 @@ struct BsPlan {
 // wave per workgroup takes the direct variant (no LDS fold)
 BsPlan plan_gemm_bs(size_t M, size_t K, size_t ncols, int groups = 1, bool grouped = false);
 
+// Side product of a single bit-sliced launch: y = A (x) x over plain rows of
+// ncols bytes (the recoded coding vectors beside the recoded pieces); 16-byte
+// aligned rows and pitches, ldx >= ncols rounded up to 16, K * ldx < 2^31.
+struct BsSide {
+  const uint8_t* x = nullptr;
+  size_t ldx = 0;
+  uint8_t* y = nullptr;
+  size_t ldy = 0;
+  size_t ncols = 0;
+};
+bool side_ok(const BsSide& side, size_t K);
+
 // Y = A (x) X with X bit-sliced (bitslice_rows), Y in plain bytes.  group:
 // up to kGemmGroupMax products of this shape in one launch (X = group->x[i],
-// A + i * a_stride, Y + i * y_stride; dXbs unused).
+// A + i * a_stride, Y + i * y_stride; dXbs unused).  side (single launches,
+// not accumulating): also y = A (x) x in the same launch.
 hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dXbs, size_t ldx,
                       uint8_t* dY, size_t ldy, size_t ncols, int device, hipStream_t stream,
-                      bool accumulate = false, const GemmGroupArgs* group = nullptr);
+                      bool accumulate = false, const GemmGroupArgs* group = nullptr,
+                      const BsSide* side = nullptr);
 
 }  // namespace kodr_amd

@@ -264,8 +264,29 @@ LOOPS = {"main": lambda: gen.main_loop(True),
          "sload": lambda: gen.main_loop(True, True, gen.ROW_PRIO, None, (), True)}
 
 
+@pytest.fixture
+def four_copies():
+    """The tuning loops written for 4 body copies (HALF, DYN)."""
+    c0 = gen.NCOPY
+    gen.set_ncopy(4)
+    yield
+    gen.set_ncopy(c0)
+
+
+@pytest.mark.parametrize("ncopy", [3, 4])
 @pytest.mark.parametrize("variant", sorted(LOOPS))
-def test_threaded_dispatch_end_to_end_vs_oracle(variant):
+def test_threaded_dispatch_end_to_end_vs_oracle(variant, ncopy):
+    if variant == "half" and ncopy != 4:
+        pytest.skip("the half-priority stubs exist for 4 copies only")
+    c0 = gen.NCOPY
+    gen.set_ncopy(ncopy)
+    try:
+        _threaded_dispatch(variant)
+    finally:
+        gen.set_ncopy(c0)
+
+
+def _threaded_dispatch(variant):
     rng = np.random.default_rng(11)
     for nr in (8, 16, 24):
         X = rng.integers(0, 256, (nr, 32), dtype=np.uint8)
@@ -347,7 +368,7 @@ class _DynWave(_Wave):
 
 
 @pytest.mark.parametrize("K,kw", [(8, 1), (13, 2), (40, 3), (33, 4)])
-def test_dynamic_rows_end_to_end_vs_oracle(K, kw):
+def test_dynamic_rows_end_to_end_vs_oracle(K, kw, four_copies):
     rng = np.random.default_rng(100 + K)
     X = rng.integers(0, 256, (K, 32), dtype=np.uint8)
     A = rng.integers(0, 256, (8, K), dtype=np.uint8)
@@ -404,9 +425,9 @@ def test_two_row_ring_end_to_end_vs_oracle():
 @pytest.mark.parametrize("ncopy", [2, 3])
 @pytest.mark.parametrize("ring", [1, 2])
 def test_fewer_copies_end_to_end_vs_oracle(ncopy, ring):
-    # the A/B builds with fewer body copies (KODR_BS_NCOPY): row groups of
-    # ncopy rows joined by ceil(8/ncopy)-1 stubs, return address computed per
-    # row; SGPRs stay below the kernel's budget
+    # the shipped 3 copies and the 2-copy A/B build (KODR_BS_NCOPY): row
+    # groups of ncopy rows joined by ceil(8/ncopy)-1 stubs, return address
+    # computed per row; SGPRs stay below the kernel's budget
     c0, p0 = gen.NCOPY, gen.P
     gen.set_ncopy(ncopy)
     gen.set_ring(ring)

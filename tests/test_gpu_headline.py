@@ -336,8 +336,8 @@ def test_grouped_recode_vs_oracle(gpu_ctx, G, k, L, n, count, compact):
 def test_recode_c2_device_split_plan(gpu_ctx, c2_generation):
     # the bench's c2_recode leg at B = 32 through the device API: the piece
     # columns take the encoder's launch shape (64 column chunks x 4 row
-    # groups, one round of KW = 16 workgroups) and the vector columns a
-    # narrow gf_gemm; every recoded wire row against the oracle's recode
+    # groups, one round of KW = 16 workgroups) and the vector columns are
+    # that launch's side product; every recoded wire row against the oracle
     P = c2_generation
     k, L = P.shape
     rng = np.random.default_rng(0x2EC0)
