@@ -298,7 +298,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
 // multiply once its row lands, and the tail after the last row is short.
 // Partial sums: lane groups by v_permlane16/32_swap, waves through one LDS
 // slot each and a single barrier (no atomics, nothing to zero).
-template <int KW, int RPW, int S>
+template <int KW, int RPW, int S, int AUX = 0>
 __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restrict__ A, int K,
                                                           const uint8_t* __restrict__ X, size_t ldx,
                                                           uint8_t* __restrict__ Y, int ncols, int accum) {
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restr
   u32x4 ring[STEPS];
 #pragma unroll
   for (int j = 0; j < STEPS; j++)
-    ring[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (r0 + S * j + g) * ildx + col, 0, 0);
+    ring[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (r0 + S * j + g) * ildx + col, 0, AUX);
   __builtin_amdgcn_sched_barrier(0);
   uint4 t01[STEPS];
   uint32_t t2[STEPS];
@@ -653,7 +653,8 @@ static bool env_config(GemmConfig* g) {
 // groups: 8.5 us per 32 MiB/256 coded piece in rocprof against 9.4 on
 // gf_gemm_kernel<1, 16, 2> (profiles/r03/b1/); four lane groups (256-byte
 // chunks, two workgroups per CU) measured 9.4.  KODR_GEMV=0/2/4 selects
-// gf_gemm_kernel / 2 / 4 lane groups (A/B measurements).
+// gf_gemm_kernel / 2 / 4 lane groups, 3 two lane groups with non-temporal
+// row loads (A/B measurements).
 static int gemv_enabled() {
   static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 2;
   return v;
@@ -675,6 +676,9 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
     if (S == 4)
       hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 4>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
                          dX, ldx, dY, (int)ncols, acc);
+    else if (gemv == 3)
+      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2, 2>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA,
+                         (int)K, dX, ldx, dY, (int)ncols, acc);
     else
       hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
                          dX, ldx, dY, (int)ncols, acc);
