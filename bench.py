@@ -196,6 +196,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--no-encode-decode", action="store_true",
+                    help="skip the encode_decode round trip (PMC runs of the headline launch alone)")
     args = ap.parse_args()
 
     from kodr_amd import dist as kdist
@@ -286,7 +288,7 @@ def main():
 
     extras = {"construct_ms_per_generation": round(construct_ms, 3)}
     ed = None
-    if rank == 0:
+    if rank == 0 and not args.no_encode_decode:
         try:
             ed = encode_decode(ctx, L_, errors, encs, k, L)
         except Exception as e:  # secondary measurement: never lose the headline line

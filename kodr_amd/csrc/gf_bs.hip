@@ -200,6 +200,7 @@ struct BsSideK {
   uint8_t* y;
   uint32_t ldx, ldy;
   int ncols;  // 0: no side product
+  int stage;  // stage the block's first row's inputs in LDS (one-workgroup-per-CU plans)
 };
 constexpr int kSideSteps = 8;
 
@@ -237,6 +238,30 @@ __device__ __forceinline__ void side_store(const uint4* part, int kw, const BsSi
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
     for (int i = 0; col + i < sd.ncols; i++) dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
   }
+}
+
+// LDS-DMA copy of 16 bytes per lane: base[voff .. voff + 16) (zero past nrec)
+// to LDS address lds_addr + 16 * lane.  Inline asm, so that the compiler
+// neither counts these loads nor waits for them at its own LDS accesses; the
+// caller issues them before any load of its own (vmcnt retires in issue
+// order, so the compiler's counts stay right) and waits for them itself.
+__device__ __forceinline__ void bs_lds_dma(uint64_t base, uint32_t nrec, uint32_t voff, uint32_t lds_addr) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) & 0xffffu;
+  const uint32_t sl = __builtin_amdgcn_readfirstlane(lds_addr), sn = __builtin_amdgcn_readfirstlane(nrec);
+  // m0 is saved and restored (the compiler does not take it as a clobber)
+  asm volatile(
+      "s_mov_b32 s35, m0\n\t"
+      "s_mov_b32 s36, %[lo]\n\t"
+      "s_mov_b32 s37, %[hi]\n\t"
+      "s_mov_b32 s38, %[n]\n\t"
+      "s_mov_b32 s39, 0x00020000\n\t"
+      "s_mov_b32 m0, %[l]\n\t"
+      "buffer_load_dwordx4 %[v], s[36:39], 0 offen lds\n\t"
+      "s_mov_b32 m0, s35\n\t"
+      :
+      : [lo] "s"(lo), [hi] "s"(hi), [n] "s"(sn), [l] "s"(sl), [v] "v"(voff)
+      : "s35", "s36", "s37", "s38", "s39", "memory");
 }
 
 // every (row, column block) of the side product this block owns, except the
@@ -448,6 +473,27 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     const int i = tid + j * 64 * KW;
     ot[j] = i < kTgt ? tgt[i] : 0u;
   }
+  // side product staged in LDS (side.stage): the block's coefficient row and
+  // the whole K x ncols side input are copied by LDS-DMA loads issued before
+  // every other load of the block; the product runs from LDS after the store
+  const bool side_staged = SIDE && side.ncols > 0 && side.stage && (int)blockIdx.x < M;
+  const int s_P16 = (side.ncols + 15) >> 4;  // 16-byte units per staged row
+  uint32_t* side_a = lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4 + KW * 64 * 4;  // 1 KiB: the coefficient row
+  uint32_t* side_c = side_a + 256;                                              // K rows of 16 * s_P16 bytes
+  if constexpr (SIDE) {
+    if (side_staged) {
+      const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(side_a);
+      const uint32_t lc = (uint32_t)reinterpret_cast<uintptr_t>(side_c);
+      if (w == 0)
+        bs_lds_dma(reinterpret_cast<uint64_t>(A + (size_t)blockIdx.x * lda), (uint32_t)K, (uint32_t)lane * 16u, la);
+      const int units = K * s_P16;
+      for (int u0 = w * 64; u0 < units; u0 += KW * 64) {
+        const int u = u0 + lane, row = u / s_P16, c16 = u - row * s_P16;
+        bs_lds_dma(reinterpret_cast<uint64_t>(side.x), (uint32_t)K * side.ldx,
+                   (uint32_t)row * side.ldx + (uint32_t)c16 * 16u, lc + (uint32_t)u0 * 16u);
+      }
+    }
+  }
   uint32_t c[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
@@ -456,8 +502,8 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // (vmcnt retires in issue order), through buffer descriptors that read
   // zero past K (and everything when the block has no such row)
   const int s_S = side_groups(side.ncols), s_GL = 64 / s_S, s_g = lane / s_GL, s_li = lane % s_GL;
-  const bool side_fast = SIDE && side.ncols > 0 && (int)blockIdx.x < M && side.ncols <= s_GL * 16 &&
-                         K <= kSideSteps * KW * s_S;
+  const bool side_fast = SIDE && side.ncols > 0 && !side.stage && (int)blockIdx.x < M &&
+                         side.ncols <= s_GL * 16 && K <= kSideSteps * KW * s_S;
   uint4 s_x[kSideSteps];
   uint32_t s_c[kSideSteps];
   if constexpr (SIDE) {
@@ -676,9 +722,32 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
         dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
     }
   }
-  if constexpr (SIDE)
-    if (side.ncols > 0 && (!side_fast || (int)blockIdx.x + (int)gridDim.x < M))
-      bs_side_rest<KW>(A, lda, M, K, side, side_part, side_fast);
+  if constexpr (SIDE) {
+    if (side_staged) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const uint8_t* al = reinterpret_cast<const uint8_t*>(side_a);
+      const uint4* cl = reinterpret_cast<const uint4*>(side_c);
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};
+      for (int k = w * s_S + s_g; k < K; k += KW * s_S) {
+        const uint4 x = s_li < s_P16 ? cl[k * s_P16 + s_li] : make_uint4(0u, 0u, 0u, 0u);
+        uint4 t01;
+        uint32_t t2;
+        gf_make_tables(al[k], t01, t2);
+        acc[0] = gf_mul_acc4(acc[0], x.x, t01, t2);
+        acc[1] = gf_mul_acc4(acc[1], x.y, t01, t2);
+        acc[2] = gf_mul_acc4(acc[2], x.z, t01, t2);
+        acc[3] = gf_mul_acc4(acc[3], x.w, t01, t2);
+      }
+      side_lane_fold(acc, s_S);
+      if (lane < s_GL) side_part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+      __syncthreads();
+      if (tid < s_GL) side_store(side_part, KW, side, blockIdx.x, s_li * 16, tid);
+    }
+    const bool first_done = side_fast || side_staged;
+    if (side.ncols > 0 && (!first_done || (int)blockIdx.x + (int)gridDim.x < M))
+      bs_side_rest<KW>(A, lda, M, K, side, side_part, first_done);
+  }
   if constexpr (MODE == 8) {  // timeline build: stamps past the M output rows (the caller sizes Y)
     __syncthreads();
     stamp[3] = __builtin_amdgcn_s_memtime();
@@ -880,6 +949,15 @@ bool bs_direct_allowed() {
 
 }  // namespace
 
+size_t ncols_side_units(int ncols) { return ((size_t)ncols + 15) / 16; }
+
+// KODR_SIDE_STAGE=1: stage the side inputs in LDS where the plan has one
+// workgroup per CU (A/B; the register path otherwise)
+bool side_stage_enabled() {
+  static const bool v = getenv("KODR_SIDE_STAGE") ? atoi(getenv("KODR_SIDE_STAGE")) != 0 : false;
+  return v;
+}
+
 bool side_ok(const BsSide& sd, size_t K) {
   return sd.x && sd.y && (uintptr_t)sd.x % 16 == 0 && (uintptr_t)sd.y % 16 == 0 && sd.ldx % 16 == 0 &&
          sd.ldy % 16 == 0 && sd.ldx >= (sd.ncols + 15) / 16 * 16 && sd.ldy >= sd.ncols && K * sd.ldx < ((size_t)1 << 31) &&
@@ -926,7 +1004,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   BsSideK sk{};
   if (side && side->ncols) {
     if (group || accumulate || !side_ok(*side, K)) return hipErrorInvalidValue;
-    sk = BsSideK{side->x, side->y, (uint32_t)side->ldx, (uint32_t)side->ldy, (int)side->ncols};
+    sk = BsSideK{side->x, side->y, (uint32_t)side->ldx, (uint32_t)side->ldy, (int)side->ncols, 0};
   }
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
@@ -942,7 +1020,18 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     p.lds_bytes = bs_lds_bytes(kw, p.rpw);
   }
 #endif
-  if (sk.ncols && p.lds_bytes + (size_t)p.kw * 64 * 16 > kLdsPerCu) return hipErrorInvalidValue;
+  size_t side_lds = 0;
+  if (sk.ncols) {
+    side_lds = (size_t)p.kw * 64 * 16;
+    // staged side inputs when one workgroup holds the CU anyway (KW = 16)
+    const size_t staged = 1024 + (K * ((ncols_side_units(sk.ncols)) * 16) + 1023) / 1024 * 1024;
+    if (p.kw == 16 && side_stage_enabled() && K <= 1024 && sk.ncols <= 1024 &&
+        p.lds_bytes + side_lds + staged <= kLdsPerCu) {
+      sk.stage = 1;
+      side_lds += staged;
+    }
+    if (p.lds_bytes + side_lds > kLdsPerCu) return hipErrorInvalidValue;
+  }
   const BsDevice* bd = nullptr;
   hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;
@@ -965,7 +1054,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
 #endif
 #define KODR_BS_CALL(KW_, MODE_)                                                                  \
   bs_launch<KW_, MODE_>(dA, ild, iM, iK, dXbs, ilx, dY, ldy, inc, p.rpw, p.ncx, p.nrg,                 \
-                        p.lds_bytes + (sk.ncols ? (size_t)p.kw * 64 * 16 : 0), bd, stream, accumulate ? 1 : 0, \
+                        p.lds_bytes + side_lds, bd, stream, accumulate ? 1 : 0,                         \
                         group, sk)
 #ifdef KODR_TUNE_MODES
 #define KODR_BS_CASE(KW_)                                                                         \

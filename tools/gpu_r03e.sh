@@ -6,6 +6,7 @@
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-r03e}; mkdir -p $OUT
+timeout -k 10 60 tools/probe/cu_map 4096 > $OUT/cu_map.txt || exit 1
 timeout -k 10 300 python -u -m pytest -x -v -m gpu --timeout 120 --timeout-method thread tests/test_gpu_recode_side.py > $OUT/pytest_side.log 2>&1 || { tail -40 $OUT/pytest_side.log; exit 1; }
 tail -1 $OUT/pytest_side.log
 for rep in 1 2 3; do

@@ -14,6 +14,9 @@ out, B = sys.argv[1], int(sys.argv[2])
 KERNEL = sys.argv[3] if len(sys.argv) > 3 else ("gf_bs_kernel" if B >= 16 else "gf_gemm_kernel")
 # the library's one-workgroup probe launch of the same template is not a product
 MIN_GRID = int(sys.argv[4]) if len(sys.argv) > 4 else 64 * 64
+# argv[5] == "headline": only the counter rows of the most common grid of the
+# kernel (the timed launch; warmup and setup launches of other shapes aside)
+ONLY_MODAL = len(sys.argv) > 5 and sys.argv[5] == "headline"
 
 
 def rows(pattern):
@@ -29,8 +32,20 @@ fetch = [float(r["Counter_Value"]) for r in rows("fetch/**/*counter_collection.c
 write = [float(r["Counter_Value"]) for r in rows("write/**/*counter_collection.csv")
          if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE"
          and int(r.get("Grid_Size", MIN_GRID)) >= MIN_GRID]
+grid = None
+if ONLY_MODAL:
+    import collections
+    grids = collections.Counter(r["Grid_Size"] for r in rows("fetch/**/*counter_collection.csv")
+                                if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE")
+    grid = grids.most_common(1)[0][0] if grids else None
+    fetch = [float(r["Counter_Value"]) for r in rows("fetch/**/*counter_collection.csv")
+             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE" and r["Grid_Size"] == grid]
+    write = [float(r["Counter_Value"]) for r in rows("write/**/*counter_collection.csv")
+             if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == "WRITE_SIZE" and r["Grid_Size"] == grid]
 res = {
     "batch": B,
+    "counter_grid_threads": grid,
+    "counter_launches": len(fetch),
     "kernel": KERNEL,
     "kernel_launches_traced": len(dur),
     "avg_kernel_us": round(statistics.mean(dur) / 1e3, 3) if dur else None,

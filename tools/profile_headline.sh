@@ -16,12 +16,13 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
   || { tail -20 "$OUT/trace.err"; exit 1; }
 python3 "$R/tools/prof_headline.py" "$OUT/trace/run_kernel_trace.csv" "$OUT/bench_trace.json" \
   --out "$OUT/prof_headline.json" > /dev/null || exit 1
-HB=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-extras --no-cpu-baseline)
+HB=(python3 "$R/bench.py" --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-encode-decode)
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- "${HB[@]}" \
   > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err" || { tail -20 "$OUT/fetch.err"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- "${HB[@]}" \
   > "$OUT/bench_write.json" 2> "$OUT/write.err" || { tail -20 "$OUT/write.err"; exit 1; }
-python3 "$R/tools/pmc_summary.py" "$OUT" 32 "gf_bs_kernel<" > "$OUT/pmc_summary.json" || exit 1
+# the headline launch's grid (threads): the most common gf_bs_kernel grid of the PMC runs
+python3 "$R/tools/pmc_summary.py" "$OUT" 32 "gf_bs_kernel<" 4096 headline > "$OUT/pmc_summary.json" || exit 1
 python3 - "$OUT" <<'PY'
 import json, sys
 o = sys.argv[1]
