@@ -238,7 +238,10 @@ size_t rlnc_recoder_coded_piece_len(const rlnc_recoder* rec);    /* k + L */
 /* `count` CodedPiece() calls (full/recoder.go:27-46): r = count x n caller
  * bytes; out = count x (k+L) wire rows [r x C | sum r_i P_i] */
 int rlnc_recoder_coded_pieces(rlnc_recoder* rec, const uint8_t* r, size_t count, uint8_t* out);
-/* device-resident: d_r count x n (device), d_out count wire rows at out_pitch */
+/* device-resident: d_r count x n (device), d_out count wire rows at out_pitch
+ * (any pitch >= k + L; rows that are not 16-byte aligned are computed aside and
+ * copied).  From 9 pieces and k a multiple of 16, one bit-sliced launch writes
+ * whole wire rows (the coding-vector columns are that launch's side product). */
 int rlnc_recoder_coded_pieces_device(rlnc_recoder* rec, const uint8_t* d_r, size_t count,
                                      uint8_t* d_out, size_t out_pitch);
 
