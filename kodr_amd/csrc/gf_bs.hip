@@ -186,114 +186,74 @@ struct BsGroupK {
 };
 
 // Side product of a single launch (BsSideK, ncols > 0): Y2 = A x X2 over
-// plain rows X2 of at most a few hundred columns -- the recoded coding
-// vectors r x C next to the recoded pieces (full/recoder.go:32-40), which
-// as a separate gf_gemm launch cost ~3 us at B = 32.  Output row m is done by
-// workgroup m mod gridDim.x: its waves split K (and the lanes of a wave, in
-// S groups of 64/S lanes x 16 bytes), multiply by v_perm tables
-// (gf_make_tables) and fold through LDS.  In the common case (the block's
-// first row, one column block, K <= kSideSteps x KW x S) the loads are
-// issued in the prologue ahead of the row ring, so the work overlaps the
-// ring's HBM latency; the rest runs after the block's store.
+// plain rows X2 of a few hundred columns -- the recoded coding vectors r x C
+// next to the recoded pieces (full/recoder.go:32-40), otherwise a gf_gemm
+// launch of their own (~5 us at B = 32).  The work is spread over every
+// workgroup of the launch, so that none of them finishes late: a unit is one
+// output row x 16 bytes, block b owns units [b U / nb, (b + 1) U / nb) of
+// U = M x ceil(ncols / 16); thread t owns dword t % 4 of the unit and the
+// input rows k = t / 4 + j x 16 KW, multiplies by v_perm tables
+// (gf_make_tables), and the block folds through lane shuffles and LDS.  Up to
+// kSideUnits units x kSidePass row steps are loaded in the prologue, ahead of
+// the row ring, and multiplied while the ring's rows are in flight; blocks
+// with more run their units after the store.
 struct BsSideK {
   const uint8_t* x;
   uint8_t* y;
   uint32_t ldx, ldy;
   int ncols;  // 0: no side product
-  int stage;  // stage the block's first row's inputs in LDS (one-workgroup-per-CU plans)
 };
-constexpr int kSideSteps = 8;
+constexpr int kSideUnits = 2, kSidePass = 4;
 
-__device__ __forceinline__ int side_groups(int ncols) { return ncols <= 256 ? 4 : ncols <= 512 ? 2 : 1; }
-
-// sum over the S lane groups (lane ^ 16, lane ^ 32)
-__device__ __forceinline__ void side_lane_fold(uint32_t acc[4], int S) {
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    uint32_t v = acc[d];
-    if (S == 4) {
-      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-      v = r[0] ^ r[1];
-    }
-    if (S >= 2) {
-      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-      v = r[0] ^ r[1];
-    }
-    acc[d] = v;
+// XOR over the 16 lanes of a wave that share lane % 4 (lane ^ 4 ... ^ 32)
+__device__ __forceinline__ uint32_t side_fold16(uint32_t v) {
+  v ^= __shfl_xor(v, 4);
+  v ^= __shfl_xor(v, 8);
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // lane ^ 16
+    v = r[0] ^ r[1];
   }
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);    // lane ^ 32
+  return r[0] ^ r[1];
 }
 
-// lane li of the first wave: the KW waves' partial sums of 16 bytes at col
-__device__ __forceinline__ void side_store(const uint4* part, int kw, const BsSideK& sd, int m, int col, int li) {
-  uint4 v = part[li];
-  for (int w = 1; w < kw; w++) {
-    const uint4 o = part[w * 64 + li];
-    v = make_uint4(v.x ^ o.x, v.y ^ o.y, v.z ^ o.z, v.w ^ o.w);
-  }
+// dword d of unit u from the KW waves' partial sums part[w * 4 + d]
+__device__ __forceinline__ void side_store_dword(const uint32_t* part, int kw, const BsSideK& sd, int n16, int u,
+                                                 int d) {
+  uint32_t v = 0;
+  for (int w = 0; w < kw; w++) v ^= part[w * 4 + d];
+  const int row = u / n16, col = (u - row * n16) * 16 + d * 4;
   if (col >= sd.ncols) return;
-  uint8_t* dst = sd.y + (size_t)m * sd.ldy + col;
-  if (col + 16 <= sd.ncols) {
-    *reinterpret_cast<uint4*>(dst) = v;
+  uint8_t* dst = sd.y + (size_t)row * sd.ldy + col;
+  if (col + 4 <= sd.ncols) {
+    *reinterpret_cast<uint32_t*>(dst) = v;
   } else {
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    for (int i = 0; col + i < sd.ncols; i++) dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3)));
+    for (int i = 0; col + i < sd.ncols; i++) dst[i] = (uint8_t)(v >> (8 * i));
   }
 }
 
-// LDS-DMA copy of 16 bytes per lane: base[voff .. voff + 16) (zero past nrec)
-// to LDS address lds_addr + 16 * lane.  Inline asm, so that the compiler
-// neither counts these loads nor waits for them at its own LDS accesses; the
-// caller issues them before any load of its own (vmcnt retires in issue
-// order, so the compiler's counts stay right) and waits for them itself.
-__device__ __forceinline__ void bs_lds_dma(uint64_t base, uint32_t nrec, uint32_t voff, uint32_t lds_addr) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) & 0xffffu;
-  const uint32_t sl = __builtin_amdgcn_readfirstlane(lds_addr), sn = __builtin_amdgcn_readfirstlane(nrec);
-  // m0 is saved and restored (the compiler does not take it as a clobber)
-  asm volatile(
-      "s_mov_b32 s35, m0\n\t"
-      "s_mov_b32 s36, %[lo]\n\t"
-      "s_mov_b32 s37, %[hi]\n\t"
-      "s_mov_b32 s38, %[n]\n\t"
-      "s_mov_b32 s39, 0x00020000\n\t"
-      "s_mov_b32 m0, %[l]\n\t"
-      "buffer_load_dwordx4 %[v], s[36:39], 0 offen lds\n\t"
-      "s_mov_b32 m0, s35\n\t"
-      :
-      : [lo] "s"(lo), [hi] "s"(hi), [n] "s"(sn), [l] "s"(sl), [v] "v"(voff)
-      : "s35", "s36", "s37", "s38", "s39", "memory");
-}
-
-// every (row, column block) of the side product this block owns, except the
-// one the prologue did (fast_done)
+// the block's units [u0, u1) outside the prologue (blocks past the column
+// chunks, or more units or row steps than the prologue holds)
 template <int KW>
-__device__ void bs_side_rest(const uint8_t* __restrict__ A, int lda, int M, int K, const BsSideK& sd, uint4* part,
-                             bool fast_done) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int S = side_groups(sd.ncols), GL = 64 / S, g = lane / GL, li = lane % GL, CB = GL * 16;
-  for (int m = blockIdx.x; m < M; m += gridDim.x) {
-    for (int c0 = 0; c0 < sd.ncols; c0 += CB) {
-      if (fast_done && m == (int)blockIdx.x && c0 == 0) continue;
-      const int col = c0 + li * 16;
-      uint32_t acc[4] = {0u, 0u, 0u, 0u};
-      for (int k = w * S + g; k < K; k += KW * S) {
-        const uint32_t c = A[(size_t)m * lda + k];
-        const uint4 x = col < sd.ncols ? *reinterpret_cast<const uint4*>(sd.x + (size_t)k * sd.ldx + col)
-                                       : make_uint4(0u, 0u, 0u, 0u);
-        uint4 t01;
-        uint32_t t2;
-        gf_make_tables(c, t01, t2);
-        acc[0] = gf_mul_acc4(acc[0], x.x, t01, t2);
-        acc[1] = gf_mul_acc4(acc[1], x.y, t01, t2);
-        acc[2] = gf_mul_acc4(acc[2], x.z, t01, t2);
-        acc[3] = gf_mul_acc4(acc[3], x.w, t01, t2);
-      }
-      side_lane_fold(acc, S);
-      __syncthreads();  // the previous item's (or the main product's) LDS reads are done
-      if (lane < GL) part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-      __syncthreads();
-      if (tid < GL) side_store(part, KW, sd, m, col, tid);
+__device__ void bs_side_rest(const uint8_t* __restrict__ A, int lda, int K, const BsSideK& sd, uint32_t* part,
+                             int u0, int u1) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, d = tid & 3, kt = tid >> 2;
+  const int n16 = (sd.ncols + 15) >> 4;
+  for (int u = u0; u < u1; u++) {
+    const int row = u / n16, col = (u - row * n16) * 16 + d * 4;
+    uint32_t acc = 0;
+    for (int k = kt; k < K; k += 16 * KW) {
+      const uint32_t x = col < sd.ncols ? *reinterpret_cast<const uint32_t*>(sd.x + (size_t)k * sd.ldx + col) : 0u;
+      uint4 t01;
+      uint32_t t2;
+      gf_make_tables(A[(size_t)row * lda + k], t01, t2);
+      acc = gf_mul_acc4(acc, x, t01, t2);
     }
+    acc = side_fold16(acc);
+    __syncthreads();  // the previous unit's (or the main product's) LDS reads are done
+    if (lane < 4) part[w * 4 + lane] = acc;
+    __syncthreads();
+    if (tid < 4) side_store_dword(part, KW, sd, n16, u, tid);
   }
 }
 
@@ -445,10 +405,13 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const int cx = (b / (8 * nrg)) * 8 + (b & 7);
   // the side product's partial sums: past the programs (bs_lds_bytes)
   constexpr bool SIDE = !GRP && MODE == 0;
-  uint4* side_part = reinterpret_cast<uint4*>(lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4);
+  uint32_t* side_part = lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4;
+  const int s_n16 = (side.ncols + 15) >> 4;
+  const long s_U = (long)M * s_n16;
+  const int s_u0 = (int)((long)blockIdx.x * s_U / gridDim.x), s_u1 = (int)((long)(blockIdx.x + 1) * s_U / gridDim.x);
   if (cx >= ncx) {
     if constexpr (SIDE)
-      if (side.ncols > 0) bs_side_rest<KW>(A, lda, M, K, side, side_part, false);
+      if (side.ncols > 0) bs_side_rest<KW>(A, lda, K, side, side_part, s_u0, s_u1);
     return;
   }
   const int m0 = rg * kBsRows, kb = w * rpw;
@@ -473,50 +436,31 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     const int i = tid + j * 64 * KW;
     ot[j] = i < kTgt ? tgt[i] : 0u;
   }
-  // side product staged in LDS (side.stage): the block's coefficient row and
-  // the whole K x ncols side input are copied by LDS-DMA loads issued before
-  // every other load of the block; the product runs from LDS after the store
-  const bool side_staged = SIDE && side.ncols > 0 && side.stage && (int)blockIdx.x < M;
-  const int s_P16 = (side.ncols + 15) >> 4;  // 16-byte units per staged row
-  uint32_t* side_a = lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4 + KW * 64 * 4;  // 1 KiB: the coefficient row
-  uint32_t* side_c = side_a + 256;                                              // K rows of 16 * s_P16 bytes
-  if constexpr (SIDE) {
-    if (side_staged) {
-      const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(side_a);
-      const uint32_t lc = (uint32_t)reinterpret_cast<uintptr_t>(side_c);
-      if (w == 0)
-        bs_lds_dma(reinterpret_cast<uint64_t>(A + (size_t)blockIdx.x * lda), (uint32_t)K, (uint32_t)lane * 16u, la);
-      const int units = K * s_P16;
-      for (int u0 = w * 64; u0 < units; u0 += KW * 64) {
-        const int u = u0 + lane, row = u / s_P16, c16 = u - row * s_P16;
-        bs_lds_dma(reinterpret_cast<uint64_t>(side.x), (uint32_t)K * side.ldx,
-                   (uint32_t)row * side.ldx + (uint32_t)c16 * 16u, lc + (uint32_t)u0 * 16u);
-      }
-    }
-  }
   uint32_t c[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
 
-  // side product, this block's first row: its loads go ahead of the ring's
-  // (vmcnt retires in issue order), through buffer descriptors that read
-  // zero past K (and everything when the block has no such row)
-  const int s_S = side_groups(side.ncols), s_GL = 64 / s_S, s_g = lane / s_GL, s_li = lane % s_GL;
-  const bool side_fast = SIDE && side.ncols > 0 && !side.stage && (int)blockIdx.x < M &&
-                         side.ncols <= s_GL * 16 && K <= kSideSteps * KW * s_S;
-  uint4 s_x[kSideSteps];
-  uint32_t s_c[kSideSteps];
+  // side product: this block's units, loaded ahead of the row ring (vmcnt
+  // retires in issue order) through descriptors that read zero past K
+  const int s_d = tid & 3, s_kt = tid >> 2;
+  const int s_nu = s_u1 - s_u0, s_np = (K + 16 * KW - 1) / (16 * KW);
+  const bool side_fast = SIDE && side.ncols > 0 && s_nu <= kSideUnits && s_np <= kSidePass;
+  uint32_t s_x[kSideUnits][kSidePass], s_c[kSideUnits][kSidePass];
   if constexpr (SIDE) {
-    const __amdgpu_buffer_rsrc_t sxr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)side.x, (short)0, side_fast ? (int)((uint32_t)K * side.ldx) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t sar = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(A + (size_t)blockIdx.x * lda), (short)0, side_fast ? K : 0, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < kSideSteps; j++) {
-      const uint32_t k = (uint32_t)((j * KW + w) * s_S + s_g);
-      s_c[j] = __builtin_amdgcn_raw_buffer_load_b8(sar, k, 0, 0);
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(sxr, k * side.ldx + (uint32_t)s_li * 16u, 0, 0);
-      s_x[j] = make_uint4(v[0], v[1], v[2], v[3]);
+    for (int j = 0; j < kSideUnits; j++) {
+      const bool on = side_fast && j < s_nu;
+      const int u = s_u0 + j, row = on ? u / s_n16 : 0, col = on ? (u - row * s_n16) * 16 + s_d * 4 : 0;
+      const __amdgpu_buffer_rsrc_t xr2 = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)side.x, (short)0, on ? (int)((uint32_t)K * side.ldx) : 0, 0x00020000);
+      const __amdgpu_buffer_rsrc_t ar2 = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(A + (size_t)row * lda), (short)0, on ? K : 0, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < kSidePass; p++) {
+        const uint32_t k = (uint32_t)(s_kt + p * 16 * KW);
+        s_c[j][p] = __builtin_amdgcn_raw_buffer_load_b8(ar2, k, 0, 0);
+        s_x[j][p] = __builtin_amdgcn_raw_buffer_load_b32(xr2, k * side.ldx + (uint32_t)col, 0, 0);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the ring loads
   }
@@ -574,24 +518,28 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
 #endif
   if constexpr (SIDE) {
     if (side_fast) {
-      uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int j = 0; j < kSideSteps; j++) {
-        uint4 t01;
-        uint32_t t2;
-        gf_make_tables(s_c[j], t01, t2);
-        acc[0] = gf_mul_acc4(acc[0], s_x[j].x, t01, t2);
-        acc[1] = gf_mul_acc4(acc[1], s_x[j].y, t01, t2);
-        acc[2] = gf_mul_acc4(acc[2], s_x[j].z, t01, t2);
-        acc[3] = gf_mul_acc4(acc[3], s_x[j].w, t01, t2);
+      for (int j = 0; j < kSideUnits; j++) {
+        if (j < s_nu) {
+          uint32_t acc = 0;
+#pragma unroll
+          for (int p = 0; p < kSidePass; p++) {
+            if (p < s_np) {  // row steps past K: nothing to add
+              uint4 t01;
+              uint32_t t2;
+              gf_make_tables(s_c[j][p], t01, t2);
+              acc = gf_mul_acc4(acc, s_x[j][p], t01, t2);
+            }
+          }
+          acc = side_fold16(acc);
+          if (lane < 4) side_part[(j * KW + w) * 4 + lane] = acc;
+        }
       }
-      side_lane_fold(acc, s_S);
-      if (lane < s_GL) side_part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
     }
   }
+  // (the stores wait for the block's own: a store before the main loop
+  // would make the compiler wait for it, vmcnt(0), at the loop's asm)
   __syncthreads();
-  if constexpr (SIDE)
-    if (side_fast && tid < s_GL) side_store(side_part, KW, side, blockIdx.x, s_li * 16, tid);
 
   const uint32_t ngrp = __builtin_amdgcn_readfirstlane((uint32_t)(nr / kBsChunk));
   const uint64_t xa = reinterpret_cast<uint64_t>(X);
@@ -723,30 +671,9 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     }
   }
   if constexpr (SIDE) {
-    if (side_staged) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const uint8_t* al = reinterpret_cast<const uint8_t*>(side_a);
-      const uint4* cl = reinterpret_cast<const uint4*>(side_c);
-      uint32_t acc[4] = {0u, 0u, 0u, 0u};
-      for (int k = w * s_S + s_g; k < K; k += KW * s_S) {
-        const uint4 x = s_li < s_P16 ? cl[k * s_P16 + s_li] : make_uint4(0u, 0u, 0u, 0u);
-        uint4 t01;
-        uint32_t t2;
-        gf_make_tables(al[k], t01, t2);
-        acc[0] = gf_mul_acc4(acc[0], x.x, t01, t2);
-        acc[1] = gf_mul_acc4(acc[1], x.y, t01, t2);
-        acc[2] = gf_mul_acc4(acc[2], x.z, t01, t2);
-        acc[3] = gf_mul_acc4(acc[3], x.w, t01, t2);
-      }
-      side_lane_fold(acc, s_S);
-      if (lane < s_GL) side_part[w * 64 + lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-      __syncthreads();
-      if (tid < s_GL) side_store(side_part, KW, side, blockIdx.x, s_li * 16, tid);
-    }
-    const bool first_done = side_fast || side_staged;
-    if (side.ncols > 0 && (!first_done || (int)blockIdx.x + (int)gridDim.x < M))
-      bs_side_rest<KW>(A, lda, M, K, side, side_part, first_done);
+    if (side_fast && tid < 4 * s_nu)  // the prologue's sums, still in LDS
+      side_store_dword(side_part + (tid >> 2) * KW * 4, KW, side, s_n16, s_u0 + (tid >> 2), tid & 3);
+    if (side.ncols > 0 && !side_fast) bs_side_rest<KW>(A, lda, K, side, side_part, s_u0, s_u1);
   }
   if constexpr (MODE == 8) {  // timeline build: stamps past the M output rows (the caller sizes Y)
     __syncthreads();
@@ -949,15 +876,6 @@ bool bs_direct_allowed() {
 
 }  // namespace
 
-size_t ncols_side_units(int ncols) { return ((size_t)ncols + 15) / 16; }
-
-// KODR_SIDE_STAGE=1: stage the side inputs in LDS where the plan has one
-// workgroup per CU (A/B; the register path otherwise)
-bool side_stage_enabled() {
-  static const bool v = getenv("KODR_SIDE_STAGE") ? atoi(getenv("KODR_SIDE_STAGE")) != 0 : false;
-  return v;
-}
-
 bool side_ok(const BsSide& sd, size_t K) {
   return sd.x && sd.y && (uintptr_t)sd.x % 16 == 0 && (uintptr_t)sd.y % 16 == 0 && sd.ldx % 16 == 0 &&
          sd.ldy % 16 == 0 && sd.ldx >= (sd.ncols + 15) / 16 * 16 && sd.ldy >= sd.ncols && K * sd.ldx < ((size_t)1 << 31) &&
@@ -1004,7 +922,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   BsSideK sk{};
   if (side && side->ncols) {
     if (group || accumulate || !side_ok(*side, K)) return hipErrorInvalidValue;
-    sk = BsSideK{side->x, side->y, (uint32_t)side->ldx, (uint32_t)side->ldy, (int)side->ncols, 0};
+    sk = BsSideK{side->x, side->y, (uint32_t)side->ldx, (uint32_t)side->ldy, (int)side->ncols};
   }
   if (ldx % kBsBlock || ldy % 16 || (size_t)K * ldx >= ((size_t)1 << 32) || ldx > 0x7fffffff ||
       lda > 0x7fffffff || M > 0x7fffffff)
@@ -1020,18 +938,9 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     p.lds_bytes = bs_lds_bytes(kw, p.rpw);
   }
 #endif
-  size_t side_lds = 0;
-  if (sk.ncols) {
-    side_lds = (size_t)p.kw * 64 * 16;
-    // staged side inputs when one workgroup holds the CU anyway (KW = 16)
-    const size_t staged = 1024 + (K * ((ncols_side_units(sk.ncols)) * 16) + 1023) / 1024 * 1024;
-    if (p.kw == 16 && side_stage_enabled() && K <= 1024 && sk.ncols <= 1024 &&
-        p.lds_bytes + side_lds + staged <= kLdsPerCu) {
-      sk.stage = 1;
-      side_lds += staged;
-    }
-    if (p.lds_bytes + side_lds > kLdsPerCu) return hipErrorInvalidValue;
-  }
+  // the side product's partial sums: kSideUnits x KW dwords x 4
+  const size_t side_lds = sk.ncols ? (size_t)kSideUnits * p.kw * 16 : 0;
+  if (p.lds_bytes + side_lds > kLdsPerCu) return hipErrorInvalidValue;
   const BsDevice* bd = nullptr;
   hipError_t e = bs_init(device, &bd);
   if (e != hipSuccess) return e;

@@ -17,10 +17,12 @@ __device__ __forceinline__ void gf_make_tables(uint32_t c, uint4& t01, uint32_t&
   const uint32_t c16 = gf_xt(c8), c32 = gf_xt(c16), c64 = gf_xt(c32), c128 = gf_xt(c64);
   const uint32_t lo0 = (c1 << 8) | (c2 << 16) | ((c1 ^ c2) << 24);
   const uint32_t lo1 = (c8 << 8) | (c16 << 16) | ((c8 ^ c16) << 24);
+  // byte broadcasts by v_perm (selector 0: byte 0 of the second source in
+  // every byte), not a quarter-rate 32-bit multiply
   t01.x = lo0;
-  t01.y = lo0 ^ (c4 * 0x01010101u);
+  t01.y = lo0 ^ __builtin_amdgcn_perm(0u, c4, 0u);
   t01.z = lo1;
-  t01.w = lo1 ^ (c32 * 0x01010101u);
+  t01.w = lo1 ^ __builtin_amdgcn_perm(0u, c32, 0u);
   t2 = (c64 << 8) | (c128 << 16) | ((c64 ^ c128) << 24);
 }
 

@@ -15,7 +15,7 @@ for d in sys.argv[1:]:
         continue
     c = collections.defaultdict(list)
     for r in csv.DictReader(open(f[0])):
-        name = r["Kernel_Name"].split("(")[0].replace("void kodr_amd::(anonymous namespace)::", "")
+        name = r["Kernel_Name"].replace("void ", "").replace("kodr_amd::(anonymous namespace)::", "").split("(")[0]
         c[(name, r["Grid_Size_X"], r["Grid_Size_Y"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {f"{k[0]} grid {k[1]}x{k[2]}": {"n": len(v), "median_us": round(statistics.median(v), 2)}
            for k, v in sorted(c.items(), key=lambda kv: -sum(kv[1]))[:8]}
