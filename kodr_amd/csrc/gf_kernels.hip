@@ -293,12 +293,16 @@ __global__ __launch_bounds__(64 * KW) void gf_gemm_kernel(
 // and all K rows, split over KW waves of RPW rows; the coefficient and then
 // every row load of a wave are issued before anything else.  Unlike
 // gf_gemm_kernel there are no LDS tables and no barrier before the first
-// multiply: each lane builds the tables of all its rows in registers from the
-// coefficients while the rows are in flight, so a step costs only its
-// multiply once its row lands, and the tail after the last row is short.
+// multiply: the tables are built in registers from the coefficients while the
+// rows are in flight (SHT: lane r for row r, fetched per step by ds_bpermute),
+// so a step costs only its multiply once its row lands, and the tail after
+// the last row is short.
 // Partial sums: lane groups by v_permlane16/32_swap, waves through one LDS
 // slot each and a single barrier (no atomics, nothing to zero).
-template <int KW, int RPW, int S, int AUX = 0>
+// SHT: the tables are built once per row, by the lane that holds the row's
+// coefficient, and each lane group fetches its row's five table dwords with
+// ds_bpermute (5 crossbar reads per step instead of ~45 VALU per row per lane).
+template <int KW, int RPW, int S, int AUX = 0, bool SHT = false>
 __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restrict__ A, int K,
                                                           const uint8_t* __restrict__ X, size_t ldx,
                                                           uint8_t* __restrict__ Y, int ncols, int accum) {
@@ -325,13 +329,32 @@ __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restr
   __builtin_amdgcn_sched_barrier(0);
   uint4 t01[STEPS];
   uint32_t t2[STEPS];
+  if constexpr (SHT) {
+    uint4 m01;
+    uint32_t m2;
+    gf_make_tables(cv, m01, m2);  // lane r: row r0 + r (zero tables past K and RPW)
 #pragma unroll
-  for (int j = 0; j < STEPS; j++) {
-    uint32_t c = __builtin_amdgcn_readlane(cv, S * j);
+    for (int j = 0; j < STEPS; j++) {
+      const int src = (S * j + g) * 4;  // byte address of the lane holding row S j + g
+      t01[j].x = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01.x);
+      t01[j].y = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01.y);
+      t01[j].z = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01.z);
+      t01[j].w = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01.w);
+      t2[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m2);
+    }
+  } else {
 #pragma unroll
-    for (int q = 1; q < S; q++) c = g == q ? __builtin_amdgcn_readlane(cv, S * j + q) : c;
-    gf_make_tables(c, t01[j], t2[j]);
+    for (int j = 0; j < STEPS; j++) {
+      uint32_t c = __builtin_amdgcn_readlane(cv, S * j);
+#pragma unroll
+      for (int q = 1; q < S; q++) c = g == q ? __builtin_amdgcn_readlane(cv, S * j + q) : c;
+      gf_make_tables(c, t01[j], t2[j]);
+    }
   }
+  // every table before the first row wait: otherwise the scheduler mixes the
+  // first steps' multiplies into the table build and waits for rows 0 and 1
+  // before building the rest (~400 VALU on the critical path)
+  __builtin_amdgcn_sched_barrier(0);
   uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int j = 0; j < STEPS; j++) {
@@ -649,12 +672,13 @@ static bool env_config(GemmConfig* g) {
   return sscanf(s, "%d,%d,%d,%d", &g->mt, &g->kw, &g->s, &g->p) >= 3;
 }
 
-// One-row products of 129..256 input rows take gf_gemv_kernel with two lane
-// groups: 8.5 us per 32 MiB/256 coded piece in rocprof against 9.4 on
-// gf_gemm_kernel<1, 16, 2> (profiles/r03/b1/); four lane groups (256-byte
-// chunks, two workgroups per CU) measured 9.4.  KODR_GEMV=0/2/4 selects
-// gf_gemm_kernel / 2 / 4 lane groups, 3 two lane groups with non-temporal
-// row loads (A/B measurements).
+// One-row products of 129..256 input rows take gf_gemv_kernel (two lane
+// groups, tables shared through ds_bpermute): 7.56 us per 32 MiB/256 coded
+// piece in rocprof against 8.20 with per-lane tables and 9.4 on
+// gf_gemm_kernel<1, 16, 2> (profiles/r03/b1/, profiles/r03/gemv_ab/); 512
+// workgroups of 8 waves (four lane groups) or 256 of 8 waves (16 rows in
+// flight per lane) measured 7.88 / 8.80.  KODR_GEMV=0 selects gf_gemm_kernel,
+// 1 the per-lane tables (A/B measurements).
 static int gemv_enabled() {
   static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 2;
   return v;
@@ -672,17 +696,14 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   if (M == 1 && !grp && !force && K > (size_t)kGemvKW * kGemvRPW / 2 && K <= (size_t)kGemvKW * kGemvRPW &&
       ncols >= 16384 &&
       (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv) {
-    const int S = gemv == 4 ? 4 : 2, nx = (int)((ncols + 1024 / S - 1) / (1024 / S));
-    if (S == 4)
-      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 4>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
-                         dX, ldx, dY, (int)ncols, acc);
-    else if (gemv == 3)
-      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2, 2>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA,
-                         (int)K, dX, ldx, dY, (int)ncols, acc);
-    else
+    const int nx = (int)((ncols + 511) / 512);
+    if (gemv == 1)
       hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA, (int)K,
                          dX, ldx, dY, (int)ncols, acc);
-    last_launch_plan() = LaunchPlan{3, 1, kGemvKW, S, kGemvRPW / S, kGemvRPW, 1, nx};
+    else
+      hipLaunchKernelGGL((gf_gemv_kernel<kGemvKW, kGemvRPW, 2, 0, true>), dim3(nx), dim3(64 * kGemvKW), 0, stream, dA,
+                         (int)K, dX, ldx, dY, (int)ncols, acc);
+    last_launch_plan() = LaunchPlan{3, 1, kGemvKW, 2, kGemvRPW / 2, kGemvRPW, 1, nx};
     return hipGetLastError();
   }
   GemmConfig g = force ? *force : grp ? choose_group_config(M, K, ncols, (size_t)grp->n)

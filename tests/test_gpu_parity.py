@@ -175,6 +175,35 @@ def test_gf_matmul_few_rows_wide_vs_oracle(gpu_ctx, M, K, ncols):
     assert (Y[:, ncols:] == 0xA5).all(), "wrote past ncols"
 
 
+@pytest.mark.parametrize("K,ncols", [(129, 16384), (200, 65536 + 16), (256, 131072), (256, 131072 + 48),
+                                     (255, 40000 + 7)])
+def test_gf_gemv_vs_oracle(gpu_ctx, K, ncols):
+    # one coded piece of a wide generation (M = 1, 129..256 rows, >= 16 KiB
+    # rows): the streaming gf_gemv_kernel (plan kernel 3), bit-exact with zero
+    # coefficients, ragged columns, nothing written past ncols
+    rng = np.random.default_rng(K * 131 + ncols)
+    ld = (ncols + 255) // 256 * 256
+    A = rng.integers(0, 256, (1, K), dtype=np.uint8)
+    A[0, rng.random(K) < 0.2] = 0
+    X = np.zeros((K, ld), np.uint8)
+    X[:, :ncols] = rng.integers(0, 256, (K, ncols), dtype=np.uint8)
+    dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(X.nbytes), gpu_ctx.alloc(ld)
+    try:
+        gpu_ctx.h2d(dA, A)
+        gpu_ctx.h2d(dX, X)
+        gpu_ctx.h2d(dY, np.full(ld, 0xA5, np.uint8))
+        errors.check(_lib.lib().rlnc_gf_matmul_device(gpu_ctx.handle, dA, K, 1, K, dX, ld, dY, ld, ncols))
+        plan = _lib.last_launch_plan()
+        Y = gpu_ctx.d2h(dY, ld)
+    finally:
+        for p in (dA, dX, dY):
+            gpu_ctx.free(p)
+    assert plan["kernel"] == 3, plan
+    _, ref = oracle.matmul(A, X[:, :ncols])
+    assert np.array_equal(Y[:ncols], ref[0]), (K, ncols)
+    assert (Y[ncols:] == 0xA5).all(), "wrote past ncols"
+
+
 def test_c2_encode_batch_full_compare(gpu_ctx):
     # BASELINE config 2: 32 MiB / 256 pieces, 8 coded pieces compared in full
     rng = np.random.default_rng(0x6B6F6472)

@@ -1,7 +1,7 @@
 """One coded piece per launch at 32 MiB/256 (B = 1, rlnc_encoder_coded_pieces_device),
 16 rotating prepared generations (HBM-cold), HIP events over back-to-back
 launches, median of reps; the piece is checked against the oracle.  Run with
-KODR_GEMV=0/1 for the A/B of gf_gemv_kernel against gf_gemm_kernel."""
+KODR_GEMV=0 (gf_gemm_kernel) / 1 (per-lane tables) / 2 (default, shared tables) for A/B."""
 import ctypes
 import json
 import os
