@@ -170,6 +170,19 @@ def body_lines(c, r=0):
     return out
 
 
+def body_inline(c, m):
+    """Body of coefficient c straight into row m's accumulators, no jump (the
+    tuning loop INLINE: the dispatch-free bound of the real kernel)."""
+    out = []
+    for j, lo, hi in body_ops(c):
+        a = ACC + 8 * m + j
+        if lo and hi:
+            out.append(f"v_bitop3_b32 v{a}, v{a}, v{tl(lo)}, v{th(hi)} bitop3:0x96")
+        else:
+            out.append(f"v_xor_b32_e32 v{a}, v{a}, v{tl(lo) if lo else th(hi)}")
+    return out
+
+
 def body_bytes(c):
     # v_bitop3 (VOP3) 8 bytes, v_xor_b32_e32 (VOP2) 4, s_setpc_b64 4
     return sum(8 if lo and hi else 4 for _j, lo, hi in body_ops(c)) + 4
@@ -224,7 +237,7 @@ def ROW_PRIO(j):
     return j % 4
 
 
-def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False):
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
@@ -250,7 +263,10 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
     if not sload:
         t += [f"v_readlane_b32 s{row_target(m)}, v{PG}, {8 * j + m}"
               for m in range(NCOPY, 8)] * (2 if "readlane" in twice else 1)
-    if dispatch:
+    if inline is not None:  # tuning: every output row's body inlined for the fixed coefficient `inline`
+        for m in range(8):
+            t += body_inline(inline, m)
+    elif dispatch:
         C = NCOPY
         if half_prio:  # this row's own stub, which sets the second half's priority
             assert C == 4
@@ -319,7 +335,7 @@ def prologue_lines(dispatch=True, sload=False):
     return pro
 
 
-def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
@@ -332,7 +348,7 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()
                 t += stub_lines(f"stub{j}", half_prio(j))
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads, prio, half_prio, twice, sload)
+        t += row_lines(j, dispatch, loads, prio, half_prio, twice, sload, inline)
     if not sload:
         t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
               f"v_add_u32_e32 v{PL}, 256, v{PL}"]
@@ -533,6 +549,9 @@ def main():
     p0 = P
     set_ring(2)
     out += emit("KODR_BS_MAIN_P2", main_loop(True))
+    # tuning (MODE 30): the grouped two-row loop with every body inlined for
+    # one coefficient (19: eight XOR3s) -- no jumps, wrong products
+    out += emit("KODR_BS_MAIN_P2_INLINE", main_loop(True, inline=19))
     ops2 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
     out.append("#define KODR_BS_RING_OPERANDS_P2 " + ", ".join(ops2))
     clob2 = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, VMAX))]
