@@ -12,6 +12,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <chrono>
 #include <new>
 #include <string>
 #include <vector>
@@ -19,11 +20,13 @@
 #include "../../include/kodr_rlnc.h"
 #include "decoder_core.hpp"
 #include "host_gf.hpp"
+#include "host_pool.hpp"
 #include "gf_kernels.hpp"
 #include "pool.hpp"
 #include "staging.hpp"
 
 using kodr_amd::DecoderCore;
+using kodr_amd::HostPool;
 
 namespace {
 
@@ -96,6 +99,8 @@ struct rlnc_ctx {
   DevBuf elim_out;           // gf_elim's per-generation states and counts
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
+  hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
+  hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
 };
 
 struct rlnc_encoder {
@@ -462,6 +467,11 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->elim_out.release();
   ctx->gtmat[0].release();
   ctx->gtmat[1].release();
+  if (ctx->side) {
+    (void)hipStreamSynchronize(ctx->side);
+    (void)hipStreamDestroy(ctx->side);
+    (void)hipEventDestroy(ctx->side_done);
+  }
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return RLNC_OK;
@@ -1684,6 +1694,20 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
 
 namespace {
 
+// KODR_ADD_SIDE=0 keeps the batched AddPiece's row copies on the context
+// stream ahead of the elimination (A/B)
+bool add_side_stream() {
+  static const bool v = getenv("KODR_ADD_SIDE") ? atoi(getenv("KODR_ADD_SIDE")) != 0 : true;
+  return v;
+}
+
+int ctx_side(rlnc_ctx* ctx) {
+  if (ctx->side) return RLNC_OK;
+  HIPC(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  HIPC(hipEventCreateWithFlags(&ctx->side_done, hipEventDisableTiming));
+  return RLNC_OK;
+}
+
 // the field tables gf_elim reads (uploaded once per context)
 int ctx_elim_tables(rlnc_ctx* ctx) {
   if (ctx->elim_tab_ok) return RLNC_OK;
@@ -1715,6 +1739,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(ctx));
+  static const int timing = getenv("KODR_ADD_TIMING") ? atoi(getenv("KODR_ADD_TIMING")) : 0;
+  const auto tnow = [] { return std::chrono::duration<double, std::micro>(
+                             std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double tt0 = timing ? tnow() : 0;
+  double tt1 = 0, tt2 = 0, tt3 = 0;
   // GPU elimination for fresh decoders with >= 2 rows (kElimMaxGens per
   // launch); every other decoder takes rlnc_decoder_add_pieces
   std::vector<size_t> gpu;
@@ -1732,7 +1761,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     gpu.push_back(g);
   }
   // the deferred row copies: one launch per kCopyGroupMax decoders (one piece
-  // length, so one pitch)
+  // length, so one pitch).  With a side stream they run beside the
+  // elimination, launched after it so that its workgroups get their CUs
+  // first; the context stream waits for them before anything later.
+  const bool side = !defer.empty() && !gpu.empty() && add_side_stream();
+  if (side) TRY(ctx_side(ctx));
+  auto launch_copies = [&]() -> int {
   for (size_t c0 = 0; c0 < defer.size(); c0 += kodr_amd::kCopyGroupMax) {
     const size_t nc = std::min<size_t>(kodr_amd::kCopyGroupMax, defer.size() - c0);
     kodr_amd::CopyGroup cg = {};
@@ -1743,8 +1777,18 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       cg.dbs[i] = defer[c0 + i].dbs;
       cg.rows[i] = (int)defer[c0 + i].rows;
     }
-    HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len, ctx->stream));
+    HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len,
+                                              side ? ctx->side : ctx->stream));
   }
+  return RLNC_OK;
+  };
+  if (side) {
+    HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the rows' producer work, ordered before the copies
+    HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
+  } else {
+    TRY(launch_copies());
+  }
+  if (timing) tt1 = tnow();
   if (gpu.empty()) return RLNC_OK;
   // full batches first: launches of full batches only take the blocked kernel
   std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return counts[g] >= k; });
@@ -1772,6 +1816,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
     a.k = (int)k;
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
+    if (side && c0 == 0) {
+      TRY(launch_copies());
+      HIPC(hipEventRecord(ctx->side_done, ctx->side));
+      HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
+    }
+    if (timing) tt2 = tnow();
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
     // back (one 2D copy: the generations' rows are evenly strided), else the
     // whole states
@@ -1796,13 +1846,22 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       for (size_t i = 0; i < nc; i++) memset(hostp + i * sizeof(int), 0, sizeof(int));
     }
 #endif
+    if (timing) tt3 = tnow();
     const int* cnt = reinterpret_cast<const int*>(hostp);
-    for (size_t i = 0; i < nc; i++) {
-      const size_t g = gpu[c0 + i];
-      rlnc_decoder* d = ds[g];
+    // the states into the decoders' host mirrors: independent per decoder,
+    // memory-bound (a 256 x 520-byte arena each), so spread over host threads
+    std::vector<size_t> got(nc);
+    HostPool::get().run(nc, [&](size_t i) {
+      rlnc_decoder* d = ds[gpu[c0 + i]];
       size_t c = (size_t)std::max(cnt[i], 0);
       if (c && tonly && !(c == k && d->core.load_inverse(hostp + hdr + i * k * k, k))) c = 0;
       if (c && !tonly && !d->core.load_rref(hostp + hdr + i * ostride, opitch, c)) c = 0;
+      got[i] = c;
+    });
+    for (size_t i = 0; i < nc; i++) {
+      const size_t g = gpu[c0 + i];
+      rlnc_decoder* d = ds[g];
+      const size_t c = got[i];
       // the rest of the batch (past a row off its diagonal, or past k) through
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;
@@ -1825,6 +1884,9 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       status[g] = pst != RLNC_OK ? pst : st;
     }
   }
+  if (timing)
+    fprintf(stderr, "add_pieces_gpu G=%zu side=%d: pre+copies %.1f us, elim launch %.1f, wait+read-back %.1f, "
+            "host post %.1f\n", G, (int)side, tt1 - tt0, tt2 - tt1, tt3 - tt2, tnow() - tt3);
   return RLNC_OK;
 }
 
@@ -1953,18 +2015,23 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
     const size_t n = std::min(kGroupGetChunk, G - g0);
     bool grouped = n > 1;
     for (size_t i = 0; i < n && grouped; i++) {
-      rlnc_decoder* d = ds[g0 + i];
+      const rlnc_decoder* d = ds[g0 + i];
       grouped = d->core.received() == recv && d->core.rank() == rows && d->pitch == pitch;
-      if (!grouped) break;
-      uint8_t* t = hT.data() + i * tsz;
-      d->core.copy_transform(t, recv);
-      for (size_t r = 0; r < rows && grouped; r++, t += recv) {  // a unit row is a copy: per-decoder route
-        size_t nz = 0, last = 0;
-        for (size_t j = 0; j < recv && nz < 2; j++)
-          if (t[j]) nz++, last = j;
-        grouped = !(nz == 1 && t[last] == 1);
-      }
     }
+    // the transforms, one decoder per host task (disjoint slices of hT)
+    std::vector<uint8_t> unit(n, 0);
+    if (grouped)
+      HostPool::get().run(n, [&](size_t i) {
+        uint8_t* t = hT.data() + i * tsz;
+        ds[g0 + i]->core.copy_transform(t, recv);
+        for (size_t r = 0; r < rows && !unit[i]; r++, t += recv) {  // a unit row is a copy: per-decoder route
+          size_t nz = 0, last = 0;
+          for (size_t j = 0; j < recv && nz < 2; j++)
+            if (t[j]) nz++, last = j;
+          unit[i] = nz == 1 && t[last] == 1;
+        }
+      });
+    for (size_t i = 0; i < n && grouped; i++) grouped = !unit[i];
     if (!grouped) {
       for (size_t i = 0; i < n; i++)
         TRY(rlnc_decoder_get_pieces_device(ds[g0 + i], d_out + (g0 + i) * ostride, out_pitch));
