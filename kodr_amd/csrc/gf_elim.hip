@@ -510,6 +510,174 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_blocked_kernel(ElimAr
 }
 
 
+// ---- FULL batches, blocked, one dword per lane: the "circular" row -------
+// The same panels as gf_elim_blocked_kernel, on half the bytes.  At any panel
+// boundary a row's coefficient byte s and its T byte s are never both in
+// play except where the row's own identity sits: coefficient columns [0, jb)
+// are eliminated (zero) exactly where T columns [0, jb) can be non-zero, and
+// an unpicked row j has T = e_j + (columns < jb).  So slot s (s < k) holds
+// coefficient[s] XOR T[s], 64 lanes x 4 slots cover k <= 256 (against
+// 2 dwords per lane for [C | T] at k > 128), and every step stays linear:
+//  * a candidate's panel block is its slots with its identity XORed out;
+//  * a new pivot row N[c] = S x (candidate rows) is the same combination of
+//    slots (coefficient part e_(jb+c) + columns >= jb + 16, T part columns
+//    < jb + 16, both in the panel's slots);
+//  * a non-candidate row's panel slots are pure coefficients (its T is zero
+//    there), so its multipliers read as before, and row ^= sum f_c N[c]
+//    leaves 0 ^ T in those slots: f_c ^ f_c from N's identity.
+// At the end the pivot row of column col holds e_col ^ T: T is its slots
+// with byte col flipped.  The output is the blocked kernel's: [I | C^-1] at
+// out_pitch, T from byte k.
+__global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs args) {
+  __shared__ ElimBlkLds lds;
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = args.k;
+  const int j0 = w * kElimRowsPerWave;
+  const uint8_t* vec = args.vecs[g];
+  const size_t vp = args.vpitch;
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  cu32* tb = (cu32*)args.tables;
+
+  for (int i = tid; i < 256 * 2; i += 64 * kElimWaves)
+    lds.tab[i] = make_uint4(args.tables[4 * i], args.tables[4 * i + 1], args.tables[4 * i + 2], args.tables[4 * i + 3]);
+  for (int i = tid; i < 256; i += 64 * kElimWaves) lds.colof[i] = -1;
+  if (tid == 0) lds.fail = 0;
+
+  // slots of rows j0 .. j0 + 15: C[j] ^ e_j (slots >= k zero)
+  uint32_t R[kElimRowsPerWave];
+#pragma unroll
+  for (int i = 0; i < kElimRowsPerWave; i++) {
+    const int j = j0 + i;
+    uint32_t v = 0;
+    if (j < k) {
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int col = lane * 4 + b;
+        uint32_t byte = col < k ? vec[(size_t)j * vp + col] : 0u;
+        if (col == j) byte ^= 1u;
+        v |= byte << (8 * b);
+      }
+    }
+    R[i] = v;
+  }
+  __syncthreads();
+
+  const int npanels = (k + 15) / 16;
+  for (int pb = 0; pb < npanels; pb++) {
+    const int jb = pb * 16, nb = min(16, k - jb);
+    const int pl0 = jb >> 2;  // lane of the panel's first slot
+    if (w == pb) {
+      // ---- 1. the owner: old rows out, panel block (identity removed) inverted ----
+#pragma unroll
+      for (int i = 0; i < kElimRowsPerWave; i++) {
+        lds.prow[i][lane] = R[i];
+        if (lane >= pl0 && lane < pl0 + 4) {
+          uint32_t blk = R[i];
+          if (i < nb && lane == pl0 + (i >> 2)) blk ^= 1u << (8 * (i & 3));  // row jb + i's own T byte
+          lds.pan[i][lane - pl0] = blk;
+        }
+      }
+      panel_gj(lds, jb, nb, tb, lane);
+    }
+    __syncthreads();
+    if (lds.fail) break;  // uniform
+    // ---- 2. the new pivot rows: one (panel column, slot dword) per thread ----
+    {
+      const int c = __builtin_amdgcn_readfirstlane(tid >> 6), dw = lane;
+      if (c < nb) {
+        uint32_t acc = 0;
+        for (int u4 = 0; u4 < 4; u4++) {
+          const uint32_t sw = __builtin_amdgcn_readfirstlane(lds.sd[c][u4]);
+          uint32_t x[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) x[e] = lds.prow[4 * u4 + e][dw];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const uint32_t su = (sw >> (8 * e)) & 0xffu;
+            const uint4 ts = {tb[su * 8], tb[su * 8 + 1], tb[su * 8 + 2], tb[su * 8 + 3]};
+            const uint32_t ts2 = tb[su * 8 + 4];
+            acc ^= gmul4(ts, ts2, sel0(x[e]), sel1(x[e]), sel2(x[e]));
+          }
+        }
+        lds.np[c][dw] = acc;
+      }
+    }
+    __syncthreads();
+    // ---- 3. the owner's rows become the pivot rows, the others drop the panel ----
+    if (w == pb) {
+#pragma unroll
+      for (int i = 0; i < kElimRowsPerWave; i++)
+        if (i < nb) {
+          const int c = __builtin_amdgcn_readfirstlane(lds.colof[jb + i]) - jb;
+          R[i] = lds.np[c][lane];
+        }
+    } else if (j0 < k) {
+      // every multiplier first: N[c]'s panel slots carry T bytes, so applying
+      // N[c] changes the row's later panel slots (unlike [C | T], where they
+      // hold the zero coefficients of N's identity block)
+      uint32_t F[kElimRowsPerWave][4];
+#pragma unroll
+      for (int i = 0; i < kElimRowsPerWave; i++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) F[i][q] = __builtin_amdgcn_readlane(R[i], pl0 + q);
+      // (all 16 columns, unrolled, so that F is indexed by constants only and
+      // stays in registers; past nb, in the last panel, every multiplier is
+      // a slot >= k, zero in every row, so the stale N[c] adds nothing)
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const uint32_t x = lds.np[c][lane];
+        const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+        const int qd = c >> 2, qs = 8 * (c & 3);
+        auto fetch = [&](int i, uint4& t, uint32_t& t2) {
+          const uint32_t f = (F[i][qd] >> qs) & 0xffu;
+          t = lds.tab[2 * f];
+          t2 = lds.tab[2 * f + 1].x;
+        };
+        uint4 ta, tb1, tn;
+        uint32_t ta2, tb2, tn2;
+        fetch(0, ta, ta2);
+        fetch(1, tb1, tb2);
+#pragma unroll
+        for (int i = 0; i < kElimRowsPerWave; i++) {
+          if (i + 2 < kElimRowsPerWave) fetch(i + 2, tn, tn2);
+          const uint32_t p0 = __builtin_amdgcn_perm(ta.y, ta.x, s0);
+          const uint32_t p1 = __builtin_amdgcn_perm(ta.w, ta.z, s1);
+          const uint32_t p2 = __builtin_amdgcn_perm(ta2, ta2, s2);
+          R[i] = __builtin_amdgcn_bitop3_b32(R[i], p0, p1, 0x96) ^ p2;
+          ta = tb1;
+          ta2 = tb2;
+          tb1 = tn;
+          tb2 = tn2;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int c = lds.fail ? 0 : k;
+  uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+  if (c) {
+#pragma unroll
+    for (int i = 0; i < kElimRowsPerWave; i++) {
+      const int j = j0 + i;
+      if (j >= k) continue;
+      const int at = lds.colof[j];
+      uint8_t* row = out + (size_t)at * args.out_pitch;
+      uint32_t e = 0;  // e_at in this lane's 4 slots
+      if (at >= 4 * lane && at < 4 * lane + 4) e = 1u << (8 * (at - 4 * lane));
+      const uint32_t t = R[i] ^ e;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * lane + b < k) {
+          row[4 * lane + b] = (uint8_t)(e >> (8 * b));      // [I]
+          row[k + 4 * lane + b] = (uint8_t)(t >> (8 * b));  // [C^-1]
+        }
+    }
+  }
+  if (tid == 0) args.counts[g] = c;
+}
+
 }  // namespace
 
 void elim_tables(uint32_t* host_out) {
@@ -574,7 +742,10 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   // (a row-per-lane layout of the same algorithm -- one LDS gather per
   // multiplier serving 64 rows, pivot rows as scalars -- measured slower too:
   // 536 vs 493 us at k = 256, profiles/r02/elim/elim_rows_ab.log)
-  if (full && args.k <= 128)
+  static const bool circ = getenv("KODR_ELIM_CIRC") ? atoi(getenv("KODR_ELIM_CIRC")) != 0 : true;
+  if (full && circ)
+    hipLaunchKernelGGL(gf_elim_circ_kernel, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
+  else if (full && args.k <= 128)
     hipLaunchKernelGGL(gf_elim_blocked_kernel<1>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full)
     hipLaunchKernelGGL(gf_elim_blocked_kernel<2>, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
