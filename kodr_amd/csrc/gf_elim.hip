@@ -565,6 +565,20 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
   __syncthreads();
 
   const int npanels = (k + 15) / 16;
+#ifdef KODR_ELIM_TIMING
+  uint64_t tacc[6] = {0, 0, 0, 0, 0, 0};  // owner panel, barrier 1, pivot rows, barrier 2, row update
+  uint64_t tq = __builtin_amdgcn_s_memtime(), tstart = tq;
+#define KODR_STAMP(i)                                 \
+  do {                                                \
+    const uint64_t tn = __builtin_amdgcn_s_memtime(); \
+    tacc[i] += tn - tq;                               \
+    tq = tn;                                          \
+  } while (0)
+#else
+#define KODR_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
   for (int pb = 0; pb < npanels; pb++) {
     const int jb = pb * 16, nb = min(16, k - jb);
     const int pl0 = jb >> 2;  // lane of the panel's first slot
@@ -581,7 +595,9 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
       }
       panel_gj(lds, jb, nb, tb, lane);
     }
+    KODR_STAMP(0);
     __syncthreads();
+    KODR_STAMP(1);
     if (lds.fail) break;  // uniform
     // ---- 2. the new pivot rows: one (panel column, slot dword) per thread ----
     {
@@ -604,7 +620,9 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
         lds.np[c][dw] = acc;
       }
     }
+    KODR_STAMP(2);
     __syncthreads();
+    KODR_STAMP(3);
     // ---- 3. the owner's rows become the pivot rows, the others drop the panel ----
     if (w == pb) {
 #pragma unroll
@@ -632,7 +650,7 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
         const int qd = c >> 2, qs = 8 * (c & 3);
         auto fetch = [&](int i, uint4& t, uint32_t& t2) {
           const uint32_t f = (F[i][qd] >> qs) & 0xffu;
-          t = lds.tab[2 * f];
+          t = lds.tab[2 * f];  // (scalar loads of tb instead: 384 vs 368 us, profiles/r03/elim_circ/)
           t2 = lds.tab[2 * f + 1].x;
         };
         uint4 ta, tb1, tn;
@@ -653,7 +671,18 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
         }
       }
     }
+    KODR_STAMP(4);
   }
+#ifdef KODR_ELIM_TIMING
+  tacc[5] = __builtin_amdgcn_s_memtime() - tstart;
+  if (lane == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(args.out + (size_t)g * args.out_gen_stride) + 8 * w;
+    for (int q = 0; q < 6; q++) o[q] = tacc[q];
+  }
+  if (tid == 0) args.counts[g] = 0;
+  return;
+#endif
+#undef KODR_STAMP
   __syncthreads();
   const int c = lds.fail ? 0 : k;
   uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
@@ -742,7 +771,7 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   // (a row-per-lane layout of the same algorithm -- one LDS gather per
   // multiplier serving 64 rows, pivot rows as scalars -- measured slower too:
   // 536 vs 493 us at k = 256, profiles/r02/elim/elim_rows_ab.log)
-  static const bool circ = getenv("KODR_ELIM_CIRC") ? atoi(getenv("KODR_ELIM_CIRC")) != 0 : true;
+  static const int circ = getenv("KODR_ELIM_CIRC") ? atoi(getenv("KODR_ELIM_CIRC")) : 1;
   if (full && circ)
     hipLaunchKernelGGL(gf_elim_circ_kernel, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full && args.k <= 128)
