@@ -333,7 +333,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(B, k, L, per_step),
-                         "kernel": {1: "gf_gemm_kernel", 2: "gf_bs_kernel"}.get(plan["kernel"], "?"),
+                         "kernel": kernel_name(plan),
                          "plan": plan,
                          "traffic_source": pmc_traffic_file(B, k, L, per_step),
                          "hbm_bytes_per_launch": compulsory,
@@ -363,6 +363,11 @@ def main():
 
 
 WARM_S = 0.08
+
+
+def kernel_name(plan):
+    """The kernel a launch plan names (rlnc_last_launch_plan: the library's last launch)."""
+    return {1: "gf_gemm_kernel", 2: "gf_bs_kernel", 3: "gf_gemv_kernel"}.get(plan["kernel"], "?")
 
 
 def pmc_traffic_file(B, k, L, G=1):
@@ -626,6 +631,7 @@ def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
     resident generations in ONE launch (rlnc_encoder_group_coded_pieces_device,
     gf_gemm_kernel with a generation grid dimension), so the launch and ramp
     are paid once per G x 32 MiB.  HIP events on the context stream."""
+    from kodr_amd._lib import last_launch_plan
     import ctypes
     import numpy as np
     from kodr_amd import device as kdev
@@ -647,7 +653,7 @@ def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
         t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / iters_c
         hbm = G * (k * L + count * (k + L))
         # prepared encoders: the bit-sliced launch from 5 pieces (capi.cpp kGroupBsMinRows)
-        res[str(count)] = {"kernel": "gf_bs_kernel (grouped)" if count >= 5 else "gf_gemm_kernel (grouped)",
+        res[str(count)] = {"kernel": kernel_name(last_launch_plan()) + " (grouped)",
                            "us_per_launch": round(t * 1e6, 2), "us_per_generation": round(t / G * 1e6, 3),
                            "coded_MBps": round(G * count * setbytes(k, L) / t / 1e6, 1),
                            "hbm_GBps": round(hbm / t / 1e9, 1),
@@ -665,6 +671,7 @@ def recode_c2(ctx, L_, errors, enc, k, L, rng, iters=40):
     engine's encoder), B recoded pieces per call, kodr's SetBytes
     (n+1)(k+L) per piece (benches/full/recoder_test.go:53).  The recoder's
     bit-sliced twin is built at construction (rlnc_recoder_prepare)."""
+    from kodr_amd._lib import last_launch_plan
     import ctypes
     import numpy as np
     from kodr_amd import device as kdev
@@ -694,7 +701,7 @@ def recode_c2(ctx, L_, errors, enc, k, L, rng, iters=40):
         ctx.record(e1)
         t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / it
         res[str(b)] = {"us_per_call": round(t * 1e6, 2), "recoded_MBps": round(b * (n + 1) * clen / t / 1e6, 1),
-                       "kernel": "gf_bs_kernel" if b >= 9 else "gf_gemm_kernel"}
+                       "kernel": kernel_name(last_launch_plan())}
     L_.rlnc_recoder_destroy(rh)
     for p in (dW, dR, dO):
         ctx.free(p)
