@@ -421,9 +421,11 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   const int nr = __builtin_amdgcn_readfirstlane(max(0, min(rpw, kpad - kb)));
 
   // Prologue loads in retirement order (vmcnt counts in issue order): the
-  // target table and this wave's first 512 coefficients, then the ring's
-  // first rows, so the program build waits only for the former while the
-  // rows' HBM latency overlaps it.
+  // target table and this wave's coefficients (all of them up to K = 256:
+  // kPre per lane), then the ring's first rows, so the program build waits
+  // only for the former while the rows' HBM latency overlaps it.  (With 8
+  // per lane, a one-wave task of 256 rows loaded the rest in three more
+  // rounds, each behind the ring's rows in the vmcnt order.)
   const int ne = nr * kBsRows;
   auto coef = [&](int e) -> uint32_t {
     const int k = kb + (e >> 3), row = m0 + (e & 7);
@@ -436,9 +438,10 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     const int i = tid + j * 64 * KW;
     ot[j] = i < kTgt ? tgt[i] : 0u;
   }
-  uint32_t c[8];
+  constexpr int kPre = KW == 1 ? 32 : KW == 2 ? 16 : KW == 3 ? 12 : 8;  // ceil(256 / KW) rows x 8 / 64 lanes
+  uint32_t c[kPre];
 #pragma unroll
-  for (int j = 0; j < 8; j++) c[j] = coef(j * 64 + lane);
+  for (int j = 0; j < kPre; j++) c[j] = coef(j * 64 + lane);
 
   // side product: this block's units, loaded ahead of the row ring (vmcnt
   // retires in issue order) through descriptors that read zero past K
@@ -494,15 +497,19 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // program: entry e = the target of (output row m0 + e%8, input row kb + e/8):
   // body c in copy (e%8) % KODR_BS_NCOPY
   uint32_t* wp = prog_l + w * rpw * kBsRows;
-  for (int e0 = 0; e0 < ne; e0 += 64 * 8) {
-    if (e0) {
 #pragma unroll
-      for (int j = 0; j < 8; j++) c[j] = coef(e0 + j * 64 + lane);
-    }
+  for (int j = 0; j < kPre; j++) {
+    const int e = j * 64 + lane;
+    if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)((e & 7) % KODR_BS_NCOPY) * KODR_BS_COPY_BYTES;
+  }
+  for (int e0 = kPre * 64; e0 < ne; e0 += 64 * 8) {  // K > 256: the rest in rounds of 8 per lane
+    uint32_t cc[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) cc[j] = coef(e0 + j * 64 + lane);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       const int e = e0 + j * 64 + lane;
-      if (e < ne) wp[e] = tgt_l[c[j]] + (uint32_t)((e & 7) % KODR_BS_NCOPY) * KODR_BS_COPY_BYTES;
+      if (e < ne) wp[e] = tgt_l[cc[j]] + (uint32_t)((e & 7) % KODR_BS_NCOPY) * KODR_BS_COPY_BYTES;
     }
   }
 #ifdef KODR_TUNE_MODES
