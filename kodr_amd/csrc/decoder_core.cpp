@@ -311,7 +311,11 @@ bool DecoderCore::solve_systematic_batch(const uint8_t* vecs, size_t pitch) {
 // and add_many takes kodr's route.  One thread: the matrix is ~160 KB, and a
 // spin-barrier thread pool splitting its 64-byte column chunks over cores
 // (measured on the box: 2 threads 365 us, 8 threads 456 us, against 88 us on
-// one) moved more cache lines between cores per panel than it saved.
+// one) moved more cache lines between cores per panel than it saved.  Round
+// 3 re-tried it with every cache line of every row owned by one thread for
+// the whole solve (64-byte-aligned slots, the panel bytes passed through a
+// 4 KB buffer): 199-255 us on 2-8 threads against 88 us on one
+// (tools/probe/solve_threads.cpp, profiles/r03/solve_threads/).
 namespace {
 
 double now_us() {
