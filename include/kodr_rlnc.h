@@ -296,7 +296,7 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t
  * generations cost about one.  d_rows[g], counts[g]: decoder g's batch;
  * per-decoder results in consumed[g] and status[g] (what
  * rlnc_decoder_add_pieces_gpu would return).  The call itself fails only on
- * bad arguments or device errors. */
+ * bad arguments (including a decoder listed twice) or device errors. */
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
                                  const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                  int* status);

@@ -1736,6 +1736,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     consumed[g] = 0;
     status[g] = RLNC_OK;
   }
+  {  // each decoder once: their host mirrors are loaded concurrently below
+    std::vector<const rlnc_decoder*> u(ds, ds + G);
+    std::sort(u.begin(), u.end());
+    if (std::adjacent_find(u.begin(), u.end()) != u.end()) return RLNC_ERR_INVALID_ARGUMENT;
+  }
   for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   if (pitch < k + piece_len) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(ctx));

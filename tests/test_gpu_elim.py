@@ -252,3 +252,23 @@ def test_gpu_elimination_many_decoders(gpu_ctx, k):
     gpu_ctx.synchronize()
     for d in bufs:
         gpu_ctx.free(d)
+
+
+def test_gpu_elimination_rejects_a_decoder_listed_twice(gpu_ctx):
+    """The batched call loads the decoders' host mirrors concurrently, so a
+    handle listed twice is a bad argument, and nothing is consumed."""
+    k, L = 32, 64
+    rng = np.random.default_rng(11)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V = rng.integers(0, 256, (k, k), dtype=np.uint8)
+    d, pitch = _rows(gpu_ctx, V, P, L)
+    a, b = Dec(gpu_ctx, k), Dec(gpu_ctx, k)
+    decs = (ctypes.c_void_p * 3)(a.h.value, b.h.value, a.h.value)
+    rows_p = (ctypes.c_void_p * 3)(d, d, d)
+    counts = (ctypes.c_size_t * 3)(k, k, k)
+    consumed, status = (ctypes.c_size_t * 3)(), (ctypes.c_int * 3)()
+    rc = _lib.lib().rlnc_decoders_add_pieces_gpu(decs, 3, rows_p, counts, pitch, L, consumed, status)
+    assert rc == -1  # RLNC_ERR_INVALID_ARGUMENT
+    assert a.state()[1] == 0 and b.state()[1] == 0
+    gpu_ctx.synchronize()
+    gpu_ctx.free(d)
