@@ -402,6 +402,107 @@ __global__ __launch_bounds__(64 * KW) void gf_gemv_kernel(const uint8_t* __restr
   }
 }
 
+// gf_gemv_kernel for M <= MT output rows (two coded pieces of one generation
+// per call; MT = 2 is the instance used): the same stream -- 16 waves x 16 rows, every row load
+// issued first -- and the same shared tables, one set per output row: lane r
+// builds the MT table sets of row r0 + r, each step fetches its MT sets by
+// ds_bpermute, and a data dword's selectors serve all MT rows.  Rows >= M
+// have coefficient 0 and are not stored.
+template <int MT>
+__global__ __launch_bounds__(1024) void gf_gemv_multi_kernel(const uint8_t* __restrict__ A, int lda, int M, int K,
+                                                             const uint8_t* __restrict__ X, size_t ldx,
+                                                             uint8_t* __restrict__ Y, size_t ldy, int ncols,
+                                                             int accum) {
+  constexpr int KW = 16, RPW = 16, S = 2, STEPS = RPW / S, GL = 64 / S, CB = GL * kLaneBytes;
+  __shared__ uint4 part[KW][MT][GL];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane / GL, li = lane % GL;
+  const int col = blockIdx.x * CB + li * kLaneBytes;
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)((size_t)K * ldx), 0x00020000);
+  const int ildx = (int)ldx;
+  const int r0 = w * RPW;
+  uint32_t cv[MT];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+    cv[m] = (lane < RPW && r0 + lane < K && m < M) ? (uint32_t)A[(size_t)m * lda + r0 + lane] : 0u;
+  __builtin_amdgcn_sched_barrier(0);
+  u32x4 ring[STEPS];
+#pragma unroll
+  for (int j = 0; j < STEPS; j++)
+    ring[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (r0 + S * j + g) * ildx + col, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  uint4 m01[MT];
+  uint32_t m2[MT];
+#pragma unroll
+  for (int m = 0; m < MT; m++) gf_make_tables(cv[m], m01[m], m2[m]);
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t acc[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int d = 0; d < 4; d++) acc[m][d] = 0u;
+#pragma unroll
+  for (int j = 0; j < STEPS; j++) {
+    const int src = (S * j + g) * 4;
+    uint4 t01[MT];
+    uint32_t t2[MT];
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      t01[m].x = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01[m].x);
+      t01[m].y = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01[m].y);
+      t01[m].z = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01[m].z);
+      t01[m].w = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m01[m].w);
+      t2[m] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)m2[m]);
+    }
+    const u32x4 x = ring[j];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t s0 = x[d] & 0x07070707u, s1 = (x[d] >> 3) & 0x07070707u, s2 = (x[d] >> 6) & 0x03030303u;
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        const uint32_t a0 = __builtin_amdgcn_perm(t01[m].y, t01[m].x, s0);
+        const uint32_t a1 = __builtin_amdgcn_perm(t01[m].w, t01[m].z, s1);
+        const uint32_t a2 = __builtin_amdgcn_perm(t2[m], t2[m], s2);
+        acc[m][d] = __builtin_amdgcn_bitop3_b32(acc[m][d], a0, a1, 0x96) ^ a2;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const auto r = __builtin_amdgcn_permlane32_swap(acc[m][d], acc[m][d], false, false);  // lane ^ 32
+      acc[m][d] = r[0] ^ r[1];
+    }
+  if (g == 0)
+#pragma unroll
+    for (int m = 0; m < MT; m++) part[w][m][li] = make_uint4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+  __syncthreads();
+  if (tid >= MT * GL) return;
+  const int m = tid / GL, l = tid % GL;
+  if (m >= M) return;
+  uint4 v = part[0][m][l];
+#pragma unroll
+  for (int q = 1; q < KW; q++) {
+    const uint4 p = part[q][m][l];
+    v = make_uint4(v.x ^ p.x, v.y ^ p.y, v.z ^ p.z, v.w ^ p.w);
+  }
+  const int cc = blockIdx.x * CB + l * kLaneBytes;
+  if (cc >= ncols) return;
+  uint8_t* dst = Y + (size_t)m * ldy + cc;
+  if (cc + kLaneBytes <= ncols) {
+    if (accum) {
+      const uint4 o = *reinterpret_cast<const uint4*>(dst);
+      v = make_uint4(v.x ^ o.x, v.y ^ o.y, v.z ^ o.z, v.w ^ o.w);
+    }
+    *reinterpret_cast<uint4*>(dst) = v;
+  } else {
+    const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+    for (int i = 0; cc + i < ncols; i++) dst[i] = (uint8_t)(vv[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
+  }
+}
+
 // One product, or (grp != nullptr) grp->n products of the same shape in one launch.
 template <int MT, int KW, int S, int RC, int P, int MODE = 0, int AUX = 0>
 hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, size_t ldx,
@@ -684,6 +785,15 @@ static int gemv_enabled() {
   return v;
 }
 
+// Two rows on gf_gemv_multi_kernel: 9.1 against 10.4 us at 32 MiB/256
+// (profiles/r03/gemv_multi_ab/); four measured 11.8 against 11.0 on
+// gf_gemm_kernel (20 ds_bpermute per step), so 3-8 rows stay there.
+// KODR_GEMV_MULTI=0 keeps gf_gemm_kernel for two rows too (A/B).
+static bool gemv_multi_enabled() {
+  static const bool v = getenv("KODR_GEMV_MULTI") ? atoi(getenv("KODR_GEMV_MULTI")) != 0 : true;
+  return v;
+}
+
 hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint8_t* dX,
                    size_t ldx, uint8_t* dY, size_t ldy, size_t ncols, hipStream_t stream,
                    const GemmConfig* force, bool accumulate, const GemmGroupArgs* grp) {
@@ -693,6 +803,14 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   // streaming kernel (row offsets of all 256 lanes' rows fit 31 bits)
   constexpr int kGemvKW = 16, kGemvRPW = 16;
   const int gemv = gemv_enabled();
+  if (M == 2 && !grp && !force && K > (size_t)kGemvKW * kGemvRPW / 2 && K <= (size_t)kGemvKW * kGemvRPW &&
+      ncols >= 16384 && (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv_multi_enabled()) {
+    const int nx = (int)((ncols + 511) / 512);
+    hipLaunchKernelGGL(gf_gemv_multi_kernel<2>, dim3(nx), dim3(1024), 0, stream, dA, (int)lda, (int)M, (int)K, dX,
+                       ldx, dY, ldy, (int)ncols, acc);
+    last_launch_plan() = LaunchPlan{3, 2, kGemvKW, 2, kGemvRPW / 2, kGemvRPW, 1, nx};
+    return hipGetLastError();
+  }
   if (M == 1 && !grp && !force && K > (size_t)kGemvKW * kGemvRPW / 2 && K <= (size_t)kGemvKW * kGemvRPW &&
       ncols >= 16384 &&
       (size_t)kGemvKW * kGemvRPW * ldx < ((size_t)1 << 31) && gemv) {

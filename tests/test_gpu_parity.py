@@ -175,33 +175,37 @@ def test_gf_matmul_few_rows_wide_vs_oracle(gpu_ctx, M, K, ncols):
     assert (Y[:, ncols:] == 0xA5).all(), "wrote past ncols"
 
 
-@pytest.mark.parametrize("K,ncols", [(129, 16384), (200, 65536 + 16), (256, 131072), (256, 131072 + 48),
-                                     (255, 40000 + 7)])
-def test_gf_gemv_vs_oracle(gpu_ctx, K, ncols):
-    # one coded piece of a wide generation (M = 1, 129..256 rows, >= 16 KiB
-    # rows): the streaming gf_gemv_kernel (plan kernel 3), bit-exact with zero
-    # coefficients, ragged columns, nothing written past ncols
-    rng = np.random.default_rng(K * 131 + ncols)
+@pytest.mark.parametrize("M,K,ncols", [(1, 129, 16384), (1, 200, 65536 + 16), (1, 256, 131072), (1, 256, 131072 + 48),
+                                       (1, 255, 40000 + 7), (2, 256, 131072), (2, 130, 16384 + 5), (3, 256, 65536 + 48),
+                                       (4, 256, 131072), (4, 177, 40000 + 7)])
+def test_gf_gemv_vs_oracle(gpu_ctx, M, K, ncols):
+    # a few coded pieces of a wide generation (M = 1..4, 129..256 rows,
+    # >= 16 KiB rows): the streaming gf_gemv_kernel / gf_gemv_multi_kernel
+    # (plan kernel 3, M <= 2), gf_gemm_kernel for 3-4 rows, bit-exact with zero coefficients, lda > K, ragged
+    # columns, nothing written past ncols or past row M
+    rng = np.random.default_rng(M * 7 + K * 131 + ncols)
     ld = (ncols + 255) // 256 * 256
-    A = rng.integers(0, 256, (1, K), dtype=np.uint8)
-    A[0, rng.random(K) < 0.2] = 0
+    lda = K + 5
+    A = np.zeros((M, lda), np.uint8)
+    A[:, :K] = rng.integers(0, 256, (M, K), dtype=np.uint8)
+    A[:, :K][rng.random((M, K)) < 0.2] = 0
     X = np.zeros((K, ld), np.uint8)
     X[:, :ncols] = rng.integers(0, 256, (K, ncols), dtype=np.uint8)
-    dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(X.nbytes), gpu_ctx.alloc(ld)
+    dA, dX, dY = gpu_ctx.alloc(A.nbytes), gpu_ctx.alloc(X.nbytes), gpu_ctx.alloc((M + 1) * ld)
     try:
         gpu_ctx.h2d(dA, A)
         gpu_ctx.h2d(dX, X)
-        gpu_ctx.h2d(dY, np.full(ld, 0xA5, np.uint8))
-        errors.check(_lib.lib().rlnc_gf_matmul_device(gpu_ctx.handle, dA, K, 1, K, dX, ld, dY, ld, ncols))
+        gpu_ctx.h2d(dY, np.full((M + 1) * ld, 0xA5, np.uint8))
+        errors.check(_lib.lib().rlnc_gf_matmul_device(gpu_ctx.handle, dA, lda, M, K, dX, ld, dY, ld, ncols))
         plan = _lib.last_launch_plan()
-        Y = gpu_ctx.d2h(dY, ld)
+        Y = gpu_ctx.d2h(dY, (M + 1) * ld).reshape(M + 1, ld)
     finally:
         for p in (dA, dX, dY):
             gpu_ctx.free(p)
-    assert plan["kernel"] == 3, plan
-    _, ref = oracle.matmul(A, X[:, :ncols])
-    assert np.array_equal(Y[:ncols], ref[0]), (K, ncols)
-    assert (Y[ncols:] == 0xA5).all(), "wrote past ncols"
+    assert plan["kernel"] == (3 if M <= 2 else 1), plan   # 3-4 rows: gf_gemm_kernel
+    _, ref = oracle.matmul(A[:, :K], X[:, :ncols])
+    assert np.array_equal(Y[:M, :ncols], ref), (M, K, ncols)
+    assert (Y[:M, ncols:] == 0xA5).all() and (Y[M] == 0xA5).all(), "wrote past ncols or row M"
 
 
 def test_c2_encode_batch_full_compare(gpu_ctx):
