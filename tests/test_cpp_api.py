@@ -29,3 +29,18 @@ def test_cpp_api_runs_kodr_flows():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok (0 failures)" in r.stdout
+
+
+def test_host_pool_runs_every_task_once():
+    """kodr_amd/csrc/host_pool.hpp (the grouped entry points' per-decoder host
+    work): every task once per call, calls from two threads kept apart, and
+    with KODR_HOST_THREADS=1 (no workers) the same results."""
+    src = os.path.join(ROOT, "tests", "cpp", "host_pool_test.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "host_pool_test")
+    r = subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-Wall", src, "-o", exe], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    for threads in ("8", "1"):
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=120,
+                           env={**os.environ, "KODR_HOST_THREADS": threads})
+        assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout + r.stderr
