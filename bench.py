@@ -413,12 +413,13 @@ class HipRelayEngine:
         self.ctx.synchronize()
 
 
-def run_relay(engine, k, L, rng, torch, dist, kdist, device="cuda", reps=6, keep=False):
+def run_relay(engine, k, L, rng, torch, dist, kdist, device="cuda", reps=6, keep=False, self_p2p=False):
     """BASELINE config 5 on N GPUs: every rank encodes k coded pieces of its
     generation (wire layout, kodr_amd.dist.wire_pitch), ring-shifts them to
     rank+1 over RCCL/xGMI, and recodes the k pieces it received.  Returns
     per-phase times (max over ranks); keep=True also returns the last
-    repetition's buffers (tests check them against the oracle)."""
+    repetition's buffers (tests check them against the oracle); self_p2p
+    runs the exchange through the P2P ops even with one rank (GPU test)."""
     import numpy as np
     clen = k + L
     pitch = kdist.wire_pitch(k, L)
@@ -435,7 +436,7 @@ def run_relay(engine, k, L, rng, torch, dist, kdist, device="cuda", reps=6, keep
         engine.encode_wire(send, k, pitch)     # k wire rows [vector | piece]
         engine.synchronize()
         t1 = time.perf_counter()
-        kdist.ring_shift(send, recv)
+        kdist.ring_shift(send, recv, self_p2p=self_p2p)
         if device == "cuda":
             torch.cuda.synchronize()
         t2 = time.perf_counter()

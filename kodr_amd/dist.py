@@ -34,11 +34,14 @@ def wire_pitch(k, L):
     return (k + L + 255) // 256 * 256
 
 
-def ring_shift(send, recv, group=None):
-    """Send `send` to rank+1 and receive into `recv` from rank-1 (one P2P step)."""
+def ring_shift(send, recv, group=None, self_p2p=False):
+    """Send `send` to rank+1 and receive into `recv` from rank-1 (one P2P step).
+    With one rank the shift is a copy, unless self_p2p: then the same
+    isend/irecv pair runs with the rank as its own peer (the GPU test that
+    moves bytes through RCCL on a one-GPU box)."""
     import torch.distributed as dist
     rank, ws = dist.get_rank(group), dist.get_world_size(group)
-    if ws == 1:
+    if ws == 1 and not self_p2p:
         recv.copy_(send)
         return
     if send.is_cuda and dist.get_backend(group) == "gloo":   # CPU-transport rehearsal
