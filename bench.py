@@ -603,6 +603,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["c5_encode_recode_one_gpu_grouped"] = c5_one_gpu_grouped(ctx, L_, errors, encs[:8], k, L, rng)
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
     out["batched_decode_elimination"] = batched_elim(ctx, L_, errors, rng)
+    out["batched_decode_elimination_rounds"] = batched_elim_rounds(ctx, L_, errors, rng)
     out["c1_roundtrip"] = c1_roundtrip(ctx, L_, errors, rng)
     out["encode_two_streams"] = two_streams(L_, errors, k, L, rng)
     out["host_path"] = host_roundtrip(ctx, L_, errors, k, L, rng)
@@ -1019,6 +1020,68 @@ def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
                 L_.rlnc_decoder_destroy(x)
             best = t if best is None else min(best, t)
         res[mode + "_ms"] = round(best * 1e3, 3)
+        res[mode + "_ok"] = ok
+    res["gpu_speedup"] = round(res["host_ms"] / res["gpu_ms"], 2)
+    for d in bufs:
+        ctx.free(d)
+    return res
+
+
+def batched_elim_rounds(ctx, L_, errors, rng, k=256, G=32, L=256, rounds=4, reps=3):
+    """Batched AddPiece on G decoders fed in `rounds` batches each (k + 2
+    device wire rows split evenly, short pieces so the coefficient side
+    dominates): host elimination per decoder (rlnc_decoder_add_pieces)
+    against one rlnc_decoders_add_pieces_gpu call per round.  After the first
+    round the decoders are no longer fresh: their batches are eliminated on
+    the GPU from [held coefficient rows ; batch vectors] (continued decoders,
+    DecoderCore::load_continued).  Wall time per round, best of reps."""
+    import ctypes
+    import numpy as np
+    n = k + 2
+    pitch = (k + L + 15) // 16 * 16
+    cuts = [round(i * n / rounds) for i in range(rounds + 1)]
+    bufs = []
+    for g in range(G):
+        rows = rng.integers(0, 256, (n, pitch), dtype=np.uint8)
+        d = ctx.alloc(rows.nbytes)
+        ctx.h2d(d, rows)
+        bufs.append(d)
+    res = {"k": k, "generations": G, "piece_len": L, "rows_per_round": [cuts[i + 1] - cuts[i] for i in range(rounds)]}
+    for mode in ("host", "gpu"):
+        best, ok = None, True
+        for rep in range(reps):
+            decs = []
+            for g in range(G):
+                h = ctypes.c_void_p()
+                errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+                decs.append(h)
+            ts = []
+            for r in range(rounds):
+                ctx.synchronize()
+                t0 = time.perf_counter()
+                cnt = cuts[r + 1] - cuts[r]
+                if mode == "host":
+                    for g in range(G):
+                        c = ctypes.c_size_t()
+                        st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g] + cuts[r] * pitch, cnt, pitch, L, 1,
+                                                        ctypes.byref(c))
+                        ok = ok and st in (0, 3)
+                else:
+                    cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+                    errors.check(L_.rlnc_decoders_add_pieces_gpu(
+                        (ctypes.c_void_p * G)(*[x.value for x in decs]), G,
+                        (ctypes.c_void_p * G)(*[b + cuts[r] * pitch for b in bufs]),
+                        (ctypes.c_size_t * G)(*([cnt] * G)), pitch, L, cons, sts))
+                    ok = ok and all(s_ in (0, 3) for s_ in sts)
+                ctx.synchronize()
+                ts.append(time.perf_counter() - t0)
+            ok = ok and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
+            for x in decs:
+                L_.rlnc_decoder_destroy(x)
+            if best is None or sum(ts) < sum(best):
+                best = ts
+        res[mode + "_ms_per_round"] = [round(t * 1e3, 3) for t in best]
+        res[mode + "_ms"] = round(sum(best) * 1e3, 3)
         res[mode + "_ok"] = ok
     res["gpu_speedup"] = round(res["host_ms"] / res["gpu_ms"], 2)
     for d in bufs:

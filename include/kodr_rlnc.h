@@ -286,9 +286,12 @@ int rlnc_decoder_add_pieces(rlnc_decoder* dec, const uint8_t* rows, size_t count
  * (decoder_state.go:15-182) on the GPU: one workgroup runs kodr's pivots for
  * the rows that land on their diagonals (gf_elim.hip); the rest of the batch,
  * if any, continues on the host from the state it left.  Same state, return
- * code and *consumed as rlnc_decoder_add_pieces (is_device = 1).  Used on a
- * fresh decoder with 2 <= piece_count <= 256; otherwise it IS
- * rlnc_decoder_add_pieces. */
+ * code and *consumed as rlnc_decoder_add_pieces (is_device = 1).  Used for
+ * batches of >= 2 rows with 2 <= piece_count <= 256 on a fresh decoder, or
+ * on one whose received pieces were all kept (none dependent) when the batch
+ * can complete the rank or the held rows are diagonal pivots (the GPU then
+ * eliminates [held coefficient rows ; batch vectors] and the host maps the
+ * transform back to arrival order); otherwise it IS rlnc_decoder_add_pieces. */
 int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t count, size_t pitch,
                                 size_t piece_len, size_t* consumed);
 /* G decoders of one context and one piece_count at once: one GPU launch

@@ -97,6 +97,7 @@ struct rlnc_ctx {
   DevBuf elim_tab;           // gf_elim's field tables (once per context)
   bool elim_tab_ok = false;
   DevBuf elim_out;           // gf_elim's per-generation states and counts
+  DevBuf elim_in;            // gf_elim's input for continued decoders: [coefficient rows ; vectors]
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
@@ -1749,14 +1750,23 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
                              std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double tt0 = timing ? tnow() : 0;
   double tt1 = 0, tt2 = 0, tt3 = 0;
-  // GPU elimination for fresh decoders with >= 2 rows (kElimMaxGens per
-  // launch); every other decoder takes rlnc_decoder_add_pieces
+  // GPU elimination (kElimMaxGens per launch) for batches of >= 2 rows on
+  //  * fresh decoders, from the rows' coding vectors;
+  //  * decoders whose r received rows were all kept ("continued") and whose
+  //    batch can complete the rank, from M = [their r coefficient rows ; the
+  //    batch's first k - r vectors] (load_continued);
+  // every other decoder takes rlnc_decoder_add_pieces.  (Continued batches
+  // that cannot complete the rank would take the per-step kernel over all
+  // r + n rows of M: measured slower than the host's add_panel, 1.7 against
+  // 1.3 ms for 32 decoders at k = 256 adding 65 rows to 64, profiles/r03/elim_cont/.)
   std::vector<size_t> gpu;
   std::vector<BatchCopy> bcs(G);
   std::vector<DeferredCopy> defer;
   for (size_t g = 0; g < G; g++) {
     rlnc_decoder* d = ds[g];
-    const bool ok = k >= 2 && k <= 256 && counts[g] >= 2 && d->core.received() == 0;
+    const size_t r = d->core.received();
+    const bool cont = r >= 1 && r < k && d->core.rank() == r && r + counts[g] >= k;
+    const bool ok = k >= 2 && k <= 256 && counts[g] >= 2 && (r == 0 || cont);
     if (!ok) {
       status[g] = rlnc_decoder_add_pieces(d, rows[g], counts[g], pitch, piece_len, 1, &consumed[g]);
       continue;
@@ -1795,25 +1805,54 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   }
   if (timing) tt1 = tnow();
   if (gpu.empty()) return RLNC_OK;
-  // full batches first: launches of full batches only take the blocked kernel
-  std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return counts[g] >= k; });
+  // fresh decoders first (their launches read the rows' vectors in place),
+  // full batches first among them: launches of full batches only take the
+  // blocked kernel
+  std::vector<size_t> base(G, 0);  // rows a continued decoder held before
+  for (size_t g : gpu) base[g] = ds[g]->core.received();
+  std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return base[g] + counts[g] >= k; });
+  std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return base[g] == 0; });
+  const size_t nfresh = (size_t)std::count_if(gpu.begin(), gpu.end(), [&](size_t g) { return base[g] == 0; });
   TRY(ctx_elim_tables(ctx));
   const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
   const size_t chunk = std::min<size_t>(gpu.size(), kodr_amd::kElimMaxGens);
   ctx->elim_out.bind(ctx->device, ctx->stream);
   TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
+  if (nfresh < gpu.size()) {  // continued decoders: their M, k x k each
+    ctx->elim_in.bind(ctx->device, ctx->stream);
+    TRY(ctx->elim_in.reserve(chunk * k * k));
+  }
   // only what the kernel wrote is read back: no zero-fill, grown once per context
   if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
   uint8_t* const hostp = ctx->elim_host.data();
-  for (size_t c0 = 0; c0 < gpu.size(); c0 += chunk) {
-    const size_t nc = std::min(chunk, gpu.size() - c0);
+  bool copies_out = !side;
+  std::vector<uint8_t> hm;
+  // chunks never mix fresh and continued decoders (one vector pitch per launch)
+  for (size_t c0 = 0; c0 < gpu.size();) {
+    const bool cont = c0 >= nfresh;
+    const size_t nc = std::min(chunk, (cont ? gpu.size() : nfresh) - c0);
     kodr_amd::ElimArgs a = {};
     for (size_t i = 0; i < nc; i++) {
       const size_t g = gpu[c0 + i];
-      a.vecs[i] = rows[g];
-      a.n[i] = (int)std::min(counts[g], k);
+      a.n[i] = (int)std::min(base[g] + counts[g], k);
+      a.vecs[i] = cont ? ctx->elim_in.p + i * k * k : rows[g];
     }
-    a.vpitch = pitch;
+    if (cont) {
+      // M of each decoder (k x k at pitch k): its coefficient rows, in row
+      // order, in one upload for the chunk, then the batch's first k - r
+      // vectors (device to device) below them
+      hm.resize(nc * k * k);
+      HostPool::get().run(nc, [&](size_t i) {
+        const rlnc_decoder* d = ds[gpu[c0 + i]];
+        for (size_t j = 0; j < base[gpu[c0 + i]]; j++) memcpy(hm.data() + (i * k + j) * k, d->core.coeff_row(j), k);
+      });
+      HIPC(ctx->stage.h2d(ctx->elim_in.p, k, hm.data(), k, k, nc * k, ctx->stream));
+      for (size_t i = 0; i < nc; i++) {
+        const size_t g = gpu[c0 + i], r = base[g];
+        HIPC(kodr_amd::copy_rows(rows[g], pitch, ctx->elim_in.p + (i * k + r) * k, k, k - r, k, ctx->stream));
+      }
+    }
+    a.vpitch = cont ? k : pitch;
     a.tables = reinterpret_cast<const uint32_t*>(ctx->elim_tab.p);
     a.out = ctx->elim_out.p + hdr;
     a.out_gen_stride = ostride;
@@ -1821,10 +1860,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
     a.k = (int)k;
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
-    if (side && c0 == 0) {
+    if (!copies_out) {
       TRY(launch_copies());
       HIPC(hipEventRecord(ctx->side_done, ctx->side));
       HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
+      copies_out = true;
     }
     if (timing) tt2 = tnow();
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
@@ -1854,14 +1894,21 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     if (timing) tt3 = tnow();
     const int* cnt = reinterpret_cast<const int*>(hostp);
     // the states into the decoders' host mirrors: independent per decoder,
-    // memory-bound (a 256 x 520-byte arena each), so spread over host threads
+    // memory-bound (a 256 x 520-byte arena each), so spread over host threads.
+    // got[i] = rows of the batch accepted
     std::vector<size_t> got(nc);
     HostPool::get().run(nc, [&](size_t i) {
       rlnc_decoder* d = ds[gpu[c0 + i]];
+      const size_t r = base[gpu[c0 + i]];
       size_t c = (size_t)std::max(cnt[i], 0);
-      if (c && tonly && !(c == k && d->core.load_inverse(hostp + hdr + i * k * k, k))) c = 0;
-      if (c && !tonly && !d->core.load_rref(hostp + hdr + i * ostride, opitch, c)) c = 0;
-      got[i] = c;
+      bool ok = false;
+      if (c == k && cont)
+        ok = tonly ? d->core.load_continued(hostp + hdr + i * k * k, k, true)
+                   : d->core.load_continued(hostp + hdr + i * ostride, opitch, false);
+      else if (c && !cont)
+        ok = tonly ? c == k && d->core.load_inverse(hostp + hdr + i * k * k, k)
+                   : d->core.load_rref(hostp + hdr + i * ostride, opitch, c);
+      got[i] = ok ? c - r : 0;
     });
     for (size_t i = 0; i < nc; i++) {
       const size_t g = gpu[c0 + i];
@@ -1888,6 +1935,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       consumed[g] = n;
       status[g] = pst != RLNC_OK ? pst : st;
     }
+    c0 += nc;
   }
   if (timing)
     fprintf(stderr, "add_pieces_gpu G=%zu side=%d: pre+copies %.1f us, elim launch %.1f, wait+read-back %.1f, "

@@ -791,6 +791,48 @@ bool DecoderCore::load_inverse(const uint8_t* tinv, size_t pitch) {
   return true;
 }
 
+bool DecoderCore::load_continued(const uint8_t* state, size_t pitch, bool inverse) {
+  const size_t k = k_, r = received_, c = k;
+  if (r == 0 || r >= k || rows_.size() != r) return false;
+  if (!inverse)
+    for (size_t i = 0; i < c; i++)
+      if (state[i * pitch + i] != 1) return false;
+  ensure_tcap(c);  // may move the rows: their pointers are read after it
+  std::vector<const uint8_t*> tr(r);
+  for (size_t m = 0; m < r; m++) tr[m] = rows_[m] + k;  // T_r, row m of M
+  const size_t w = k + c;
+  std::vector<uint8_t> buf(c * w, 0);
+  for (size_t i = 0; i < c; i++) {
+    uint8_t* o = buf.data() + i * w;
+    const uint8_t* s = state + i * pitch;
+    const uint8_t* f = inverse ? s : s + k;
+    if (inverse) o[i] = 1;
+    else memcpy(o, s, k);
+    hostgf::accumulate(o + k, tr.data(), f, r, r);  // F[:, :r] x T_r
+    memcpy(o + k + r, f + r, c - r);                 // the batch's columns
+  }
+  for (uint8_t* row : rows_) free_.push_back(row);
+  rows_.clear();
+  up_.clear();
+  ut_.clear();
+  std::fill(ucnt_.begin(), ucnt_.end(), 0u);
+  ndense_ = 0;
+  dense_pos_.clear();
+  for (size_t i = 0; i < c; i++) {
+    uint8_t* row = free_.back();
+    free_.pop_back();
+    memcpy(row, buf.data() + i * w, w);
+    memset(row + w, 0, tcap_ - c);
+    push_row(row, -1, 0);
+    clean_[i] = 1;
+    touched_[i] = 0;
+  }
+  received_ = c;
+  useful_ = c;
+  all_clean_ = true;
+  return true;
+}
+
 size_t DecoderCore::decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const {
   row_of->assign(k_, -1);
   scale->assign(k_, 0);

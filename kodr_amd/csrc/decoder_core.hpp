@@ -45,6 +45,15 @@ class DecoderCore {
   // C are independent: [I | C^-1], given as C^-1 (k rows of k bytes at `pitch`,
   // columns in arrival order).  Returns false (and changes nothing) otherwise.
   bool load_inverse(const uint8_t* tinv, size_t pitch);
+  // A decoder holding r = received() >= 1 rows, all kept (rank() == r),
+  // whose next k - r arrivals make its first k coding vectors C independent:
+  // kodr ends in [I | C^-1] from any such state (an independent row never
+  // becomes zero, rank counts kept rows).  The state comes from elsewhere
+  // (gf_elim.hip) over M = [its r coefficient rows, in row order ; those
+  // k - r vectors] = diag(T_r, I) x C, T_r its transform: k rows of k
+  // coefficient bytes (I) then F = M^-1 at `pitch`, or with `inverse` only
+  // F; C^-1 = F x diag(T_r, I).  Returns false (and changes nothing) otherwise.
+  bool load_continued(const uint8_t* state, size_t pitch, bool inverse);
 
   bool is_decoded() const { return useful_ >= k_; }   // full/decoder.go:32-34
   size_t required() const { return k_ - useful_; }    // full/decoder.go:38-40

@@ -127,8 +127,9 @@ def test_gpu_elimination_matches_host(gpu_ctx, kind, k):
 
 def test_gpu_elimination_batched_generations(gpu_ctx):
     """Several decoders in one launch: fresh ones with clean and quirky
-    batches, one that already holds a piece (host path), one with a single
-    row (host path); each ends exactly as rlnc_decoder_add_pieces leaves it."""
+    batches, one that already holds a piece (a continued decoder: its batch
+    completes the rank), one with a single row (host path); each ends exactly
+    as rlnc_decoder_add_pieces leaves it."""
     rng = np.random.default_rng(77)
     k, L = 64, 100
     kinds = ["dense", "tiny", "dense", "lowrank", "dense", "systematic", "dense"]
@@ -148,7 +149,7 @@ def test_gpu_elimination_batched_generations(gpu_ctx):
         bufs.append(d)
         hosts.append(Dec(gpu_ctx, k))
         gpus.append(Dec(gpu_ctx, k))
-    # decoder 2 already holds one piece: not fresh, takes the host path
+    # decoder 2 already holds one piece: not fresh, eliminated from [its row ; the batch]
     c0 = ctypes.c_size_t()
     for dec in (hosts[2], gpus[2]):
         assert _lib.lib().rlnc_decoder_add_pieces(dec.h, ctypes.c_void_p(bufs[2]), 1, pitch, L, 1,
@@ -272,3 +273,86 @@ def test_gpu_elimination_rejects_a_decoder_listed_twice(gpu_ctx):
     assert a.state()[1] == 0 and b.state()[1] == 0
     gpu_ctx.synchronize()
     gpu_ctx.free(d)
+
+
+def _split(rng, n, k, scheme):
+    if scheme == "one_then_rest":
+        cuts = [1]
+    elif scheme == "halves":
+        cuts = [k // 2]
+    elif scheme == "quarters":
+        cuts = [k // 4, k // 2, 3 * k // 4]
+    elif scheme == "random":
+        cuts = sorted(set(int(x) for x in rng.integers(1, n, 4)))
+    elif scheme == "tail_pair":  # the last batch is 2 rows
+        cuts = [n - 2]
+    else:
+        raise ValueError(scheme)
+    b = [0] + [c for c in cuts if 0 < c < n] + [n]
+    return [(b[i], b[i + 1]) for i in range(len(b) - 1)]
+
+
+CONT_KINDS = ["dense", "tiny", "lowrank", "zero_mid", "systematic", "first_zero", "dense", "dense"]
+CONT_SCHEMES = ["one_then_rest", "halves", "quarters", "random", "tail_pair", "quarters", "random", "halves"]
+
+
+@pytest.mark.parametrize("k", [4, 16, 64, 129, 256])
+def test_gpu_elimination_continued_batches(gpu_ctx, k):
+    """Decoders fed in several batched GPU AddPiece calls (rounds): after the
+    first batch a decoder is no longer fresh; a later batch that can complete
+    the rank of a decoder whose rows were all kept is eliminated on the GPU
+    from M = [its coefficient rows ; the batch's vectors] (DecoderCore::
+    load_continued: C^-1 = M^-1 x diag(T_r, I)), other batches on the host.  Each round's status,
+    rows consumed, counters, coefficients and transform equal host decoders
+    fed the same batches (rlnc_decoder_add_pieces), the final coefficients
+    equal the oracle's literal decoder (decoder_state.go:15-182) fed the rows
+    one by one, and decoded generations come back byte for byte."""
+    rng = np.random.default_rng(1000 + k)
+    L = 72
+    G = len(CONT_KINDS)
+    gens = []
+    for gi, kind in enumerate(CONT_KINDS):
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        n = k + int(rng.integers(0, 4))
+        V = _vectors(rng, kind, n, k)
+        gens.append((P, V, _split(rng, n, k, CONT_SCHEMES[gi])))
+    pitch = ((k + L + 15) // 16) * 16
+    bufs, hosts, gpus = [], [], []
+    for P, V, _ in gens:
+        rows = np.zeros((V.shape[0], pitch), np.uint8)
+        rows[:, :k], rows[:, k:k + L] = V, oracle.encode(P, V)
+        d = gpu_ctx.alloc(rows.nbytes)
+        gpu_ctx.h2d(d, rows)
+        bufs.append(d)
+        hosts.append(Dec(gpu_ctx, k))
+        gpus.append(Dec(gpu_ctx, k))
+    rounds = max(len(sp) for _, _, sp in gens)
+    for rd in range(rounds):
+        part = [gi for gi in range(G) if rd < len(gens[gi][2])]
+        n_ = len(part)
+        counts = (ctypes.c_size_t * n_)(*[gens[gi][2][rd][1] - gens[gi][2][rd][0] for gi in part])
+        rows_p = (ctypes.c_void_p * n_)(*[bufs[gi] + gens[gi][2][rd][0] * pitch for gi in part])
+        decs = (ctypes.c_void_p * n_)(*[gpus[gi].h.value for gi in part])
+        consumed = (ctypes.c_size_t * n_)()
+        status = (ctypes.c_int * n_)()
+        errors.check(_lib.lib().rlnc_decoders_add_pieces_gpu(decs, n_, rows_p, counts, pitch, L, consumed, status))
+        for j, gi in enumerate(part):
+            c = ctypes.c_size_t()
+            st = _lib.lib().rlnc_decoder_add_pieces(hosts[gi].h, ctypes.c_void_p(rows_p[j]), counts[j], pitch, L, 1,
+                                                    ctypes.byref(c))
+            assert (status[j], consumed[j]) == (st, c.value), (gi, rd)
+            _same(hosts[gi], gpus[gi])
+    for gi, (P, V, _) in enumerate(gens):
+        ref = oracle.Decoder(k)
+        C = oracle.encode(P, V)
+        for i in range(V.shape[0]):
+            if ref.add(V[i], C[i]) != 0:
+                break
+        assert gpus[gi].state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded()), gi
+        assert np.array_equal(gpus[gi].coefficients(), ref.coeffs()), gi
+        if ref.is_decoded():
+            st, out = gpus[gi].get_all()
+            assert st == 0 and np.array_equal(out, P), gi
+    gpu_ctx.synchronize()
+    for d in bufs:
+        gpu_ctx.free(d)
