@@ -604,6 +604,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     out["c4_systematic_decode"] = c4_decode(ctx, L_, errors, rng)
     out["batched_decode_elimination"] = batched_elim(ctx, L_, errors, rng)
     out["batched_decode_elimination_rounds"] = batched_elim_rounds(ctx, L_, errors, rng)
+    out["c2_decode_piecewise_grouped"] = piecewise_grouped(ctx, L_, errors, encs, k, L)
     out["c1_roundtrip"] = c1_roundtrip(ctx, L_, errors, rng)
     out["encode_two_streams"] = two_streams(L_, errors, k, L, rng)
     out["host_path"] = host_roundtrip(ctx, L_, errors, k, L, rng)
@@ -1024,6 +1025,81 @@ def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
     res["gpu_speedup"] = round(res["host_ms"] / res["gpu_ms"], 2)
     for d in bufs:
         ctx.free(d)
+    return res
+
+
+def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
+    """C2 fed the way kodr's decoder is (one AddPiece per piece,
+    full/decoder.go:50-66), for every resident generation at once: G decoders
+    take k device wire rows each, round-robin, one rlnc_decoder_add_piece_device
+    call per piece (lazy AddPiece queues them), then the queues are eliminated
+    either by ONE rlnc_decoders_flush_gpu call (GPU elimination) or by each
+    decoder's own state read (host); two more pieces per generation follow
+    (refused once decoded, used where the first k were dependent), and one
+    grouped GetPieces decodes all.
+    ctypes arguments are built outside the timed region (a Go caller pays no
+    such cost); best of reps."""
+    import ctypes
+    import numpy as np
+    G, W, n = len(encs), k + L, k + 2
+    earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+    dW = ctx.alloc(G * n * W)
+    dO = ctx.alloc(G * k * L)
+    res = {"generations": G}
+    for mode in ("host", "gpu"):
+        best, ok = None, True
+        for rep in range(reps + 1):
+            errors.check(L_.rlnc_encoder_group_coded_wire_device(earr, G, n, dW, W))
+            vec = ctx.d2h(dW, G * n * W).reshape(G * n, W)[:, :k].copy()
+            decs = []
+            for g in range(G):
+                h = ctypes.c_void_p()
+                errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+                decs.append(h)
+            darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
+            add = L_.rlnc_decoder_add_piece_device
+            args = [(decs[g], vec[g * n + i].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), dW + (g * n + i) * W + k)
+                    for i in range(n) for g in range(G)]
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for h, v, p_ in args[:k * G]:
+                if add(h, v, k, p_, L) != 0:
+                    ok = False
+            t1 = time.perf_counter()
+            if mode == "gpu":
+                errors.check(L_.rlnc_decoders_flush_gpu(darr, G))
+            else:
+                for h in decs:
+                    L_.rlnc_decoder_is_decoded(h)
+            t2 = time.perf_counter()
+            for h, v, p_ in args[k * G:]:
+                if add(h, v, k, p_, L) not in (0, 3):
+                    ok = False
+            errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, dO, L))
+            ctx.synchronize()
+            t3 = time.perf_counter()
+            ok = ok and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
+            for x in decs:
+                L_.rlnc_decoder_destroy(x)
+            if rep and (best is None or t3 - t0 < best[0]):
+                best = (t3 - t0, t1 - t0, t2 - t1, t3 - t2)
+        pitch = ctypes.c_size_t()
+        for g in (0, G - 1):
+            dp = L_.rlnc_encoder_device_pieces(encs[g], ctypes.byref(pitch))
+            a = ctx.d2h(dO + g * k * L, k * L)
+            b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
+            ok = ok and bool(np.array_equal(a, b))
+        t, t_add, t_flush, t_rest = best
+        res[mode] = {"ms": round(t * 1e3, 3), "us_per_generation": round(t / G * 1e6, 1),
+                     "add_calls_us_per_generation": round(t_add / G * 1e6, 1),
+                     "flush_us_per_generation": round(t_flush / G * 1e6, 1),
+                     "spare_adds_and_get_us_per_generation": round(t_rest / G * 1e6, 1), "roundtrip_ok": ok}
+    res["flush_speedup"] = round(res["host"]["flush_us_per_generation"] / res["gpu"]["flush_us_per_generation"], 2)
+    res["note"] = ("k AddPiece calls per generation (device pieces, round-robin over the generations), the queued "
+                   "eliminations flushed by one rlnc_decoders_flush_gpu (gpu) or by each decoder's IsDecoded (host), "
+                   "2 more AddPiece calls per generation, one grouped GetPieces; wall time")
+    ctx.free(dW)
+    ctx.free(dO)
     return res
 
 

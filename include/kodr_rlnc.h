@@ -303,6 +303,17 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
                                  const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                  int* status);
+/* The pending AddPiece calls of G decoders (one context, one piece_count),
+ * eliminated together: one AddPiece call per piece only queues the coding
+ * vector while the queue cannot complete the rank (lazy AddPiece), and a
+ * decoder's next state read eliminates its queue on the host.  This call
+ * takes every decoder whose queue completes its rank from a state of kept
+ * pieces (none dependent) through ONE GPU elimination launch (gf_elim.hip, a
+ * workgroup each; no kodr counterpart: a server feeding many generations
+ * piece by piece calls it once per tick); the rest, and singular batches,
+ * take the host flush.  Queued device pieces are gathered as well.  The
+ * state afterwards is the one the individual state reads would leave. */
+int rlnc_decoders_flush_gpu(rlnc_decoder* const* decs, size_t G);
 int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */
 size_t rlnc_decoder_required(const rlnc_decoder* dec);       /* Required  :38-40 */
 size_t rlnc_decoder_useful(const rlnc_decoder* dec);         /* rank */

@@ -86,6 +86,7 @@ SIGNATURES = {
     "rlnc_decoder_get_decoded": (_int, [_vp, _sz, _vp, _int]),
     "rlnc_decoder_bind_output": (_int, [_vp, _vp, _sz]),
     "rlnc_decoders_add_pieces_gpu": (_int, [_vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp]),
+    "rlnc_decoders_flush_gpu": (_int, [_vp, _sz]),
     "rlnc_decoders_get_pieces_device": (_int, [_vp, _sz, _vp, _sz]),
     "rlnc_recoder_group_coded_pieces_device": (_int, [_vpp, _sz, _vp, _sz, _vp, _sz]),
     "rlnc_decoder_is_decoded": (_int, [_vp]),

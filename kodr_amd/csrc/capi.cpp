@@ -1953,6 +1953,90 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t cou
   return st;
 }
 
+// The lazy queues of G decoders (one AddPiece call per piece) eliminated
+// together: every decoder whose queued vectors complete its rank from a
+// state of kept rows -- fresh (r = 0) or continued -- in one GPU launch per
+// kElimMaxGens, from M = [its r coefficient rows ; the queued vectors], all on
+// the host already (one upload); the others, and any singular M, through
+// the host flush their next state read would run.  Then every decoder's
+// borrowed device pieces are gathered.  Same state as G host flushes.
+int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
+  if (!ds || !G) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
+  if (!ctx) return RLNC_ERR_NO_DEVICE;
+  const size_t k = ds[0]->core.piece_count();
+  for (size_t g = 0; g < G; g++)
+    if (!ds[g] || ds[g]->ctx != ctx || ds[g]->core.piece_count() != k) return RLNC_ERR_INVALID_ARGUMENT;
+  {  // each decoder once: their host mirrors are loaded concurrently below
+    std::vector<const rlnc_decoder*> u(ds, ds + G);
+    std::sort(u.begin(), u.end());
+    if (std::adjacent_find(u.begin(), u.end()) != u.end()) return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  TRY(set_dev(ctx));
+  std::vector<size_t> el;
+  for (size_t g = 0; g < G; g++) {
+    const rlnc_decoder* d = ds[g];
+    const size_t r = d->core.received();
+    if (k >= 2 && k <= 256 && d->npend >= 2 && d->core.rank() == r && r + d->npend >= k) el.push_back(g);
+  }
+  if (!el.empty()) {
+    TRY(ctx_elim_tables(ctx));
+    const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
+    const size_t chunk = std::min<size_t>(el.size(), kodr_amd::kElimMaxGens);
+    ctx->elim_out.bind(ctx->device, ctx->stream);
+    TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
+    ctx->elim_in.bind(ctx->device, ctx->stream);
+    TRY(ctx->elim_in.reserve(chunk * k * k));
+    if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
+    uint8_t* const hostp = ctx->elim_host.data();
+    std::vector<uint8_t> hm(chunk * k * k);
+    for (size_t c0 = 0; c0 < el.size(); c0 += chunk) {
+      const size_t nc = std::min(chunk, el.size() - c0);
+      kodr_amd::ElimArgs a = {};
+      HostPool::get().run(nc, [&](size_t i) {  // M: coefficient rows in row order, then the queue
+        const rlnc_decoder* d = ds[el[c0 + i]];
+        const size_t r = d->core.received();
+        uint8_t* m = hm.data() + i * k * k;
+        for (size_t j = 0; j < r; j++) memcpy(m + j * k, d->core.coeff_row(j), k);
+        memcpy(m + r * k, d->pend_v.data(), (k - r) * k);
+      });
+      for (size_t i = 0; i < nc; i++) {
+        a.vecs[i] = ctx->elim_in.p + i * k * k;
+        a.n[i] = (int)k;
+      }
+      HIPC(ctx->stage.h2d(ctx->elim_in.p, k, hm.data(), k, k, nc * k, ctx->stream));
+      a.vpitch = k;
+      a.tables = reinterpret_cast<const uint32_t*>(ctx->elim_tab.p);
+      a.out = ctx->elim_out.p + hdr;
+      a.out_gen_stride = ostride;
+      a.out_pitch = opitch;
+      a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
+      a.k = (int)k;
+      HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
+      const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
+      HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
+      if (tonly)
+        HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
+      else
+        HIPC(ctx->stage.d2h(hostp + hdr, nc * ostride, ctx->elim_out.p + hdr, nc * ostride, nc * ostride, 1,
+                            ctx->stream));
+      const int* cnt = reinterpret_cast<const int*>(hostp);
+      HostPool::get().run(nc, [&](size_t i) {
+        rlnc_decoder* d = ds[el[c0 + i]];
+        if (cnt[i] != (int)k) return;  // M singular: the host flush below
+        const uint8_t* st = tonly ? hostp + hdr + i * k * k : hostp + hdr + i * ostride;
+        const size_t sp = tonly ? k : opitch;
+        const bool ok = d->core.received() == 0
+                            ? (tonly ? d->core.load_inverse(st, sp) : d->core.load_rref(st, sp, k))
+                            : d->core.load_continued(st, sp, tonly);
+        if (ok) d->npend = 0;
+      });
+    }
+  }
+  for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
+  return RLNC_OK;
+}
+
 // The accessors observe kodr's state: queued AddPiece calls are eliminated
 // first (a host-only batch; the handle's observable state does not change).
 }  // extern "C"

@@ -150,3 +150,92 @@ def test_lazy_c2_piecewise(gpu_ctx):
     P = rng.integers(0, 256, (k, L), dtype=np.uint8)
     V, C = stream(rng, P, k + 2, "coded")
     run(gpu_ctx, P, V, C, lambda i: "dev", oracle_cols=1)
+
+
+def _feed(lib, dh, V, dbuf, pitch, idx):
+    st = []
+    for i in idx:
+        v = np.ascontiguousarray(V[i])
+        st.append(lib.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(U8P), V.shape[1], dbuf + i * pitch,
+                                                    pitch))
+    return st
+
+
+@pytest.mark.parametrize("k,L", [(16, 1024), (64, 4096), (256, 2048)])
+def test_grouped_flush_gpu_vs_host_flush(gpu_ctx, k, L):
+    """rlnc_decoders_flush_gpu: decoders fed one AddPiece per device piece
+    (lazy queues) are flushed together -- the queues that complete the rank
+    from kept rows on the GPU (fresh, or continued after a mid-stream read),
+    the others on the host -- and end exactly as twins whose own state reads
+    flush them on the host: counters, coefficients, transform, every later
+    AddPiece's return code and the decoded bytes; the coefficients also equal
+    the oracle's (decoder_state.go:15-182) fed the same pieces."""
+    lib = _lib.lib()
+    rng = np.random.default_rng(k + L)
+    # (stream kind, pieces fed, index of a mid-stream read or None)
+    plans = [("coded", k, None), ("coded", k, k // 3), ("quirky", k + 2, None), ("systematic", k, None),
+             ("coded", k - 3, None), ("dup", k + 1, k // 2), ("coded", k, 1), ("systematic", k, k // 2)]
+    pitch = L
+    gens, dec_g, dec_h, bufs = [], [], [], []
+    for kind, n, rd in plans:
+        P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        V, C = stream(rng, P, n, "coded" if kind == "dup" else kind)
+        if kind == "dup":  # a dependent piece before the read: not every row kept
+            V[rd - 1] = V[rd - 2]
+            C = oracle.encode(P, V)
+        d = gpu_ctx.alloc(n * pitch)
+        gpu_ctx.h2d(d, np.ascontiguousarray(C))
+        hs = []
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            errors.check(lib.rlnc_decoder_create(gpu_ctx.handle, k, ctypes.byref(h)))
+            hs.append(h)
+        gens.append((P, V, C, n, rd))
+        dec_g.append(hs[0])
+        dec_h.append(hs[1])
+        bufs.append(d)
+    try:
+        for gi, (P, V, C, n, rd) in enumerate(gens):
+            for dh in (dec_g[gi], dec_h[gi]):
+                if rd is None:
+                    st = _feed(lib, dh, V, bufs[gi], pitch, range(n))
+                else:
+                    st = _feed(lib, dh, V, bufs[gi], pitch, range(rd))
+                    lib.rlnc_decoder_useful(dh)  # a state read: the queue so far is eliminated (host)
+                    st += _feed(lib, dh, V, bufs[gi], pitch, range(rd, n))
+                od = oracle.Decoder(k)
+                assert st == [od.add(V[i], C[i]) for i in range(n)], gi
+        arr = (ctypes.c_void_p * len(gens))(*[h.value for h in dec_g])
+        errors.check(lib.rlnc_decoders_flush_gpu(arr, len(gens)))
+        for gi, (P, V, C, n, rd) in enumerate(gens):
+            a, b = dec_g[gi], dec_h[gi]
+            state = [(lib.rlnc_decoder_useful(h), lib.rlnc_decoder_received(h), lib.rlnc_decoder_required(h),
+                      bool(lib.rlnc_decoder_is_decoded(h))) for h in (a, b)]
+            assert state[0] == state[1], gi
+            u, r = state[0][0], state[0][1]
+            mats = []
+            for h in (a, b):
+                cf = np.empty((u, k), np.uint8)
+                tf = np.empty((u, r), np.uint8)
+                errors.check(lib.rlnc_decoder_coefficients(h, cf.ctypes.data_as(U8P)))
+                errors.check(lib.rlnc_decoder_transform(h, tf.ctypes.data_as(U8P)))
+                mats.append((cf, tf))
+            assert np.array_equal(mats[0][0], mats[1][0]) and np.array_equal(mats[0][1], mats[1][1]), gi
+            od = oracle.Decoder(k)
+            for i in range(n):
+                od.add(V[i], C[i])
+            assert np.array_equal(mats[0][0], od.coeffs()), gi
+            extra = rng.integers(0, 256, k, dtype=np.uint8)
+            piece = oracle.encode(P, extra[None, :])[0]
+            sts = [lib.rlnc_decoder_add_piece(h, extra.ctypes.data_as(U8P), k, piece.ctypes.data_as(U8P), L)
+                   for h in (a, b)]
+            assert sts[0] == sts[1] == od.add(extra, piece), gi
+            if od.is_decoded():
+                out = np.empty((k, L), np.uint8)
+                errors.check(lib.rlnc_decoder_get_pieces(a, out.ctypes.data_as(U8P)))
+                assert np.array_equal(out, P), gi
+    finally:
+        for h in dec_g + dec_h:
+            lib.rlnc_decoder_destroy(h)
+        for d in bufs:
+            gpu_ctx.free(d)
