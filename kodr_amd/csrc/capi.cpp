@@ -98,6 +98,7 @@ struct rlnc_ctx {
   bool elim_tab_ok = false;
   DevBuf elim_out;           // gf_elim's per-generation states and counts
   DevBuf elim_in;            // gf_elim's input for continued decoders: [coefficient rows ; vectors]
+  DevBuf gtab;               // grouped flush: source and destination tables of the gathered pieces
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
@@ -1958,8 +1959,9 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t cou
 // state of kept rows -- fresh (r = 0) or continued -- in one GPU launch per
 // kElimMaxGens, from M = [its r coefficient rows ; the queued vectors], all on
 // the host already (one upload); the others, and any singular M, through
-// the host flush their next state read would run.  Then every decoder's
-// borrowed device pieces are gathered.  Same state as G host flushes.
+// the host flush their next state read would run.  Every decoder's borrowed
+// device pieces are gathered by one launch beside the elimination.  Same
+// state as G host flushes.
 int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
   if (!ds || !G) return RLNC_ERR_INVALID_ARGUMENT;
   rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
@@ -1973,6 +1975,52 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
     if (std::adjacent_find(u.begin(), u.end()) != u.end()) return RLNC_ERR_INVALID_ARGUMENT;
   }
   TRY(set_dev(ctx));
+  // the borrowed device pieces of every decoder (of the first one's piece
+  // length) in ONE gather launch from uploaded source / destination tables,
+  // on the side stream beside the elimination
+  std::vector<const void*> gsrc, gdst;
+  size_t gL = 0;
+  for (size_t g = 0; g < G; g++) {
+    rlnc_decoder* d = ds[g];
+    if (d->pend_src.empty()) continue;
+    if (!gL) gL = d->L;
+    if (d->L != gL) continue;  // dec_flush below
+    const size_t m = d->pend_src.size(), r0 = d->pend_row0;
+    TRY(dec_reserve_rows(d, r0 + m, r0));
+    for (size_t j = 0; j < m; j++) {
+      gsrc.push_back(d->pend_src[j]);
+      gdst.push_back(d->recv.p + (r0 + j) * d->pitch);
+    }
+    d->pend_src.clear();
+  }
+  bool gjoined = true;
+  if (!gsrc.empty()) {
+    const size_t nr = gsrc.size();
+    std::vector<const void*> tab(gsrc);
+    tab.insert(tab.end(), gdst.begin(), gdst.end());
+    ctx->gtab.bind(ctx->device, ctx->stream);
+    TRY(ctx->gtab.reserve(tab.size() * sizeof(void*)));
+    const size_t tb = tab.size() * sizeof(void*);
+    HIPC(ctx->stage.h2d(ctx->gtab.p, tb, reinterpret_cast<const uint8_t*>(tab.data()), tb, tb, 1, ctx->stream));
+    hipStream_t gs = ctx->stream;
+    if (add_side_stream()) {
+      TRY(ctx_side(ctx));
+      HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the tables and any grown receive buffers first
+      HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
+      gs = ctx->side;
+      gjoined = false;
+    }
+    const auto* src = reinterpret_cast<const uint8_t* const*>(ctx->gtab.p);
+    const auto* dst = reinterpret_cast<uint8_t* const*>(ctx->gtab.p + nr * sizeof(void*));
+    for (size_t r0 = 0; r0 < nr; r0 += 65535)
+      HIPC(kodr_amd::gather_rows(src + r0, nullptr, 0, std::min<size_t>(65535, nr - r0), gL, gs, dst + r0));
+    if (!gjoined) HIPC(hipEventRecord(ctx->side_done, ctx->side));
+  }
+  auto join = [&]() -> int {  // everything after this point on the context stream sees the gathered rows
+    if (!gjoined) HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));
+    gjoined = true;
+    return RLNC_OK;
+  };
   std::vector<size_t> el;
   for (size_t g = 0; g < G; g++) {
     const rlnc_decoder* d = ds[g];
@@ -2013,6 +2061,7 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
       a.k = (int)k;
       HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
+      TRY(join());
       const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
       if (tonly)
@@ -2033,6 +2082,7 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       });
     }
   }
+  TRY(join());
   for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   return RLNC_OK;
 }
