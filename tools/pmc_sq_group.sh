@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of the grouped headline launch (bench.py --no-extras: every
+# SQ counters of the grouped headline launch (bench.py --no-extras --no-encode-decode: every
 # gf_bs_kernel<.., true> launch in the run is a headline launch), two --pmc
 # passes without tracing domains, averaged per launch by tools/pmc_sq.py.
 set -uo pipefail
@@ -13,6 +13,6 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P -d "$OUT/p$i" -o run --output-format csv -- python3 "$R/bench.py" \
-    --steps 20 --warmup 5 --no-extras --no-cpu-baseline > "$OUT/p$i.log" 2>&1 || { tail -5 "$OUT/p$i.log"; exit 1; }
+    --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-encode-decode > "$OUT/p$i.log" 2>&1 || { tail -5 "$OUT/p$i.log"; exit 1; }
 done
 python3 "$R/tools/pmc_sq.py" "$OUT" "true>" | tee "$OUT/summary.txt"
