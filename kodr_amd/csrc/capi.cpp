@@ -100,6 +100,7 @@ struct rlnc_ctx {
   DevBuf elim_in;            // gf_elim's input for continued decoders: [coefficient rows ; vectors]
   DevBuf gtab;               // grouped flush: source and destination tables of the gathered pieces
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
+  std::vector<uint8_t> elim_hin;   // host side of elim_in (grown once)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
@@ -1827,7 +1828,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
   uint8_t* const hostp = ctx->elim_host.data();
   bool copies_out = !side;
-  std::vector<uint8_t> hm;
+  std::vector<uint8_t>& hm = ctx->elim_hin;
   // chunks never mix fresh and continued decoders (one vector pitch per launch)
   for (size_t c0 = 0; c0 < gpu.size();) {
     const bool cont = c0 >= nfresh;
@@ -1842,15 +1843,39 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       // M of each decoder (k x k at pitch k): its coefficient rows, in row
       // order, in one upload for the chunk, then the batch's first k - r
       // vectors (device to device) below them
-      hm.resize(nc * k * k);
+      if (hm.size() < nc * k * k) hm.resize(nc * k * k);  // rows past r: overwritten on the device below
       HostPool::get().run(nc, [&](size_t i) {
         const rlnc_decoder* d = ds[gpu[c0 + i]];
         for (size_t j = 0; j < base[gpu[c0 + i]]; j++) memcpy(hm.data() + (i * k + j) * k, d->core.coeff_row(j), k);
       });
       HIPC(ctx->stage.h2d(ctx->elim_in.p, k, hm.data(), k, k, nc * k, ctx->stream));
-      for (size_t i = 0; i < nc; i++) {
-        const size_t g = gpu[c0 + i], r = base[g];
-        HIPC(kodr_amd::copy_rows(rows[g], pitch, ctx->elim_in.p + (i * k + r) * k, k, k - r, k, ctx->stream));
+      // the vectors: one gather launch over all decoders of the chunk from
+      // uploaded row tables when every row is 16-byte aligned, else a copy
+      // per decoder
+      bool aligned = k % 16 == 0 && pitch % 16 == 0;
+      for (size_t i = 0; i < nc && aligned; i++) aligned = (uintptr_t)rows[gpu[c0 + i]] % 16 == 0;
+      if (aligned) {
+        std::vector<const void*> tab;
+        for (int half = 0; half < 2; half++)
+          for (size_t i = 0; i < nc; i++) {
+            const size_t g = gpu[c0 + i], r = base[g];
+            for (size_t j = 0; j < k - r; j++)
+              tab.push_back(half ? (const void*)(ctx->elim_in.p + (i * k + r + j) * k)
+                                 : (const void*)(rows[g] + j * pitch));
+          }
+        const size_t nr = tab.size() / 2, tb = tab.size() * sizeof(void*);
+        ctx->gtab.bind(ctx->device, ctx->stream);
+        TRY(ctx->gtab.reserve(tb));
+        HIPC(ctx->stage.h2d(ctx->gtab.p, tb, reinterpret_cast<const uint8_t*>(tab.data()), tb, tb, 1, ctx->stream));
+        const auto* src = reinterpret_cast<const uint8_t* const*>(ctx->gtab.p);
+        const auto* dst = reinterpret_cast<uint8_t* const*>(ctx->gtab.p + nr * sizeof(void*));
+        for (size_t r0 = 0; r0 < nr; r0 += 65535)
+          HIPC(kodr_amd::gather_rows(src + r0, nullptr, 0, std::min<size_t>(65535, nr - r0), k, ctx->stream, dst + r0));
+      } else {
+        for (size_t i = 0; i < nc; i++) {
+          const size_t g = gpu[c0 + i], r = base[g];
+          HIPC(kodr_amd::copy_rows(rows[g], pitch, ctx->elim_in.p + (i * k + r) * k, k, k - r, k, ctx->stream));
+        }
       }
     }
     a.vpitch = cont ? k : pitch;
@@ -2037,7 +2062,8 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
     TRY(ctx->elim_in.reserve(chunk * k * k));
     if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
     uint8_t* const hostp = ctx->elim_host.data();
-    std::vector<uint8_t> hm(chunk * k * k);
+    std::vector<uint8_t>& hm = ctx->elim_hin;  // grown once per context, never zero-filled again
+    if (hm.size() < chunk * k * k) hm.resize(chunk * k * k);
     for (size_t c0 = 0; c0 < el.size(); c0 += chunk) {
       const size_t nc = std::min(chunk, el.size() - c0);
       kodr_amd::ElimArgs a = {};

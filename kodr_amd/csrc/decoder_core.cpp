@@ -802,14 +802,19 @@ bool DecoderCore::load_continued(const uint8_t* state, size_t pitch, bool invers
   for (size_t m = 0; m < r; m++) tr[m] = rows_[m] + k;  // T_r, row m of M
   const size_t w = k + c;
   std::vector<uint8_t> buf(c * w, 0);
+  const size_t f0 = inverse ? 0 : k;  // F's offset in a state row
   for (size_t i = 0; i < c; i++) {
     uint8_t* o = buf.data() + i * w;
-    const uint8_t* s = state + i * pitch;
-    const uint8_t* f = inverse ? s : s + k;
+    const uint8_t* f = state + i * pitch + f0;
     if (inverse) o[i] = 1;
-    else memcpy(o, s, k);
-    hostgf::accumulate(o + k, tr.data(), f, r, r);  // F[:, :r] x T_r
-    memcpy(o + k + r, f + r, c - r);                 // the batch's columns
+    else memcpy(o, state + i * pitch, k);
+    memcpy(o + k + r, f + r, c - r);  // the batch's columns
+  }
+  for (size_t i = 0; i < c; i += 4) {  // F[:, :r] x T_r, four output rows per pass over T_r
+    const size_t np = std::min<size_t>(4, c - i);
+    uint8_t* v[4];
+    for (size_t p = 0; p < np; p++) v[p] = buf.data() + (i + p) * w + k;
+    hostgf::accumulate_multi(v, np, tr.data(), state + i * pitch + f0, pitch, r, r);
   }
   for (uint8_t* row : rows_) free_.push_back(row);
   rows_.clear();
