@@ -255,3 +255,17 @@ class _Decoder:
     def bind_output(self, d_out, pitch):
         """Decoded pieces land at row j of the device buffer d_out (None unbinds)."""
         errors.check(lib().rlnc_decoder_bind_output(self._h, None if d_out is None else ctypes.c_void_p(d_out), pitch))
+
+
+def flush_decoders(decoders):
+    """Extension (no kodr counterpart): the pending AddPiece calls of many
+    decoders (one context, one piece count), eliminated together -- every
+    queue that completes its decoder's rank in one GPU launch
+    (rlnc_decoders_flush_gpu), the rest as each decoder's next read would.
+    A receiver keeping kodr's one-AddPiece-per-piece loop calls it once per
+    tick; the decoders' observable state is the same either way."""
+    decoders = list(decoders)
+    if not decoders:
+        return
+    arr = (ctypes.c_void_p * len(decoders))(*[d._h.value for d in decoders])
+    errors.check(lib().rlnc_decoders_flush_gpu(arr, len(decoders)))

@@ -4,7 +4,7 @@ return value or a raised kodr_amd.errors.Err* exception."""
 import ctypes
 
 from . import errors
-from ._codec import FULL, _Decoder, _Encoder, _Recoder
+from ._codec import FULL, _Decoder, _Encoder, _Recoder, flush_decoders  # noqa: F401 (extension)
 from ._lib import lib, u8
 from .device import default_context
 

@@ -275,3 +275,24 @@ def test_minimal_shapes(gpu_ctx):
     while not dec.IsDecoded():
         dec.AddPiece(enc.CodedPiece())
     assert b"".join(dec.GetPieces()) == data
+
+
+def test_flush_decoders_groups_piecewise_feeds(gpu_ctx):
+    # kodr's decoder loop (full/decoder_test.go:20-40: AddPiece per coded
+    # piece) on several generations at once, their queued eliminations run
+    # together by full.flush_decoders (rlnc_decoders_flush_gpu); the counters,
+    # the refusal once decoded and GetPieces are kodr's
+    rng = np.random.default_rng(5)
+    k = 32
+    gens = [gen_pieces(rng, k, 1024 + 16 * g) for g in range(4)]
+    encs = [full.NewFullRLNCEncoder(p, rng=rng_bytes(rng)) for p in gens]
+    decs = [full.NewFullRLNCDecoder(k) for _ in gens]
+    for i in range(k):
+        for e, d in zip(encs, decs):
+            d.AddPiece(e.CodedPiece())
+    full.flush_decoders(decs)
+    for e, d, p in zip(encs, decs, gens):
+        assert d.IsDecoded() and d.Required() == 0
+        with pytest.raises(errors.ErrAllUsefulPiecesReceived):
+            d.AddPiece(e.CodedPiece())
+        assert d.GetPieces() == [bytes(x) for x in p]
