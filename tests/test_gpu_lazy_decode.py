@@ -239,3 +239,40 @@ def test_grouped_flush_gpu_vs_host_flush(gpu_ctx, k, L):
             lib.rlnc_decoder_destroy(h)
         for d in bufs:
             gpu_ctx.free(d)
+
+
+def test_grouped_flush_more_decoders_than_one_launch(gpu_ctx):
+    """70 decoders (more than the elimination's 64 generations per launch):
+    two launches, every queue eliminated and every piece gathered."""
+    lib = _lib.lib()
+    rng = np.random.default_rng(70)
+    k, L, G = 8, 64, 70
+    Ps = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    Vs = []
+    for _ in range(G):
+        while True:  # an invertible coding matrix, so every queue completes the rank
+            V = rng.integers(0, 256, (k, k), dtype=np.uint8)
+            od = oracle.Decoder(k)
+            if all(od.add(V[i], np.zeros(1, np.uint8)) == 0 for i in range(k)) and od.is_decoded():
+                break
+        Vs.append(V)
+    rows = np.concatenate([oracle.encode(P, V) for P, V in zip(Ps, Vs)])
+    d = gpu_ctx.alloc(rows.nbytes)
+    gpu_ctx.h2d(d, np.ascontiguousarray(rows))
+    hs = []
+    try:
+        for g in range(G):
+            h = ctypes.c_void_p()
+            errors.check(lib.rlnc_decoder_create(gpu_ctx.handle, k, ctypes.byref(h)))
+            hs.append(h)
+            assert _feed(lib, h, Vs[g], d + g * k * L, L, range(k)) == [0] * k
+        errors.check(lib.rlnc_decoders_flush_gpu((ctypes.c_void_p * G)(*[h.value for h in hs]), G))
+        for g, h in enumerate(hs):
+            assert lib.rlnc_decoder_is_decoded(h)
+            out = np.empty((k, L), np.uint8)
+            errors.check(lib.rlnc_decoder_get_pieces(h, out.ctypes.data_as(U8P)))
+            assert np.array_equal(out, Ps[g]), g
+    finally:
+        for h in hs:
+            lib.rlnc_decoder_destroy(h)
+        gpu_ctx.free(d)
