@@ -2004,17 +2004,21 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
   // length) in ONE gather launch from uploaded source / destination tables,
   // on the side stream beside the elimination
   std::vector<const void*> gsrc, gdst;
+  std::vector<rlnc_decoder*> gdec;
   size_t gL = 0;
   for (size_t g = 0; g < G; g++) {
     rlnc_decoder* d = ds[g];
     if (d->pend_src.empty()) continue;
     if (!gL) gL = d->L;
     if (d->L != gL) continue;  // dec_flush below
-    const size_t m = d->pend_src.size(), r0 = d->pend_row0;
-    TRY(dec_reserve_rows(d, r0 + m, r0));
-    for (size_t j = 0; j < m; j++) {
+    TRY(dec_reserve_rows(d, d->pend_row0 + d->pend_src.size(), d->pend_row0));
+    gdec.push_back(d);
+  }
+  // every receive buffer is in place: the queues move into the tables
+  for (rlnc_decoder* d : gdec) {
+    for (size_t j = 0; j < d->pend_src.size(); j++) {
       gsrc.push_back(d->pend_src[j]);
-      gdst.push_back(d->recv.p + (r0 + j) * d->pitch);
+      gdst.push_back(d->recv.p + (d->pend_row0 + j) * d->pitch);
     }
     d->pend_src.clear();
   }
