@@ -44,3 +44,18 @@ def test_host_pool_runs_every_task_once():
         r = subprocess.run([exe], capture_output=True, text=True, timeout=120,
                            env={**os.environ, "KODR_HOST_THREADS": threads})
         assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout + r.stderr
+
+
+def test_decoder_core_continued_state():
+    """DecoderCore::load_continued (the continued decoders of the batched GPU
+    AddPiece and of the grouped flush) against kodr's route row by row, on the
+    CPU: k = 2..256, r = 1..k-1 held rows (dense, a systematic prefix, and a
+    dependent row that must be refused), M^-1 given alone or as whole state
+    rows at a padded pitch."""
+    src = os.path.join(ROOT, "tests", "cpp", "core_continued_test.cpp")
+    core = os.path.join(ROOT, "kodr_amd", "csrc", "decoder_core.cpp")
+    exe = os.path.join(ROOT, "tests", "cpp", "core_continued_test")
+    r = subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", src, core, "-o", exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok (0 failures)" in r.stdout, r.stdout + r.stderr[-3000:]
