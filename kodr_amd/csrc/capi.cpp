@@ -1988,8 +1988,8 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t cou
 // device pieces are gathered by one launch beside the elimination.  Same
 // state as G host flushes.
 int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
-  if (!ds || !G) return RLNC_ERR_INVALID_ARGUMENT;
-  rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
+  if (!ds || !G || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_ctx* ctx = ds[0]->ctx;
   if (!ctx) return RLNC_ERR_NO_DEVICE;
   const size_t k = ds[0]->core.piece_count();
   for (size_t g = 0; g < G; g++)

@@ -437,3 +437,18 @@ def test_grouped_entry_points_argument_checks():
     b.add(np.array([1, 1], np.uint8))
     b.add(np.array([0, 1], np.uint8))
     assert L.rlnc_decoders_get_pieces_device(both, 2, buf, 16) == -4  # coefficient-side decoders: no device
+
+
+def test_grouped_flush_argument_checks():
+    # rlnc_decoders_flush_gpu rejects bad arguments before any device work
+    # (no decoders, a null handle); coefficient-side decoders (no context)
+    # have no device to eliminate on, and keep their state
+    L = _lib.lib()
+    vp = ctypes.c_void_p
+    assert L.rlnc_decoders_flush_gpu(None, 1) == -1
+    assert L.rlnc_decoders_flush_gpu((vp * 1)(None), 1) == -1
+    a = CoreDecoder(4)
+    a.add(np.array([1, 2, 3, 4], np.uint8))
+    assert L.rlnc_decoders_flush_gpu((vp * 1)(a.h.value), 0) == -1
+    assert L.rlnc_decoders_flush_gpu((vp * 1)(a.h.value), 1) == -4   # no context: no device
+    assert a.state() == (1, 1, 3, False)                              # and nothing changed
