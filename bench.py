@@ -579,7 +579,7 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
         errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
         t0 = time.perf_counter()
         for i in range(n):
-            st = L_.rlnc_decoder_add_piece_device(dh, vptr[i], k, pptr[i], L)
+            st = L_.rlnc_decoder_add_piece_device_borrowed(dh, vptr[i], k, pptr[i], L)
             if st == 3:
                 break
             errors.check(st)
@@ -1031,7 +1031,7 @@ def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
 def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
     """C2 fed the way kodr's decoder is (one AddPiece per piece,
     full/decoder.go:50-66), for every resident generation at once: G decoders
-    take k device wire rows each, round-robin, one rlnc_decoder_add_piece_device
+    take k device wire rows each, round-robin, one rlnc_decoder_add_piece_device_borrowed
     call per piece (lazy AddPiece queues them), then the queues are eliminated
     either by ONE rlnc_decoders_flush_gpu call (GPU elimination) or by each
     decoder's own state read (host); two more pieces per generation follow
@@ -1057,7 +1057,7 @@ def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
                 errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
                 decs.append(h)
             darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
-            add = L_.rlnc_decoder_add_piece_device
+            add = L_.rlnc_decoder_add_piece_device_borrowed
             args = [(decs[g], vec[g * n + i].ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), dW + (g * n + i) * W + k)
                     for i in range(n) for g in range(G)]
             ctx.synchronize()

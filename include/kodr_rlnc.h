@@ -256,22 +256,28 @@ int rlnc_decoder_destroy(rlnc_decoder* dec);
  * first piece; a different length is RLNC_ERR_INVALID_ARGUMENT). */
 int rlnc_decoder_add_piece(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                            const uint8_t* piece, size_t piece_len);
-/* same, with the piece bytes already on the device.  Under the LAZY policy
- * (the default) a 16-byte aligned d_piece is BORROWED: the decoder reads it
- * on the context stream at its next data flush -- the next GetPiece/GetPieces/
- * get_decoded/bind_output/set_policy/batched AddPiece call, or once 1024
- * pieces are queued -- so the caller keeps those bytes unchanged until then
- * (kodr's own decoder keeps the caller's CodedPiece for good,
- * decoder_state.go:205-208).  Unaligned pieces, and every piece under EAGER,
- * are copied D2D in the call (async).
- * Lazy elimination (both entry points): while the queued rows cannot complete
- * the rank (useful + queued < piece_count) AddPiece only queues the coding
- * vector; the queue goes through kodr's elimination as one batch when any
- * accessor (is_decoded, required, useful, coefficients, GetPiece...) or a
+/* same, with the piece bytes already on the device: the piece is copied D2D
+ * on the context stream in the call (async), so the caller may reuse d_piece
+ * for work queued on that stream after this call.
+ * Lazy elimination (every AddPiece entry point): while the queued rows cannot
+ * complete the rank (useful + queued < piece_count) AddPiece only queues the
+ * coding vector; the queue goes through kodr's elimination as one batch when
+ * any accessor (is_decoded, required, useful, coefficients, GetPiece...) or a
  * later AddPiece needs the state.  Every return code and every value an
  * accessor returns is exactly kodr's after the same calls. */
 int rlnc_decoder_add_piece_device(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
                                   const uint8_t* d_piece, size_t piece_len);
+/* same, BORROWING the piece (opt-in; no kodr counterpart beyond kodr keeping
+ * the caller's CodedPiece for good, decoder_state.go:205-208): under the LAZY
+ * policy a 16-byte aligned d_piece is not copied in the call; the decoder
+ * reads it on the context stream at its next data flush -- the next GetPiece/
+ * GetPieces/get_decoded/bind_output/set_policy/batched AddPiece/
+ * rlnc_decoders_flush_gpu call, or once 1024 pieces are queued -- so the
+ * caller keeps those bytes unchanged until then.  Many pieces then cost one
+ * gather launch instead of a copy each.  Unaligned pieces, and every piece
+ * under EAGER, are copied in the call as above. */
+int rlnc_decoder_add_piece_device_borrowed(rlnc_decoder* dec, const uint8_t* vector, size_t vector_len,
+                                           const uint8_t* d_piece, size_t piece_len);
 /* batch AddPiece over `count` wire rows (vector ++ piece, as CodedPiece.Flatten,
  * kodr_internals/coded.go) at row pitch `pitch` >= piece_count + piece_len,
  * on the host or the device (is_device).  piece_len follows AddPiece's rule
@@ -314,6 +320,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint
  * take the host flush.  Queued device pieces are gathered as well.  The
  * state afterwards is the one the individual state reads would leave. */
 int rlnc_decoders_flush_gpu(rlnc_decoder* const* decs, size_t G);
+/* State reads.  is_decoded, required, useful, coefficients, transform and
+ * decoded_mask first run the decoder's queued (lazy) AddPiece calls through
+ * the elimination, so although they take a const handle they modify its
+ * internal state: like every other call on one decoder (kodr's objects are not
+ * goroutine-safe either), they must not run concurrently on the same handle. */
 int rlnc_decoder_is_decoded(const rlnc_decoder* dec);        /* IsDecoded :32-34 */
 size_t rlnc_decoder_required(const rlnc_decoder* dec);       /* Required  :38-40 */
 size_t rlnc_decoder_useful(const rlnc_decoder* dec);         /* rank */

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rlnc_decoder_destroy": (_int, [_vp]),
     "rlnc_decoder_add_piece": (_int, [_vp, _u8p, _sz, _u8p, _sz]),
     "rlnc_decoder_add_piece_device": (_int, [_vp, _u8p, _sz, _vp, _sz]),
+    "rlnc_decoder_add_piece_device_borrowed": (_int, [_vp, _u8p, _sz, _vp, _sz]),
     "rlnc_decoder_add_pieces": (_int, [_vp, _vp, _sz, _sz, _sz, _int, _szp]),
     "rlnc_decoder_add_pieces_gpu": (_int, [_vp, _vp, _sz, _sz, _sz, _szp]),
     "rlnc_decoder_set_policy": (_int, [_vp, _int]),

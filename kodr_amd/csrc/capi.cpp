@@ -406,6 +406,17 @@ int upload_generation(rlnc_encoder* e, const uint8_t* data, size_t len) {
 
 }  // namespace
 
+// runs f on every exit from a scope (error returns included)
+template <class F>
+struct ScopeExit {
+  F f;
+  ~ScopeExit() { f(); }
+};
+template <class F>
+ScopeExit<F> on_scope_exit(F f) {
+  return ScopeExit<F>{f};
+}
+
 extern "C" {
 
 const char* rlnc_version(void) { return "kodr_amd 0.1.0 (gfx950)"; }
@@ -1369,8 +1380,11 @@ int dec_flush(rlnc_decoder* d) {
   return RLNC_OK;
 }
 
+// borrow: the caller keeps a device piece's bytes unchanged until the next
+// data flush (rlnc_decoder_add_piece_device_borrowed); otherwise the piece is
+// copied in the call
 int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece, size_t plen,
-            bool dev) {
+            bool dev, bool borrow) {
   if (!d) return RLNC_ERR_INVALID_ARGUMENT;
   const size_t k = d->core.piece_count();
   // the queue could complete the rank: observe the state (full/decoder.go:52-54)
@@ -1385,7 +1399,7 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
     memcpy(d->pend_v.data() + d->npend * k, vec, k);
     d->npend++;
     if (!d->ctx) return RLNC_OK;
-    if (dev && (uintptr_t)piece % 16 == 0) {  // borrowed until the next data flush
+    if (dev && borrow && (uintptr_t)piece % 16 == 0) {  // borrowed until the next data flush
       if (d->pend_src.empty()) d->pend_row0 = row;
       d->pend_src.push_back(piece);
       if (d->pend_src.size() >= kPendMax) TRY(dec_flush_data(d));
@@ -1568,12 +1582,17 @@ int dec_materialize(rlnc_decoder* d) {
 
 int rlnc_decoder_add_piece(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* piece,
                            size_t plen) {
-  return dec_add(d, vec, vlen, piece, plen, false);
+  return dec_add(d, vec, vlen, piece, plen, false, false);
 }
 
 int rlnc_decoder_add_piece_device(rlnc_decoder* d, const uint8_t* vec, size_t vlen,
                                   const uint8_t* d_piece, size_t plen) {
-  return dec_add(d, vec, vlen, d_piece, plen, true);
+  return dec_add(d, vec, vlen, d_piece, plen, true, false);
+}
+
+int rlnc_decoder_add_piece_device_borrowed(rlnc_decoder* d, const uint8_t* vec, size_t vlen,
+                                           const uint8_t* d_piece, size_t plen) {
+  return dec_add(d, vec, vlen, d_piece, plen, true, true);
 }
 
 namespace {
@@ -1684,7 +1703,10 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
     vpitch = k;
   }
   BatchCopy bc;
-  TRY(dec_batch_pre(d, rows, count, pitch, dev, &bc));
+  if (const int e = dec_batch_pre(d, rows, count, pitch, dev, &bc)) {
+    if (vticket >= 0) d->ctx->stage.d2h_small_cancel(vticket);  // else every later small download fails
+    return e;
+  }
   if (vticket >= 0) HIPC(d->ctx->stage.d2h_small_end(vticket, d->hvecs.data(), k, k, count));
   // coefficient side, exactly as repeated AddPiece calls
   size_t n = 0;
@@ -1805,6 +1827,15 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   } else {
     TRY(launch_copies());
   }
+  bool copies_out = !side;
+  // an error return before the copies went out still launches them (the
+  // decoders' row bookkeeping assumes them) and joins the side stream
+  auto copies_guard = on_scope_exit([&] {
+    if (copies_out) return;
+    (void)launch_copies();
+    (void)hipEventRecord(ctx->side_done, ctx->side);
+    (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
+  });
   if (timing) tt1 = tnow();
   if (gpu.empty()) return RLNC_OK;
   // fresh decoders first (their launches read the rows' vectors in place),
@@ -1827,7 +1858,6 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   // only what the kernel wrote is read back: no zero-fill, grown once per context
   if (ctx->elim_host.size() < hdr + chunk * ostride) ctx->elim_host.resize(hdr + chunk * ostride);
   uint8_t* const hostp = ctx->elim_host.data();
-  bool copies_out = !side;
   std::vector<uint8_t>& hm = ctx->elim_hin;
   // chunks never mix fresh and continued decoders (one vector pitch per launch)
   for (size_t c0 = 0; c0 < gpu.size();) {
@@ -2023,6 +2053,11 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
     d->pend_src.clear();
   }
   bool gjoined = true;
+  // an error return joins too: the context stream must not run past a gather
+  // that still reads gtab and writes receive rows
+  auto join_guard = on_scope_exit([&] {
+    if (!gjoined) (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
+  });
   if (!gsrc.empty()) {
     const size_t nr = gsrc.size();
     std::vector<const void*> tab(gsrc);

@@ -88,12 +88,18 @@ class Staging {
     return hipSuccess;
   }
   hipError_t d2h_small_end(int b, uint8_t* dst, size_t dpitch, size_t width, size_t height) {
+    reserved_[b] = false;  // released on every path (the event still orders the chunk's next use)
     hipError_t e = hipEventSynchronize(ev_[b]);
     if (e != hipSuccess) return e;
     pending_[b] = false;
-    reserved_[b] = false;
     pack(dst, dpitch, buf_[b], width, width, height);
     return hipSuccess;
+  }
+
+  // drop a ticket whose download will not be unpacked (an error between
+  // begin and end): the chunk is free again once its event has passed
+  void d2h_small_cancel(int b) {
+    if (b >= 0 && b < 2) reserved_[b] = false;
   }
 
   hipError_t d2h(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,

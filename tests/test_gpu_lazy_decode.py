@@ -1,7 +1,8 @@
 """GPU parity of lazy AddPiece (capi.cpp dec_add): coding vectors that cannot
 complete the rank are queued and eliminated as one batch when the state is
 next observed, and device pieces are copied by one gather at the next data
-flush.  kodr's AddPiece (full/decoder.go:50-66, decoder_state.go:15-182) is
+flush (the opt-in borrowed entry point; the default one copies each piece in
+the call, so the caller may reuse its buffer at once).  kodr's AddPiece (full/decoder.go:50-66, decoder_state.go:15-182) is
 the reference: every call's return code, the counters whenever they are read,
 the coefficient state and the decoded bytes equal the oracle's
 (oracle/kodr_oracle.c, the literal restatement), for streams with dependent,
@@ -41,7 +42,9 @@ def stream(rng, P, n, kind):
 
 
 def run(ctx, P, V, C, place, reads=(), check_every=False, oracle_cols=None):
-    """Feed (V, C) piece by piece; place(i) -> 'dev', 'dev_misaligned' or 'host'.
+    """Feed (V, C) piece by piece; place(i) -> 'dev' (borrowed), 'dev_copy'
+    (rlnc_decoder_add_piece_device: copied in the call), 'dev_misaligned' or
+    'host'.
     reads: indices after which useful()/required() and a GetPiece are read.
     oracle_cols: feed the oracle only that many bytes of each piece (its
     coefficient side, all that return codes and counters depend on; the
@@ -70,7 +73,8 @@ def run(ctx, P, V, C, place, reads=(), check_every=False, oracle_cols=None):
                 st = lib.rlnc_decoder_add_piece(dh, v.ctypes.data_as(U8P), k, host[i].ctypes.data_as(U8P), L)
             else:
                 off = i * pitch + (1 if pl == "dev_misaligned" else 0)
-                st = lib.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(U8P), k, dbuf + off, L)
+                add = lib.rlnc_decoder_add_piece_device if pl == "dev_copy" else lib.rlnc_decoder_add_piece_device_borrowed
+                st = add(dh, v.ctypes.data_as(U8P), k, dbuf + off, L)
             ost = od.add(V[i], C[i] if oracle_cols is None else C[i][:oracle_cols])
             assert st == ost, (i, st, ost)
             if check_every or i in reads:
@@ -119,8 +123,37 @@ def test_lazy_mixed_placement_and_reads(gpu_ctx):
     k, L = 48, 3000
     P = rng.integers(0, 256, (k, L), dtype=np.uint8)
     V, C = stream(rng, P, k + 5, "quirky")
-    kinds = ["dev", "dev", "dev_misaligned", "host", "dev"]
-    run(gpu_ctx, P, V, C, lambda i: kinds[i % 5], reads=(4, 20, 47, 50))
+    kinds = ["dev", "dev", "dev_misaligned", "host", "dev", "dev_copy"]
+    run(gpu_ctx, P, V, C, lambda i: kinds[i % len(kinds)], reads=(4, 20, 47, 50))
+
+
+@pytest.mark.parametrize("k,L", [(16, 1024), (64, 4096)])
+def test_default_device_add_copies_in_call(gpu_ctx, k, L):
+    # rlnc_decoder_add_piece_device copies the piece in the call: ONE receive
+    # slot (as an RCCL receive buffer) is overwritten by the next piece, and
+    # finally by garbage, right after each call, on the context stream
+    lib = _lib.lib()
+    rng = np.random.default_rng(0xD0 + k)
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    V, C = stream(rng, P, k + 3, "quirky")
+    slot = gpu_ctx.alloc(L)
+    dh = ctypes.c_void_p()
+    errors.check(lib.rlnc_decoder_create(gpu_ctx.handle, k, ctypes.byref(dh)))
+    od = oracle.Decoder(k)
+    try:
+        for i in range(V.shape[0]):
+            gpu_ctx.h2d(slot, C[i])
+            v = np.ascontiguousarray(V[i])
+            st = lib.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(U8P), k, slot, L)
+            gpu_ctx.h2d(slot, np.full(L, 0xA5, np.uint8))
+            assert st == od.add(V[i], C[i]), i
+        assert lib.rlnc_decoder_is_decoded(dh)
+        out = np.empty((k, L), np.uint8)
+        errors.check(lib.rlnc_decoder_get_pieces(dh, out.ctypes.data_as(U8P)))
+        assert np.array_equal(out, P)
+    finally:
+        lib.rlnc_decoder_destroy(dh)
+        gpu_ctx.free(slot)
 
 
 def test_lazy_counters_every_call(gpu_ctx):
@@ -156,8 +189,8 @@ def _feed(lib, dh, V, dbuf, pitch, idx):
     st = []
     for i in idx:
         v = np.ascontiguousarray(V[i])
-        st.append(lib.rlnc_decoder_add_piece_device(dh, v.ctypes.data_as(U8P), V.shape[1], dbuf + i * pitch,
-                                                    pitch))
+        st.append(lib.rlnc_decoder_add_piece_device_borrowed(dh, v.ctypes.data_as(U8P), V.shape[1],
+                                                             dbuf + i * pitch, pitch))
     return st
 
 
