@@ -102,6 +102,8 @@ struct rlnc_ctx {
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
   std::vector<uint8_t> elim_hin;   // host side of elim_in (grown once)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
+  DevBuf elim_pub;           // gf_elim_mc's hand-off granules (zeroed when allocated)
+  uint32_t elim_epoch = 0;   // gf_elim_mc's launch tag, one per launch
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
 };
@@ -479,6 +481,7 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->stage.release();
   ctx->elim_tab.release();
   ctx->elim_out.release();
+  ctx->elim_pub.release();
   ctx->gtmat[0].release();
   ctx->gtmat[1].release();
   if (ctx->side) {
@@ -1746,6 +1749,50 @@ int ctx_elim_tables(rlnc_ctx* ctx) {
   return RLNC_OK;
 }
 
+// the multi-workgroup elimination's hand-off buffer for nc decoders and this
+// launch's epoch (a new tag per launch; the buffer is zeroed when it is
+// allocated and when the tags wrap)
+int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
+  const size_t bytes = kodr_amd::gf_elim_mc_pub_bytes((int)k, (int)nc);
+  ctx->elim_pub.bind(ctx->device, ctx->stream);
+  const uint8_t* before = ctx->elim_pub.p;
+  TRY(ctx->elim_pub.reserve(bytes));
+  const bool fresh = ctx->elim_pub.p != before || ctx->elim_epoch >= 0x7ffffff0u;
+  if (fresh) {
+    HIPC(hipMemsetAsync(ctx->elim_pub.p, 0, ctx->elim_pub.cap, ctx->stream));
+    ctx->elim_epoch = 0;
+  }
+  a->pub = reinterpret_cast<uint64_t*>(ctx->elim_pub.p);
+  a->epoch = ++ctx->elim_epoch;
+  return RLNC_OK;
+}
+
+// decoders per elimination launch: the multi-workgroup kernel needs all of a
+// launch's workgroups resident at once
+size_t elim_chunk(size_t k, size_t n) {
+  size_t c = std::min<size_t>(n, kodr_amd::kElimMaxGens);
+  if (k >= 2 && k <= 256) c = std::min<size_t>(c, kodr_amd::kElimMcMaxBlocks / kodr_amd::gf_elim_mc_groups((int)k));
+  return std::max<size_t>(c, 1);
+}
+
+// per decoder of a launch: the number of state rows the kernel left (counts
+// of the one-workgroup kernels; k when every workgroup of the multi-workgroup
+// kernel reports done, else 0)
+void elim_counts(const kodr_amd::ElimArgs& a, size_t nc, bool mc, const uint8_t* hdr, int* cnt) {
+  const int* c = reinterpret_cast<const int*>(hdr);
+  const int P = kodr_amd::gf_elim_mc_groups(a.k);
+  for (size_t i = 0; i < nc; i++) {
+    if (!mc) {
+      cnt[i] = c[i];
+      continue;
+    }
+    bool ok = true;
+    for (int q = 0; q < P; q++) ok = ok && c[i * P + q] == 1;
+    cnt[i] = ok ? a.k : 0;
+  }
+}
+constexpr size_t kElimHdr = 4 * kodr_amd::kElimMcMaxBlocks;  // counts / status words ahead of the states
+
 }  // namespace
 
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_t* const* rows,
@@ -1847,8 +1894,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   std::stable_partition(gpu.begin(), gpu.end(), [&](size_t g) { return base[g] == 0; });
   const size_t nfresh = (size_t)std::count_if(gpu.begin(), gpu.end(), [&](size_t g) { return base[g] == 0; });
   TRY(ctx_elim_tables(ctx));
-  const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
-  const size_t chunk = std::min<size_t>(gpu.size(), kodr_amd::kElimMaxGens);
+  const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = kElimHdr;
+  const size_t chunk = elim_chunk(k, gpu.size());
   ctx->elim_out.bind(ctx->device, ctx->stream);
   TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
   if (nfresh < gpu.size()) {  // continued decoders: their M, k x k each
@@ -1915,6 +1962,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.out_pitch = opitch;
     a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
     a.k = (int)k;
+    TRY(ctx_elim_mc(ctx, k, nc, &a));
+    const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nc);
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
       TRY(launch_copies());
@@ -1948,7 +1997,9 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     }
 #endif
     if (timing) tt3 = tnow();
-    const int* cnt = reinterpret_cast<const int*>(hostp);
+    std::vector<int> cntv(nc);
+    elim_counts(a, nc, mc, hostp, cntv.data());
+    const int* cnt = cntv.data();
     // the states into the decoders' host mirrors: independent per decoder,
     // memory-bound (a 256 x 520-byte arena each), so spread over host threads.
     // got[i] = rows of the batch accepted
@@ -2093,8 +2144,8 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
   }
   if (!el.empty()) {
     TRY(ctx_elim_tables(ctx));
-    const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = 256;
-    const size_t chunk = std::min<size_t>(el.size(), kodr_amd::kElimMaxGens);
+    const size_t opitch = k <= 128 ? 256 : 512, ostride = k * opitch, hdr = kElimHdr;
+    const size_t chunk = elim_chunk(k, el.size());
     ctx->elim_out.bind(ctx->device, ctx->stream);
     TRY(ctx->elim_out.reserve(hdr + chunk * ostride));
     ctx->elim_in.bind(ctx->device, ctx->stream);
@@ -2125,6 +2176,8 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       a.out_pitch = opitch;
       a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
       a.k = (int)k;
+      TRY(ctx_elim_mc(ctx, k, nc, &a));
+      const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nc);
       HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
       TRY(join());
       const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
@@ -2134,7 +2187,9 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       else
         HIPC(ctx->stage.d2h(hostp + hdr, nc * ostride, ctx->elim_out.p + hdr, nc * ostride, nc * ostride, 1,
                             ctx->stream));
-      const int* cnt = reinterpret_cast<const int*>(hostp);
+      std::vector<int> cntv(nc);
+      elim_counts(a, nc, mc, hostp, cntv.data());
+      const int* cnt = cntv.data();
       HostPool::get().run(nc, [&](size_t i) {
         rlnc_decoder* d = ds[el[c0 + i]];
         if (cnt[i] != (int)k) return;  // M singular: the host flush below

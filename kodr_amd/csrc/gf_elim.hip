@@ -707,6 +707,266 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
   if (tid == 0) args.counts[g] = c;
 }
 
+// ---- FULL batches on several workgroups per decoder ("mc") ---------------
+// One decoder's k <= 256 rows are split into P = ceil(k / 32) groups of 32
+// rows, a workgroup each (16 waves: rows 2w and 2w + 1, lane = dword), so the
+// k^3 GF MACs of the inversion run on P CUs instead of one.  Padded to
+// K' = 32 P with identity rows and columns, the matrix is inverted in place
+// by block Gauss-Jordan ("Y" form: after a group's step its 32 columns hold
+// the inverse-in-progress, the columns of later groups the reduced
+// coefficients; T columns are indexed by arrival, so the result is C^-1
+// itself, the state kodr reaches: [I | C^-1], see the FULL case above):
+//  * group q's step, by its own workgroup, in two 16-wide sub-panels: the
+//    16 x 16 block of the sub-panel's rows is inverted by panel_gj (S), the
+//    sub-panel's rows become S x (rows with the block replaced by I), and the
+//    other 16 rows drop the sub-panel columns (row ^= m x new rows).  The 32
+//    rows it ends with are group q's pivot rows N_q; they are published.
+//  * every other workgroup, for every group in order, takes N_q and drops
+//    group q's columns from its rows: m = the row's 32 bytes there, those
+//    bytes zeroed, row ^= m x N_q.
+// Hand-off (MI355X_MICROARCH.md, hand-off price list, granule form R2): N_q
+// goes out as 8-byte {data, tag} granules, each ONE agent-scope relaxed store
+// (global_store_dwordx2 sc1); a consumer re-reads its granules with sc1 loads
+// until every tag is this launch's epoch.  No fence, no flag.  A singular
+// block publishes its group with the FAIL bit; a workgroup that sees one
+// publishes its own group the same way (if it has not yet) and stops, so
+// every workgroup ends; spins are bounded.  Every workgroup writes its status
+// word (1 done, 0 failed) last.  All G * P workgroups must be resident at once
+// (kElimMcMaxBlocks, one 1024-thread workgroup per CU).
+constexpr int kMcWaves = 16;
+constexpr uint32_t kMcFail = 0x80000000u;
+constexpr int kMcSpinMax = 1 << 20;  // >= ~1 s of polling: only a lost workgroup gets there
+
+struct ElimMcLds {
+  uint4 tab[256 * 2];     // the [256][8]-dword tables as 16-byte rows (as ElimBlkLds)
+  uint32_t nq[32][64];    // a consumed group's pivot rows; in the own step, a sub-panel's new rows
+  uint32_t prow[16][64];  // the sub-panel's rows before the step
+  uint32_t pan[16][4];    // its 16 x 16 block
+  uint32_t sd[16][4];     // S = block^-1 by rows: S[c][u] = byte u % 4 of sd[c][u / 4]
+  int fail;               // 1 singular / FAIL seen, 2 timeout
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ void mc_tab(const ElimMcLds& lds, uint32_t f, uint4& t, uint32_t& t2) {
+  t = lds.tab[2 * f];
+  t2 = lds.tab[2 * f + 1].x;
+}
+__device__ __forceinline__ uint32_t mc_mul(const uint4& t, uint32_t t2, uint32_t s0, uint32_t s1, uint32_t s2) {
+  return __builtin_amdgcn_perm(t.y, t.x, s0) ^ __builtin_amdgcn_perm(t.w, t.z, s1) ^
+         __builtin_amdgcn_perm(t2, t2, s2);
+}
+
+// panel_gj for the mc layout: pan (16 x 16 block, written by other waves and
+// behind a barrier) -> sd = block^-1, or fail = 1.  One wave.
+__device__ __forceinline__ void mc_panel_gj(ElimMcLds& lds, cu32* tb, int lane) {
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t P = lds.pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
+  uint32_t used = 0;
+  int mycol = 0;
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const bool nz = (d == cd) && ((P >> cb) & 0xffu) != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) {
+      if (lane == 0) lds.fail = 1;
+      return;
+    }
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t dp = (__builtin_amdgcn_readlane(P, pl) >> cb) & 0xffu;
+    cu32* tinv = tb + kElimInvTables + dp * 8;  // tables of inv(dp) (gf256.go:77-86)
+    const uint4 ti = {tinv[0], tinv[1], tinv[2], tinv[3]};
+    const uint32_t ti2 = tinv[4];
+    if (t == tp) {
+      P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
+      Tr = gmul4(ti, ti2, sel0(Tr), sel1(Tr), sel2(Tr));
+      mycol = c;
+    }
+    const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
+    uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
+    if (t == tp) f = 0u;
+    uint4 tf;
+    uint32_t tf2;
+    mc_tab(lds, f, tf, tf2);
+    P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
+    Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
+    used |= 1u << tp;
+  }
+  lds.sd[mycol][d] = Tr;
+}
+
+__device__ __forceinline__ void mc_publish(gu64* dst, uint32_t tag, uint32_t r0, uint32_t r1) {
+  __hip_atomic_store(dst, ((unsigned long long)tag << 32) | r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(dst + 64, ((unsigned long long)tag << 32) | r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args) {
+  __shared__ ElimMcLds lds;
+  const int q = blockIdx.x, g = blockIdx.y, P = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = args.k;
+  const uint32_t epoch = args.epoch;
+  cu32* tb = (cu32*)args.tables;
+  gu64* pub = (gu64*)args.pub + (size_t)g * P * 32 * 64;
+
+  for (int i = tid; i < 256 * 2; i += 64 * kMcWaves)
+    lds.tab[i] = make_uint4(args.tables[4 * i], args.tables[4 * i + 1], args.tables[4 * i + 2], args.tables[4 * i + 3]);
+  if (tid == 0) lds.fail = 0;
+
+  // rows 32q + 2w + i: C (padded with identity rows and columns past k)
+  uint32_t R[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const int gr = 32 * q + 2 * w + i;
+    uint32_t v = 0;
+    if (gr < k) {
+      const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
+    } else if (gr >> 2 == lane) {
+      v = 1u << (8 * (gr & 3));
+    }
+    R[i] = v;
+  }
+  __syncthreads();
+
+  bool published = false;
+  for (int gp = 0; gp < P; gp++) {
+    if (gp == q) {
+      // ---- own step: two 16-wide sub-panels on this workgroup's rows ----
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const int db = 8 * q + 4 * s;  // the sub-panel's first dword (lane)
+        const bool blk = (w >> 3) == s;  // waves 8s .. 8s + 7 hold its rows
+        if (blk) {
+#pragma unroll
+          for (int i = 0; i < 2; i++) {
+            const int lr = 2 * (w - 8 * s) + i;
+            lds.prow[lr][lane] = R[i];
+            if (lane >= db && lane < db + 4) lds.pan[lr][lane - db] = R[i];
+          }
+        }
+        __syncthreads();
+        if (w == 0) mc_panel_gj(lds, tb, lane);
+        __syncthreads();
+        if (lds.fail) break;  // uniform
+        {  // new row c = w: sum_u S[c][u] x row u, the block replaced by S[c]
+          uint32_t acc = 0;
+#pragma unroll
+          for (int u4 = 0; u4 < 4; u4++) {
+            const uint32_t sw = __builtin_amdgcn_readfirstlane(lds.sd[w][u4]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const uint32_t x = lds.prow[4 * u4 + e][lane];
+              uint4 t;
+              uint32_t t2;
+              mc_tab(lds, (sw >> (8 * e)) & 0xffu, t, t2);
+              acc ^= mc_mul(t, t2, sel0(x), sel1(x), sel2(x));
+            }
+          }
+          if (lane >= db && lane < db + 4) acc = lds.sd[w][lane - db];
+          lds.nq[w][lane] = acc;
+        }
+        __syncthreads();
+        if (blk) {
+#pragma unroll
+          for (int i = 0; i < 2; i++) R[i] = lds.nq[2 * (w - 8 * s) + i][lane];
+        } else {
+          uint32_t F[2][4];
+#pragma unroll
+          for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int qd = 0; qd < 4; qd++) F[i][qd] = __builtin_amdgcn_readlane(R[i], db + qd);
+          if (lane >= db && lane < db + 4) R[0] = R[1] = 0;
+#pragma unroll
+          for (int c = 0; c < 16; c++) {
+            const uint32_t x = lds.nq[c][lane];
+            const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+              uint4 t;
+              uint32_t t2;
+              mc_tab(lds, (F[i][c >> 2] >> (8 * (c & 3))) & 0xffu, t, t2);
+              R[i] ^= mc_mul(t, t2, s0, s1, s2);
+            }
+          }
+        }
+        __syncthreads();
+      }
+      if (lds.fail) break;
+      mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch, R[0], R[1]);
+      published = true;
+      continue;
+    }
+    // ---- another group's pivot rows: take them, drop its columns ----
+    {
+      const gu64* src = pub + ((size_t)gp * 32 + 2 * w) * 64 + lane;
+      int spins = 0;
+      uint64_t a, b;
+      for (;;) {
+        a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ta = (uint32_t)(a >> 32), tb2 = (uint32_t)(b >> 32);
+        const bool ok = (ta & ~kMcFail) == epoch && (tb2 & ~kMcFail) == epoch;
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+          if (__builtin_amdgcn_ballot_w64(((ta | tb2) & kMcFail) != 0) && lane == 0) lds.fail = 1;
+          break;
+        }
+        if (++spins > kMcSpinMax) {
+          if (lane == 0) lds.fail = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      lds.nq[2 * w][lane] = (uint32_t)a;
+      lds.nq[2 * w + 1][lane] = (uint32_t)b;
+    }
+    __syncthreads();
+    if (lds.fail) break;  // uniform
+    {
+      const int db = 8 * gp;
+      uint32_t F[2][8];
+#pragma unroll
+      for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int qd = 0; qd < 8; qd++) F[i][qd] = __builtin_amdgcn_readlane(R[i], db + qd);
+      if (lane >= db && lane < db + 8) R[0] = R[1] = 0;
+#pragma unroll
+      for (int c = 0; c < 32; c++) {
+        const uint32_t x = lds.nq[c][lane];
+        const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          uint4 t;
+          uint32_t t2;
+          mc_tab(lds, (F[i][c >> 2] >> (8 * (c & 3))) & 0xffu, t, t2);
+          R[i] ^= mc_mul(t, t2, s0, s1, s2);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const bool ok = lds.fail == 0;
+  if (!ok && !published)  // a later group waits for this one: tell it
+    mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch | kMcFail, 0u, 0u);
+  if (ok) {  // T rows (pivot column order = row order), [C^-1] at byte k of each out row
+    uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      const int gr = 32 * q + 2 * w + i;
+      if (gr >= k) continue;
+      uint8_t* row = out + (size_t)gr * args.out_pitch + k;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(R[i] >> (8 * b));
+    }
+  }
+  __syncthreads();
+  if (tid == 0) args.counts[g * P + q] = ok ? 1 : 0;
+}
+
 }  // namespace
 
 void elim_tables(uint32_t* host_out) {
@@ -760,8 +1020,18 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   return full;
 }
 
+bool gf_elim_mc_taken(const ElimArgs& args, int G) {
+  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 1;  // A/B knob
+  return mc && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
+         G * gf_elim_mc_groups(args.k) <= kElimMcMaxBlocks;
+}
+
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
+  if (G <= kElimMaxGens && args.k >= 2 && args.k <= 256 && gf_elim_mc_taken(args, G)) {
+    hipLaunchKernelGGL(gf_elim_mc_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(64 * kMcWaves), 0, stream, args);
+    return hipGetLastError();
+  }
   if (G > kElimMaxGens || args.k < 2 || args.k > 256 || args.out_pitch % 4 ||
       args.out_pitch < (size_t)(args.k <= 128 ? 256 : 512))
     return hipErrorInvalidValue;

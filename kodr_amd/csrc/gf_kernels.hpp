@@ -103,6 +103,10 @@ struct ElimArgs {
   uint64_t out_gen_stride, out_pitch; // out_pitch >= 256 (k <= 128) or 512
   int* counts;
   int k;
+  // gf_elim_mc only: the hand-off buffer (gf_elim_mc_pub_bytes, zeroed once
+  // when allocated) and this launch's tag (1 .. 2^31 - 1, a new one per launch)
+  uint64_t* pub;
+  uint32_t epoch;
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;
@@ -112,6 +116,17 @@ void elim_tables(uint32_t* host_out);  // kElimTableWords dwords
 // then k (the state is [I | C^-1]: only T = C^-1 needs reading back) or 0
 bool gf_elim_blocked(const ElimArgs& args, int G);
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
+// Full batches on several workgroups per decoder (gf_elim_mc_kernel): the
+// rows of a decoder are split into groups of 32, one workgroup each, which
+// hand their pivot rows to each other through `pub`.  Taken by gf_elim for
+// full batches when args.pub is set and G * groups <= kElimMcMaxBlocks.
+// Instead of counts[g] it writes one status word per workgroup,
+// counts[g * groups + q] = 1 (done) or 0 (a singular block or a timeout: the
+// host then takes kodr's route); the decoder's T is valid when all are 1.
+constexpr int kElimMcMaxBlocks = 256;
+inline int gf_elim_mc_groups(int k) { return (k + 31) / 32; }
+inline size_t gf_elim_mc_pub_bytes(int k, int G) { return (size_t)G * gf_elim_mc_groups(k) * 32 * 64 * 8; }
+bool gf_elim_mc_taken(const ElimArgs& args, int G);
 
 // ---- bit-sliced path (gf_bs.hip) ----
 // dst = src with every 32-byte block of rows [0, rows) x [0, round_up(ncols,

@@ -206,10 +206,11 @@ def test_gpu_elimination_c2_round_trip(gpu_ctx):
     gpu_ctx.free(dDec)
 
 
-@pytest.mark.parametrize("k", [32, 48])
+@pytest.mark.parametrize("k", [32, 48, 256])
 def test_gpu_elimination_many_decoders(gpu_ctx, k):
     """More decoders than one launch takes (kElimMaxGens = 64, and as many
-    grouped row copies): full dense batches (blocked kernel), {0,1,2}-valued
+    grouped row copies; at k = 256 the multi-workgroup kernel's 32 decoders
+    of 8 workgroups each): full dense batches (blocked kernel), {0,1,2}-valued
     ones (zero diagonals, panel blocks that are singular while C is not: the
     host route), a panel-local dependence, and a few short batches; every
     decoder ends as rlnc_decoder_add_pieces leaves it, pieces included."""
