@@ -70,6 +70,68 @@ def cpu_baseline(seconds=10.0):
                       f"{os.cpu_count()} ({_cpu_model()})"}
 
 
+def cpu_baseline_decode(seconds=6.0, k=K_PIECES, L=L_BYTES, widths=(256, 1024)):
+    """kodr's decode of k + 2 coded pieces by oracle/ (decoder_state.go's
+    literal loops, full/decoder.go's AddPiece; one core) on column slices of a
+    32 MiB/256 generation.  Decode is column-separable (decoder_state.go:66-73,
+    105-112, 130-132: the data bytes of a column meet only that column), so a
+    slice of w columns does the whole coefficient side and w/L of the data
+    side: t(w) = a + b w, fitted at two widths (best of the repetitions that
+    fit in `seconds`), is evaluated at w = L."""
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(2)
+    n = k + 2
+    V = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    prev = os.sched_getaffinity(0)
+    core = min(prev)
+    os.sched_setaffinity(0, {core})
+    best = {}
+    try:
+        for w in widths:
+            P = rng.integers(0, 256, (k, w), dtype=np.uint8)
+            C = oracle.encode(P, V)
+            t_end, reps = time.perf_counter() + seconds / len(widths), 0
+            while reps < 2 or time.perf_counter() < t_end:
+                t0 = time.perf_counter()
+                d = oracle.Decoder(k)
+                for i in range(n):
+                    if d.add(V[i], C[i]) == 3:
+                        break
+                dt = time.perf_counter() - t0
+                assert d.is_decoded() and np.array_equal(np.stack([d.get_piece(i)[1] for i in range(k)]), P)
+                best[w] = min(best.get(w, dt), dt)
+                reps += 1
+    finally:
+        os.sched_setaffinity(0, prev)
+    (w1, w2) = widths
+    b = (best[w2] - best[w1]) / (w2 - w1)
+    a = best[w1] - b * w1
+    t_full = a + b * L
+    return {"decode_s": round(t_full, 4), "decode_MBps_decodable_len": round(k * (k + L) / t_full / 1e6, 3),
+            "coefficient_side_s": round(max(a, 0.0), 5), "per_column_s": float(f"{b:.4g}"),
+            "slice_s": {str(w): round(best[w], 5) for w in widths}, "cores": 1, "kind": "port",
+            "sample": f"oracle.Decoder (literal decoder_state.go) fed k + 2 = {n} coded pieces of 32MiB/256 "
+                      f"column slices of {widths[0]} and {widths[1]} bytes, best of the repetitions in "
+                      f"{seconds:.0f}s, pinned to core {core}; t(L) = a + b L extrapolated to L = {L} "
+                      f"(kodr publishes 13.07 s for this decode on an i7-1260P, README.md:142)"}
+
+
+def cpu_baseline_roundtrip(enc, dec, k=K_PIECES, L=L_BYTES):
+    """The encode+decode round trip of one generation on one core, from the
+    two samples: k + 2 coded pieces at the encode rate, then the decode;
+    kodr units as encode_decode.value."""
+    n = k + 2
+    t_enc = n * setbytes(k, L) / (enc["value"] * 1e6)
+    t = t_enc + dec["decode_s"]
+    units = n * setbytes(k, L) + k * (k + L)
+    return {"value": round(units / t / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": "port",
+            "roundtrip_s_per_generation": round(t, 4), "encode_s": round(t_enc, 4), "decode_s": dec["decode_s"],
+            "sample": "k + 2 coded pieces at cpu_baseline's oracle encode rate + cpu_baseline_decode's extrapolated "
+                      "oracle decode, one core; kodr units as encode_decode.value ((k+2) x SetBytes + DecodableLen "
+                      "per generation)", "decode_detail": dec}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -183,6 +245,171 @@ class HeadlineStep:
         self.ctx.free(self.dOut)
 
 
+class RoundTripStep:
+    """The metric's encode+decode (configs[1] encode + configs[2] decode) as a
+    timed step over the G resident generations, shared with
+    tests/test_gpu_headline.py (which runs it and compares every decoded
+    byte).  Coding vectors: nsets sets of n = k + 2 per generation drawn on
+    the host up front (kodr draws them per piece from crypto/rand,
+    data.go:90-95; fresh sets rotate between steps) and written into the
+    vector columns of nsets wire-row buffers (CodedPiece.Flatten layout,
+    data.go:52-57, pitch round_up(k + L, 256)).  A step:
+      1. ONE grouped encode launch (rlnc_encoder_group_coded_pieces_device,
+         gf_bs_kernel) writes the n coded pieces of every generation into
+         the piece columns of set i % nsets -- full/encoder.go:61-71 n times
+         per generation; HIP events around it;
+      2. G fresh decoders take their n wire rows in ONE batched AddPiece call
+         (rlnc_decoders_add_pieces_gpu: row copies + bit-sliced twin beside
+         the multi-workgroup elimination, gf_elim_mc_kernel) --
+         full/decoder.go:50-66 row by row, same state;
+      3. ONE grouped GetPieces (rlnc_decoders_get_pieces_device) writes the
+         G decoded generations to device memory; HIP events around it;
+      4. the decoders are destroyed (their buffers go back to the pool).
+    Decoder construction sits in the step (host only, microseconds); kodr's
+    decoder bench builds its decoder outside the timer
+    (benches/full/decoder_test.go:71-94)."""
+
+    def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2):
+        import ctypes
+        import numpy as np
+        self.ctx, self.L_, self.errors, self.encs = ctx, L_, errors, encs
+        self.k, self.L, self.G, self.n = k, L, len(encs), k + 2
+        self.W = (k + L + 255) // 256 * 256
+        G, n, W = self.G, self.n, self.W
+        self.V = rng.integers(0, 256, (nsets, G, n, k), dtype=np.uint8)
+        self.dV, self.dW = [], []
+        wire = np.zeros((G * n, W), np.uint8)
+        for s_ in range(nsets):
+            dv, dw = ctx.alloc(G * n * k), ctx.alloc(G * n * W)
+            ctx.h2d(dv, self.V[s_])
+            wire[:, :k] = self.V[s_].reshape(G * n, k)
+            ctx.h2d(dw, wire)
+            self.dV.append(dv)
+            self.dW.append(dw)
+        del wire
+        self.dO = ctx.alloc(G * k * L)
+        self.earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
+        self.rows = [(ctypes.c_void_p * G)(*[dw + g * n * W for g in range(G)]) for dw in self.dW]
+        self.counts = (ctypes.c_size_t * G)(*([n] * G))
+        self.ev = [ctx.event() for _ in range(4)]
+        self.t_enc, self.t_add, self.t_get, self.ok = [], [], [], True
+
+    def step(self, i, timed=True):
+        import ctypes
+        from kodr_amd import device as kdev
+        ctx, L_, errors, G, k, L = self.ctx, self.L_, self.errors, self.G, self.k, self.L
+        s_ = i % len(self.dW)
+        decs = []
+        for g in range(G):
+            h = ctypes.c_void_p()
+            errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
+            decs.append(h)
+        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
+        e = self.ev
+        ctx.record(e[0])
+        errors.check(L_.rlnc_encoder_group_coded_pieces_device(self.earr, G, self.dV[s_], self.n, self.dW[s_] + k,
+                                                               self.W))
+        ctx.record(e[1])
+        ta0 = time.perf_counter()
+        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+        errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[s_], self.counts, self.W, L, cons, sts))
+        ta1 = time.perf_counter()
+        ctx.record(e[2])
+        errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
+        ctx.record(e[3])
+        self.ok = self.ok and all(st in (0, 3) for st in sts) and all(c == k for c in cons)
+        for x in decs:
+            L_.rlnc_decoder_destroy(x)        # synchronises the stream: the step ends here
+        if timed:
+            self.t_enc.append(kdev.Context.elapsed_ms(e[0], e[1]) / 1e3)
+            self.t_add.append(ta1 - ta0)
+            self.t_get.append(kdev.Context.elapsed_ms(e[2], e[3]) / 1e3)
+
+    def decoded_ok(self, gens=None):
+        """The last step's decoded generations against the resident ones."""
+        import ctypes
+        import numpy as np
+        ok = self.ok
+        pitch = ctypes.c_size_t()
+        for g in (gens if gens is not None else sorted({0, self.G - 1})):
+            dp = self.L_.rlnc_encoder_device_pieces(self.encs[g], ctypes.byref(pitch))
+            a = self.ctx.d2h(self.dO + g * self.k * self.L, self.k * self.L)
+            b = self.ctx.d2h(dp, self.k * pitch.value).reshape(self.k, pitch.value)[:, :self.L].reshape(-1)
+            ok = ok and bool(np.array_equal(a, b))
+        return ok
+
+    def units(self):
+        """kodr units per step: (k + 2) x SetBytes (encoder bench,
+        benches/full/encoder_test.go:53) + DecodableLen k (k + L) (the decoded
+        generation) per generation."""
+        return self.G * (self.n * setbytes(self.k, self.L) + self.k * (self.k + self.L))
+
+    def close(self):
+        for p_ in self.dV + self.dW + [self.dO]:
+            self.ctx.free(p_)
+
+
+def run_timed(step, steps, warmup, barrier, warm_s, max_warm=20000):
+    """W untimed steps, never fewer than one and never less than warm_s of
+    back-to-back work (the clock transient, DESIGN.md Roofline), a barrier,
+    then exactly `steps` timed steps bracketed by barriers.  Returns (wall
+    seconds of the timed steps on this rank, warmup steps run)."""
+    n_warm = 0
+    tw0 = time.perf_counter()
+    while n_warm < max(warmup, 1) or (time.perf_counter() - tw0 < warm_s and n_warm < max_warm):
+        step(n_warm, False)
+        n_warm += 1
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i, True)
+    barrier()
+    return time.perf_counter() - t0, n_warm
+
+
+def roundtrip_block(t_local, steps, warmup, n_warm, units_per_step, world, kdist, device=None):
+    """The encode_decode block: whole-job kodr units over the slowest rank's
+    time for `steps` round trips (aggregate, weak scaling: every rank decodes
+    its own generations)."""
+    t_max = kdist.max_over_ranks(t_local, device=device)
+    return {"value": round(kdist.aggregate_rate(steps, units_per_step, t_max, world), 1), "unit": "MB/s",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "warmup_steps_run": n_warm,
+            "ms_per_step": round(t_max / steps * 1e3, 5), "higher_is_better": True, "scaling": "weak",
+            "units_per_step_per_rank": units_per_step}
+
+
+def roundtrip_kernels(rt, k, L):
+    """Per-leg figures of the timed round trips (HIP events on the context
+    stream around the encode launch and the GetPieces call; the AddPiece call's
+    host wall time, which ends with the transforms read back), each against
+    its bound."""
+    import statistics
+    G, n = rt.G, rt.n
+    te, ta, tg = (statistics.mean(x) for x in (rt.t_enc, rt.t_add, rt.t_get))
+    enc_macs, get_macs, elim_macs = G * n * k * L, G * k * k * L, G * k ** 3
+    return {
+        "encode_launch": {"kernel": "gf_bs_kernel (grouped, B = k + 2 per generation)", "avg_us": round(te * 1e6, 2),
+                          "us_per_generation": round(te / G * 1e6, 2),
+                          "gf_macs_per_s": float(f"{enc_macs / te:.4g}"),
+                          "issue_frac": round(enc_macs / te / VALU_FLOOR_MACS_PER_S, 4),
+                          "hbm_bytes": G * (k * L + n * k + n * L),
+                          "hbm_frac": round(G * (k * L + n * k + n * L) / te / 1e9 / HBM_PEAK_GBS, 4)},
+        "add_pieces_call": {"avg_us": round(ta * 1e6, 2), "us_per_generation": round(ta / G * 1e6, 2),
+                            "elimination_gf_macs": elim_macs,
+                            "row_bytes": G * 3 * n * L,
+                            "note": "host wall time: vector gather + elimination (gf_elim_mc_kernel) + the rows' copy "
+                                    "and bit-sliced twin beside it (read n L, write 2 n L per generation) + T read "
+                                    "back and loaded"},
+        "get_pieces_call": {"kernel": "gf_bs_kernel (grouped T x R)", "avg_us": round(tg * 1e6, 2),
+                            "us_per_generation": round(tg / G * 1e6, 2),
+                            "gf_macs_per_s": float(f"{get_macs / tg:.4g}"),
+                            "issue_frac": round(get_macs / tg / VALU_FLOOR_MACS_PER_S, 4),
+                            "hbm_bytes": G * 2 * k * L},
+        "issue_peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
+        "note": "issue_frac against the one bit-sliced VALU floor (ISSUE_PER_S x MACS_PER_INST_BS); kernel durations "
+                "of the same command under rocprofv3 in profiles/r04/roundtrip/"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,10 +430,15 @@ def main():
     from kodr_amd import dist as kdist
     rank, world, local = kdist.world()
 
-    # CPU baseline first, before this process touches the GPU (rank 0, N=1 only)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+    # CPU baselines first, before this process touches the GPU and before the
+    # process group starts (rank 0; at N > 1 a shorter sample): the encode
+    # (value's unit) and kodr's decode, which make the round trip's baseline
+    cpu = cpu_dec = None
+    if rank == 0 and not args.no_cpu_baseline:
+        secs = args.cpu_seconds if world == 1 else min(args.cpu_seconds, 3.0)
+        cpu = cpu_baseline(secs)
+        if not args.no_encode_decode:
+            cpu_dec = cpu_baseline_decode(secs * 0.6)
 
     import numpy as np
     import torch  # plumbing: process group + shared HIP runtime
@@ -288,10 +520,26 @@ def main():
 
     extras = {"construct_ms_per_generation": round(construct_ms, 3)}
     ed = None
-    if rank == 0 and not args.no_encode_decode:
+    if not args.no_encode_decode:
+        # the metric's encode+decode round trip under the same protocol: every
+        # rank, W warmup + K timed steps, barriers, max over ranks
         try:
-            ed = encode_decode(ctx, L_, errors, encs, k, L)
-        except Exception as e:  # secondary measurement: never lose the headline line
+            rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng)
+            t_rt, n_warm_rt = run_timed(rt.step, args.steps, args.warmup, barrier, WARM_S)
+            ed = roundtrip_block(t_rt, args.steps, args.warmup, n_warm_rt, rt.units(), world, kdist, device="cuda")
+            ed["workload"] = (f"a step = {G} resident 32 MiB/256 generations x (k + 2 = {k + 2} coded pieces in one "
+                              "grouped encode launch, a fresh decoder each fed them in one batched AddPiece call "
+                              "(GPU elimination), one grouped GetPieces), device-resident; value in kodr units: "
+                              "(k + 2) x SetBytes + DecodableLen per generation")
+            ed["generations_per_step"] = G
+            ed["us_per_generation"] = round(ed["ms_per_step"] / G * 1e3, 2)
+            ed["payload_MBps"] = round(world * args.steps * G * k * L / (ed["ms_per_step"] * args.steps / 1e3) / 1e6, 1)
+            ed["legs"] = roundtrip_kernels(rt, k, L)
+            ed["roundtrip_ok"] = rt.decoded_ok()
+            if cpu is not None and cpu_dec is not None:
+                ed["cpu_baseline"] = cpu_baseline_roundtrip(cpu, cpu_dec)
+            rt.close()
+        except Exception as e:  # secondary block: never lose the headline line
             ed = {"error": repr(e)[:300]}
     if not args.no_extras and rank == 0:
         extras.update(run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng))
@@ -324,8 +572,9 @@ def main():
                                    + (f"a step = {B} coded pieces of each of the {G} resident generations in one "
                                       "grouped launch" if grouped else
                                       f"a step = {B} coded pieces of one generation (rotating over {G})")
-                                   + "; value counts encode only. The metric's encode+decode round trip (configs[1] "
-                                     "+ configs[2]) is the top-level encode_decode object",
+                                   + "; value counts encode only (configs[1]). The metric's encode+decode round "
+                                     "trip (configs[1] + configs[2]) is the top-level encode_decode block, timed "
+                                     "under the same protocol (steps, warmup, barriers, max over ranks)",
                        "value_covers": "encode", "encode_decode_in": "encode_decode",
                        "piece_count": k, "piece_size": L, "coded_pieces_per_generation_per_step": B,
                        "generations_per_step": per_step, "coded_pieces_per_step": per_step * B,
@@ -612,20 +861,19 @@ def run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng):
     return out
 
 
-# VALU floor of the bit-sliced method: per coefficient and 2 KiB wave slice 8
-# XOR3 (7.97 on average) + the row's 26 table instructions shared by 8 output
-# rows, 2048 MACs; 1024 SIMDs at 2.4 GHz issuing a wave instruction every 2.3
-# cycles with 4 waves per SIMD (profiles/r01/dispatch_probe.log, straight line).
-VALU_FLOOR_MACS_PER_S = 2048 / (7.97 + 26 / 8) * 1024 * 2.4e9 / 2.3
-# Issue ceiling of the apply kernels: 1024 SIMDs at 2.4 GHz issuing one wave
-# instruction per ~2.35 cycles with 4 waves per SIMD (profiles/r01/dispatch_probe.log),
-# times the GF MACs each instruction carries: gf_bs_kernel issues ~15 per
-# coefficient per 2 KiB wave slice (8 XOR3, table share, v_readlane, SALU;
-# DESIGN.md), gf_gemm_kernel ~5 per coefficient per 256 B (3 v_perm + 1.5 XOR3
-# + selector share).
-ISSUE_PER_S = 1024 * 2.4e9 / 2.35
-MACS_PER_INST_BS = 2048 / 15
+# One issue ceiling for every GF product kernel, one derivation: 1024 SIMDs at
+# 2.4 GHz issuing a wave instruction every 2.3 cycles with 4 waves per SIMD
+# (profiles/r01/dispatch_probe.log, straight-line XOR3), times the GF MACs per
+# VALU instruction of the kernel's method.  gf_bs_kernel: per coefficient and
+# 2 KiB wave slice 8 XOR3 (7.97 on average) + the row's 26 table instructions
+# shared by 8 output rows, 2048 MACs -> 195 T MAC/s (the VALU floor; its
+# v_readlane and SALU are left out, so this is an upper bound).
+# gf_gemm_kernel: per coefficient and 256 B 3 v_perm + 1.5 XOR3 + the
+# selector share (0.5) -> 55 T MAC/s.
+ISSUE_PER_S = 1024 * 2.4e9 / 2.3
+MACS_PER_INST_BS = 2048 / (7.97 + 26 / 8)
 MACS_PER_INST_PERM = 256 / 5
+VALU_FLOOR_MACS_PER_S = ISSUE_PER_S * MACS_PER_INST_BS
 
 
 def grouped_encode(ctx, L_, errors, encs, k, L, rng, iters=50):
@@ -834,91 +1082,6 @@ def _gf_vecmat(v, M):
     return acc.astype(np.uint8)
 
 
-def encode_decode(ctx, L_, errors, encs, k, L, reps=3):
-    """The metric's encode+decode as one round trip, device-resident, over the
-    G resident 32 MiB/256 generations: k + 2 coded pieces of each as wire rows
-    with device-drawn vectors in ONE grouped call
-    (rlnc_encoder_group_coded_wire_device: one vector launch + one bit-sliced
-    launch), then G fresh decoders take them in ONE batched AddPiece call
-    (rlnc_decoders_add_pieces_gpu: the elimination on the GPU) and ONE grouped
-    GetPieces call (rlnc_decoders_get_pieces_device).  Fresh vectors every
-    repetition; decoders constructed outside the timed region, as
-    kodr's decoder bench does (benches/full/decoder_test.go:46-94).  Wall time
-    of the whole round trip, best of reps; the decoded generations are
-    compared with the resident ones."""
-    import ctypes
-    import numpy as np
-    from kodr_amd import device as kdev
-    G, n, W = len(encs), k + 2, k + L
-    earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
-    dW = ctx.alloc(G * n * W)
-    dO = ctx.alloc(G * k * L)
-    rows = (ctypes.c_void_p * G)(*[dW + g * n * W for g in range(G)])
-    counts = (ctypes.c_size_t * G)(*([n] * G))
-    e0, e1 = ctx.event(), ctx.event()
-    best, ok = None, True
-    for rep in range(reps + 1):        # rep 0 warms the path (pool buffers, twins of the decoders)
-        decs = []
-        for g in range(G):
-            h = ctypes.c_void_p()
-            errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
-            decs.append(h)
-        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
-        ctx.synchronize()
-        t0 = time.perf_counter()
-        ctx.record(e0)
-        errors.check(L_.rlnc_encoder_group_coded_wire_device(earr, G, n, dW, W))
-        ctx.record(e1)
-        ctx.synchronize()               # the legs apart: encode | AddPiece | GetPieces
-        te = time.perf_counter()
-        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
-        errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, rows, counts, W, L, cons, sts))
-        t1 = time.perf_counter()
-        errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, dO, L))
-        ctx.synchronize()
-        t2 = time.perf_counter()
-        t_enc = kdev.Context.elapsed_ms(e0, e1) / 1e3
-        ok = ok and all(s_ in (0, 3) for s_ in sts) and all(L_.rlnc_decoder_is_decoded(x) for x in decs)
-        for x in decs:
-            L_.rlnc_decoder_destroy(x)
-        if rep and (best is None or t2 - t0 < best[0]):
-            best = (t2 - t0, t_enc, t1 - te, t2 - t1, te - t0)
-    pitch = ctypes.c_size_t()
-    for g in (0, G - 1):
-        dp = L_.rlnc_encoder_device_pieces(encs[g], ctypes.byref(pitch))
-        a = ctx.d2h(dO + g * k * L, k * L)
-        b = ctx.d2h(dp, k * pitch.value).reshape(k, pitch.value)[:, :L].reshape(-1)
-        ok = ok and bool(np.array_equal(a, b))
-    ctx.free(dW)
-    ctx.free(dO)
-    t, t_enc, t_add, t_get, t_enc_wall = best
-    enc_units = G * n * setbytes(k, L)                 # benches/full/encoder_test.go:53 per coded piece
-    dec_units = G * k * (k + L)                        # DecodableLen per decoded generation
-    apply_macs = G * k * k * L
-    return {
-        "generations": G, "coded_pieces_per_generation": n,
-        "ms": round(t * 1e3, 3), "us_per_generation": round(t / G * 1e6, 1),
-        "payload_MBps": round(G * k * L / t / 1e6, 1),
-        "kodr_units_MBps": round((enc_units + dec_units) / t / 1e6, 1),
-        "encode_us_per_generation": round(t_enc / G * 1e6, 2),
-        "encode_wall_us_per_generation": round(t_enc_wall / G * 1e6, 1),
-        "add_us_per_generation": round(t_add / G * 1e6, 1),
-        "get_us_per_generation": round(t_get / G * 1e6, 1),
-        "encode_coded_MBps": round(enc_units / t_enc / 1e6, 1),
-        "decode_apply": {"gf_macs_per_s": float(f"{apply_macs / t_get:.4g}"),
-                         "issue_frac": round(apply_macs / t_get / VALU_FLOOR_MACS_PER_S, 4),
-                         "hbm_GBps": round(G * (k * L + k * L) / t_get / 1e9, 1),
-                         "note": "grouped GetPieces wall time (host T staging included): k x k x L GF MACs per "
-                                 "generation against the bit-sliced VALU floor; hbm = received twin read once + "
-                                 "decoded pieces written"},
-        "roundtrip_ok": ok,
-        "note": "one round trip per generation: k + 2 coded wire rows (grouped encode, HIP events; its wall time "
-                "ends at a stream synchronize that separates the legs) + one batched "
-                "AddPiece (GPU elimination) + one grouped GetPieces, device-resident, wall time; payload_MBps = "
-                "original bytes through encode and decode per second; kodr_units_MBps = (k+2) x SetBytes "
-                "(encoder bench) + DecodableLen (decoder bench) per generation per second"}
-
-
 def c2_decode_grouped(ctx, L_, errors, encs, k, L, reps=3):
     """BASELINE configs[2] over many generations: each of the G resident
     generations' encoders writes k + 2 coded wire rows (device-drawn vectors),
@@ -1094,7 +1257,10 @@ def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
                      "add_calls_us_per_generation": round(t_add / G * 1e6, 1),
                      "flush_us_per_generation": round(t_flush / G * 1e6, 1),
                      "spare_adds_and_get_us_per_generation": round(t_rest / G * 1e6, 1), "roundtrip_ok": ok}
-    res["flush_speedup"] = round(res["host"]["flush_us_per_generation"] / res["gpu"]["flush_us_per_generation"], 2)
+    # the whole piecewise decode is the like-for-like comparison: the host flush
+    # (IsDecoded) leaves the gather of the queued pieces to the next data call,
+    # the GPU flush does it in the flush
+    res["decode_speedup"] = round(res["host"]["us_per_generation"] / res["gpu"]["us_per_generation"], 2)
     res["note"] = ("k AddPiece calls per generation (device pieces, round-robin over the generations), the queued "
                    "eliminations flushed by one rlnc_decoders_flush_gpu (gpu) or by each decoder's IsDecoded (host), "
                    "2 more AddPiece calls per generation, one grouped GetPieces; wall time")
@@ -1326,27 +1492,44 @@ def host_roundtrip(ctx, L_, errors, k, L, rng, pinned=False):
     tc0 = time.perf_counter()
     errors.check(L_.rlnc_encoder_coded_pieces(eh, V.ctypes.data_as(u8p), n, wire.ctypes.data_as(u8p)))
     tc1 = time.perf_counter()
+    # decode alone: the k + 2 host wire rows into a fresh decoder (one batched
+    # AddPiece: H2D of the rows, elimination) and the k decoded pieces back
     dh = ctypes.c_void_p()
     errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(dh)))
+    td0 = time.perf_counter()
     consumed = ctypes.c_size_t()
     st = L_.rlnc_decoder_add_pieces(dh, wire.ctypes.data_as(u8p), n, k + L, L, 0, ctypes.byref(consumed))
     if st != 3:
         errors.check(st)
+    td1 = time.perf_counter()
     errors.check(L_.rlnc_decoder_get_pieces(dh, outp.ctypes.data_as(u8p)))
-    t3 = time.perf_counter()
+    td2 = time.perf_counter()
     ok = bool(np.array_equal(outp, data))
     L_.rlnc_decoder_destroy(dh)
     L_.rlnc_encoder_destroy(eh)
     if pinned:
         for a in (data, V, wire, outp):
             ctx.unregister(a)
+    t_dec = td2 - td0
+    t_rt = (t1 - t0) + (tc1 - tc0) + t_dec
+    # PCIe floor of the round trip at the box's 56 GB/s each way (profiles/r01/pcie.log):
+    # the generation up, k + 2 wire rows down, the same rows up, k pieces down
+    floor = (k * L + 2 * n * (k + L) + k * L) / 56e9
     return {"upload_ms": round((t1 - t0) * 1e3, 3),
             "encode_k+2_to_host_ms": round((t2 - t1) * 1e3, 3),
             "encode_coded_MBps_incl_pcie": round(n * setbytes(k, L) / (t2 - t1) / 1e6, 1),
             "encode_k+2_one_call_ms": round((tc1 - tc0) * 1e3, 3),
             "encode_one_call_pcie_GBps": round(n * (k + L) / (tc1 - tc0) / 1e9, 1),
-            "decode_from_host_ms": round((t3 - t2) * 1e3, 3),
-            "roundtrip_ok": ok}
+            "decode_from_host_ms": round(t_dec * 1e3, 3),
+            "decode_add_pieces_ms": round((td1 - td0) * 1e3, 3),
+            "decode_get_pieces_to_host_ms": round((td2 - td1) * 1e3, 3),
+            "roundtrip_host_resident_ms": round(t_rt * 1e3, 3),
+            "roundtrip_pcie_floor_ms": round(floor * 1e3, 3),
+            "roundtrip_payload_MBps": round(k * L / t_rt / 1e6, 1),
+            "roundtrip_ok": ok,
+            "note": "one generation: upload (create from host data), k + 2 coded pieces to host in one call, "
+                    "decode from those host rows (batched AddPiece + GetPieces to host); pcie floor = 4 transfers "
+                    "of the generation's size at 56 GB/s"}
 
 
 if __name__ == "__main__":

@@ -173,3 +173,68 @@ def test_shard_generations_partition():
         for ws in range(1, 9):
             owned = [g for r in range(ws) for g in shard_generations(n, ws, r)]
             assert owned == list(range(n))
+
+
+def _roundtrip_worker(rank, ws, port, q):
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import bench
+    import oracle
+    from kodr_amd import dist as kd
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=ws)
+    try:
+        # bench.py's encode_decode protocol (run_timed + roundtrip_block) with a
+        # CPU stand-in step: k + 2 coded pieces of this rank's generation by the
+        # oracle, a fresh oracle decoder fed them; rank 1 is slower on purpose
+        k, L = 8, 96
+        P = np.random.default_rng(400 + rank).integers(0, 256, (k, L), dtype=np.uint8)
+        rng = np.random.default_rng(500 + rank)
+        seen = {"ok": True, "timed": 0}
+
+        def step(i, timed):
+            V = rng.integers(0, 256, (k + 2, k), dtype=np.uint8)
+            C = oracle.encode(P, V)
+            d = oracle.Decoder(k)
+            for j in range(k + 2):
+                if d.add(V[j], C[j]) == 3:
+                    break
+            seen["ok"] &= d.is_decoded() and np.array_equal(np.stack([d.get_piece(j)[1] for j in range(k)]), P)
+            seen["timed"] += int(timed)
+            if rank == 1:
+                time.sleep(0.01)
+
+        units = 10_000_000 * (k + 2)  # stand-in units, large enough that the rounded value is exact
+        t, n_warm = bench.run_timed(step, 5, 2, dist.barrier, 0.0)
+        blk = bench.roundtrip_block(t, 5, 2, n_warm, units, ws, kd)
+        q.put((rank, t, blk, seen["ok"], seen["timed"], n_warm))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_roundtrip_block_two_ranks():
+    # the encode_decode block at N = 2: every rank runs the round trip, the
+    # time is the slowest rank's, the value aggregates both ranks' units
+    ws, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_roundtrip_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(ws))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    t_max = max(r[1] for r in res)
+    assert res[1][1] >= 0.05                                     # the slow rank's 5 x 10 ms
+    for rank, t, blk, ok, timed, n_warm in res:
+        assert ok and timed == 5 and n_warm == 2, rank
+        assert blk["n_gpus"] == 2 and blk["steps"] == 5 and blk["warmup"] == 2
+        assert blk["ms_per_step"] == pytest.approx(t_max / 5 * 1e3, rel=1e-4)
+        assert blk["value"] == pytest.approx(2 * 5 * blk["units_per_step_per_rank"] / t_max / 1e6, rel=1e-3)
+    assert res[0][2] == res[1][2]                                # one block, whatever the rank

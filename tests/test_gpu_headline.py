@@ -105,6 +105,31 @@ def test_bench_headline_step_exact(gpu_ctx):
         assert np.array_equal(got[g], oracle.encode(P, hs.V[1, g])), g
 
 
+def test_bench_roundtrip_step_exact(gpu_ctx):
+    # The bench's encode_decode step itself (bench.RoundTripStep over 16
+    # prepared 32 MiB/256 generations): k + 2 coded pieces of each in one
+    # grouped encode launch, 16 fresh decoders in one batched GPU AddPiece
+    # call (the multi-workgroup elimination), one grouped GetPieces.  Two
+    # steps (both vector sets); after each, every decoded generation equals
+    # the original bytes, and every decoder took exactly k pieces.
+    import bench
+    L_ = _lib.lib()
+    hs = bench.HeadlineStep(gpu_ctx, L_, errors, 256, 131072, 32, 16, grouped=True,
+                            rng=np.random.default_rng(0x5EED), nvec=2, keep_data=True)
+    rt = bench.RoundTripStep(gpu_ctx, L_, errors, hs.encs, 256, 131072, np.random.default_rng(0x7E), nsets=2)
+    try:
+        for i in range(2):
+            rt.step(i, timed=True)
+            got = gpu_ctx.d2h(rt.dO, 16 * 256 * 131072).reshape(16, -1)
+            for g in range(16):
+                assert np.array_equal(got[g], hs.datas[g]), (i, g)
+            assert rt.ok and rt.decoded_ok(list(range(16)))
+        assert len(rt.t_enc) == len(rt.t_add) == len(rt.t_get) == 2
+    finally:
+        rt.close()
+        hs.close()
+
+
 # grouped bit-sliced launches that plan each KW instance of
 # gf_bs_kernel<KW, 0, true, 2> (capi.cpp plan_gemm_bs): (G, k, L, count) -> KW
 GROUPED_KW_SHAPES = [((2, 8, 4096, 40), 1), ((2, 16, 4096, 40), 2), ((2, 24, 4096, 17), 3),
