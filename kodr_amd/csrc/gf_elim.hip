@@ -47,6 +47,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "gf_kernels.hpp"
 
 namespace kodr_amd {
@@ -739,6 +741,8 @@ constexpr int kMcSpinMax = 1 << 20;  // >= ~1 s of polling: only a lost workgrou
 
 struct ElimMcLds {
   uint4 tab[256 * 2];     // the [256][8]-dword tables as 16-byte rows (as ElimBlkLds)
+  uint4 itab[256 * 2];    // the same for inv(f): a pivot's normalization from LDS (a workgroup
+                          // runs only 32 pivots, so scalar-cache reads of them would mostly miss)
   uint32_t nq[32][64];    // a consumed group's pivot rows; in the own step, a sub-panel's new rows
   uint32_t prow[16][64];  // the sub-panel's rows before the step
   uint32_t pan[16][4];    // its 16 x 16 block
@@ -757,39 +761,60 @@ __device__ __forceinline__ uint32_t mc_mul(const uint4& t, uint32_t t2, uint32_t
          __builtin_amdgcn_perm(t2, t2, s2);
 }
 
-// panel_gj for the mc layout: pan (16 x 16 block, written by other waves and
-// behind a barrier) -> sd = block^-1, or fail = 1.  One wave.
-__device__ __forceinline__ void mc_panel_gj(ElimMcLds& lds, cu32* tb, int lane) {
+// lane v gets the value of lane 4 (v / 4) + cd (a quad broadcast, DPP)
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int cd) {
+  switch (cd) {
+    case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xf, 0xf, false);
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xf, 0xf, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xaa, 0xf, 0xf, false);
+    default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xff, 0xf, 0xf, false);
+  }
+}
+
+// The 16 x 16 block inversion for the mc kernel: pan (written by other waves,
+// behind a barrier) -> sd = block^-1, or fail = 1.  One wave, lane (t, d) =
+// dword d of block row t: P (block) and Tr (the identity it turns into S).
+// Gauss-Jordan with row pivoting (the lowest unpicked row with a non-zero
+// entry), arranged so that one step waits for one dependent LDS lookup:
+//  * the row's multiplier f = byte c of its own row (a DPP quad broadcast),
+//    whose tables are gathered at once, before the pivot is known;
+//  * the pivot (ballot), its entry dp and the tables of inv(dp) (gf256.go:77-86);
+//  * the pivot row normalized, Pn = inv(dp) x row_p (broadcast by bpermute,
+//    issued beside the table read), then row ^= f x Pn; the pivot row
+//    becomes Pn (for it f x Pn would be the raw row).
+__device__ __forceinline__ void mc_panel_gj(ElimMcLds& lds, int lane) {
   const int t = lane >> 2, d = lane & 3;
   uint32_t P = lds.pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
-  uint32_t used = 0;
+  uint32_t used = 0;  // rows picked so far (uniform)
   int mycol = 0;
+#pragma unroll
   for (int c = 0; c < 16; c++) {
     const int cd = c >> 2, cb = 8 * (c & 3);
-    const bool nz = (d == cd) && ((P >> cb) & 0xffu) != 0u && !((used >> t) & 1u);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    uint4 tf;
+    uint32_t tf2;
+    mc_tab(lds, f, tf, tf2);
+    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
     const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
     if (m == 0) {
       if (lane == 0) lds.fail = 1;
       return;
     }
     const int pl = __builtin_ctzll(m), tp = pl >> 2;
-    const uint32_t dp = (__builtin_amdgcn_readlane(P, pl) >> cb) & 0xffu;
-    cu32* tinv = tb + kElimInvTables + dp * 8;  // tables of inv(dp) (gf256.go:77-86)
-    const uint4 ti = {tinv[0], tinv[1], tinv[2], tinv[3]};
-    const uint32_t ti2 = tinv[4];
-    if (t == tp) {
-      P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
-      Tr = gmul4(ti, ti2, sel0(Tr), sel1(Tr), sel2(Tr));
-      mycol = c;
-    }
+    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
+    const uint4 ti = lds.itab[2 * dp];  // tables of inv(dp)
+    const uint32_t ti2 = lds.itab[2 * dp + 1].x;
     const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
-    uint32_t f = (bperm(P, t * 4 + cd) >> cb) & 0xffu;
-    if (t == tp) f = 0u;
-    uint4 tf;
-    uint32_t tf2;
-    mc_tab(lds, f, tf, tf2);
-    P ^= gmul4(tf, tf2, sel0(Pp), sel1(Pp), sel2(Pp));
-    Tr ^= gmul4(tf, tf2, sel0(Tp), sel1(Tp), sel2(Tp));
+    const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
+    const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
+    if (t == tp) {
+      P = Pn;
+      Tr = Tn;
+      mycol = c;
+    } else {
+      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
+      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
+    }
     used |= 1u << tp;
   }
   lds.sd[mycol][d] = Tr;
@@ -807,11 +832,32 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = args.k;
   const uint32_t epoch = args.epoch;
-  cu32* tb = (cu32*)args.tables;
   gu64* pub = (gu64*)args.pub + (size_t)g * P * 32 * 64;
 
-  for (int i = tid; i < 256 * 2; i += 64 * kMcWaves)
-    lds.tab[i] = make_uint4(args.tables[4 * i], args.tables[4 * i + 1], args.tables[4 * i + 2], args.tables[4 * i + 3]);
+#ifdef KODR_ELIM_TIMING
+  // tuning build: s_memrealtime (100 MHz, chip-wide) stamps, stored by
+  // thread 0 straight into this workgroup's first out row (no result):
+  // [0] entry, [1] rows loaded, [2 + gp] after group gp's step, [2 + P] end,
+  // [3 + P + 3 s + j] inside the own step (sub-panel s: block inverted, new
+  // rows, other rows updated)
+  uint64_t* const tsout = reinterpret_cast<uint64_t*>(args.out + (size_t)g * args.out_gen_stride +
+                                                      (size_t)(32 * q) * args.out_pitch);
+  if (tid == 0) tsout[0] = __builtin_amdgcn_s_memrealtime();
+#define MC_STAMP(i)                                                \
+  do {                                                             \
+    if (tid == 0) tsout[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MC_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+  for (int i = tid; i < 256 * 2; i += 64 * kMcWaves) {
+    const uint32_t* a = args.tables + 4 * i;
+    const uint32_t* b = args.tables + kElimInvTables + 4 * i;
+    lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
+    lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
+  }
   if (tid == 0) lds.fail = 0;
 
   // rows 32q + 2w + i: C (padded with identity rows and columns past k)
@@ -831,6 +877,7 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
     R[i] = v;
   }
   __syncthreads();
+  MC_STAMP(1);
 
   bool published = false;
   for (int gp = 0; gp < P; gp++) {
@@ -849,8 +896,9 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
           }
         }
         __syncthreads();
-        if (w == 0) mc_panel_gj(lds, tb, lane);
+        if (w == 0) mc_panel_gj(lds, lane);
         __syncthreads();
+        MC_STAMP(3 + P + 3 * s);
         if (lds.fail) break;  // uniform
         {  // new row c = w: sum_u S[c][u] x row u, the block replaced by S[c]
           uint32_t acc = 0;
@@ -870,6 +918,7 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
           lds.nq[w][lane] = acc;
         }
         __syncthreads();
+        MC_STAMP(4 + P + 3 * s);
         if (blk) {
 #pragma unroll
           for (int i = 0; i < 2; i++) R[i] = lds.nq[2 * (w - 8 * s) + i][lane];
@@ -894,10 +943,12 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
           }
         }
         __syncthreads();
+        MC_STAMP(5 + P + 3 * s);
       }
       if (lds.fail) break;
       mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch, R[0], R[1]);
       published = true;
+      MC_STAMP(2 + gp);
       continue;
     }
     // ---- another group's pivot rows: take them, drop its columns ----
@@ -947,7 +998,14 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
       }
     }
     __syncthreads();
+    MC_STAMP(2 + gp);
   }
+  MC_STAMP(2 + P);
+#ifdef KODR_ELIM_TIMING
+  if (tid == 0) args.counts[g * P + q] = 0;
+  return;
+#endif
+#undef MC_STAMP
   const bool ok = lds.fail == 0;
   if (!ok && !published)  // a later group waits for this one: tell it
     mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch | kMcFail, 0u, 0u);
@@ -965,6 +1023,374 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
   }
   __syncthreads();
   if (tid == 0) args.counts[g * P + q] = ok ? 1 : 0;
+}
+
+// ---- mc2: the same inversion, pipelined inside each workgroup -------------
+// Panels of 16 columns (NP = 2P); workgroup q owns panels 2q ("A rows", its
+// local rows 0-15) and 2q + 1 ("B rows", 16-31).  In-place block
+// Gauss-Jordan in "L form": panel p publishes R_p (its 16 rows as they are
+// before its step) and S_p = (R_p's 16 x 16 block)^-1; a row i outside the
+// panel takes F_i = row_i[panel] x S_p, then row_i ^= F_i x R_p and
+// row_i[panel] = F_i; the panel's own rows become S_p x R_p with S_p in the
+// panel columns (both: new = base ^ G x R_p, then the panel columns := G,
+// with G = F_i, base = row_i or G = row of S_p, base = 0).
+// Two roles per workgroup, synchronised through LDS counters, not barriers:
+//  * row waves 0-7 hold the 32 rows (4 per wave, lane = dword) and apply
+//    every panel in order, one panel behind the chain;
+//  * chain waves 8-15 run the critical path: for an owned panel p, wave 8
+//    brings the 16 x 16 block up to date with panel p - 1 (two small products
+//    from rows as of panel p - 2, so it does not wait for the row waves'
+//    apply of p - 1), inverts it (mc2_panel_gj) and publishes S_p; for any
+//    other panel the chain waves poll R_p and S_p into LDS.
+// Hand-offs between workgroups as in gf_elim_mc_kernel (granules tagged with
+// the launch epoch, FAIL bit; bounded spins); three LDS slots per panel
+// buffer so a slot is rewritten only after both roles are two panels on.
+constexpr int kMc2Slots = 3;
+constexpr int kMc2PanelGran = 16 * 64 + 64;  // granules per panel: R_p rows, then S_p
+
+struct ElimMc2Lds {
+  uint4 tab[256 * 2];
+  uint4 itab[256 * 2];
+  uint32_t rp[kMc2Slots][16][64];  // R_p by slot p % 3
+  uint32_t sp[kMc2Slots][16][4];   // S_p by rows: S[c][u] = byte u % 4 of sp[c][u / 4]
+  uint32_t mb[kMc2Slots][16][8];   // owned panel p: its rows' panel p - 1 (dwords 0-3) and panel p (4-7) columns, as of panel p - 2
+  uint32_t mw[8][4][4];            // row wave w: its rows' columns of the panel it applies (the multipliers)
+  uint32_t fw[8][4][4];            // row wave w: G of its rows
+  uint32_t ft[16][4];              // chain: F of the block rows
+  uint32_t pan[16][4];             // chain: the block to invert
+  int rows_done;                   // row-wave iterations finished (8 per panel, 8 for the start)
+  int chain_cnt;                   // chain-wave iterations finished (8 per panel)
+  int fail;                        // 1 singular / FAIL seen, 2 timeout
+};
+
+__device__ __forceinline__ bool mc2_wait(ElimMc2Lds& lds, int* ctr, int target) {
+  for (int spins = 0;; spins++) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (spins > kMcSpinMax) {
+      __hip_atomic_store(&lds.fail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// this wave's LDS writes first, then one count
+__device__ __forceinline__ void mc2_signal(int* ctr, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// mc_panel_gj's algorithm on an LDS block, S to `s_out` ([16][4]), its rows
+// also kept in registers for publishing (returns false if singular)
+__device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab, const uint32_t (*pan)[4],
+                                             uint32_t (*s_out)[4], int lane, uint32_t* s_val, int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t P = pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
+  uint32_t used = 0;
+  int mycol = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) return false;
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
+    const uint4 ti = itab[2 * dp];
+    const uint32_t ti2 = itab[2 * dp + 1].x;
+    const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
+    const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
+    const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
+    if (t == tp) {
+      P = Pn;
+      Tr = Tn;
+      mycol = c;
+    } else {
+      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
+      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
+    }
+    used |= 1u << tp;
+  }
+  s_out[mycol][d] = Tr;
+  *s_val = Tr;
+  *s_row = mycol;
+  return true;
+}
+
+// out[t][d] = base ^ sum_c M[t][c] x X[c][d], one wave, lane (t, d): M rows
+// are 4 dwords (16 bytes), X rows 4 dwords
+__device__ __forceinline__ uint32_t mc2_small(const uint4* tab, uint32_t base, const uint32_t* mrow,
+                                              const uint32_t (*x)[4], int d) {
+  uint32_t acc = base;
+#pragma unroll 4
+  for (int c = 0; c < 16; c++) {
+    const uint32_t m = (mrow[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    const uint4 t = tab[2 * m];
+    const uint32_t t2 = tab[2 * m + 1].x;
+    const uint32_t xv = x[c][d];
+    acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
+  __shared__ ElimMc2Lds lds;
+  const int q = blockIdx.x, g = blockIdx.y, P = gridDim.x, NP = 2 * gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = args.k;
+  const uint32_t epoch = args.epoch;
+  gu64* pub = (gu64*)args.pub + (size_t)g * NP * kMc2PanelGran;
+
+  for (int i = tid; i < 256 * 2; i += 1024) {
+    const uint32_t* a = args.tables + 4 * i;
+    const uint32_t* b = args.tables + kElimInvTables + 4 * i;
+    lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
+    lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
+  }
+  if (tid == 0) {
+    lds.rows_done = 0;
+    lds.chain_cnt = 0;
+    lds.fail = 0;
+  }
+  __syncthreads();
+
+  bool ok = true;
+  if (w < 8) {
+    // ================= row waves: rows 4w .. 4w + 3 =================
+    const int half = w >> 2;  // 0: panel 2q's rows, 1: panel 2q + 1's
+    uint32_t R[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int gr = 32 * q + 4 * w + i;
+      uint32_t v = 0;
+      if (gr < k) {
+        const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+          if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
+      } else if (gr >> 2 == lane) {
+        v = 1u << (8 * (gr & 3));
+      }
+      R[i] = v;
+    }
+    // workgroup 0's first panel: its block for the chain (no earlier panel)
+    if (q == 0 && half == 0 && lane < 4)
+#pragma unroll
+      for (int i = 0; i < 4; i++) lds.mb[0][4 * w + i][4 + lane] = R[i];
+    mc2_signal(&lds.rows_done, lane);
+
+    auto apply = [&](int pa) {
+      const int slot = pa % kMc2Slots, db = 4 * pa;
+      const bool own = (pa >> 1) == q && (pa & 1) == half;
+      uint32_t G[4][4];
+      if (own) {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int u = 0; u < 4; u++) G[i][u] = __builtin_amdgcn_readfirstlane(lds.sp[slot][4 * (w & 3) + i][u]);
+      } else {
+        // F of the 4 rows: lane (cg, i, u) sums c = 4 cg .. 4 cg + 3, then
+        // the four groups are folded (lanes 16 and 32 apart)
+        if (lane >= db && lane < db + 4)
+#pragma unroll
+          for (int i = 0; i < 4; i++) lds.mw[w][i][lane - db] = R[i];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes land first
+        const int cg = lane >> 4, i = (lane >> 2) & 3, u = lane & 3;
+        const uint32_t mwd = lds.mw[w][i][cg];
+        uint32_t acc = 0;
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          const uint32_t m = (mwd >> (8 * cc)) & 0xffu;
+          const uint4 t = lds.tab[2 * m];
+          const uint32_t t2 = lds.tab[2 * m + 1].x;
+          const uint32_t xv = lds.sp[slot][4 * cg + cc][u];
+          acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+        }
+        acc ^= bperm(acc, lane ^ 16);
+        acc ^= bperm(acc, lane ^ 32);
+        if (lane < 16) lds.fw[w][i][u] = acc;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+#pragma unroll
+        for (int i2 = 0; i2 < 4; i2++)
+#pragma unroll
+          for (int u2 = 0; u2 < 4; u2++) G[i2][u2] = __builtin_amdgcn_readfirstlane(lds.fw[w][i2][u2]);
+      }
+      uint32_t acc[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
+#pragma unroll 2
+      for (int c = 0; c < 16; c++) {
+        const uint32_t x = lds.rp[slot][c][lane];
+        const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t f = (G[i][c >> 2] >> (8 * (c & 3))) & 0xffu;
+          const uint4 t = lds.tab[2 * f];
+          const uint32_t t2 = lds.tab[2 * f + 1].x;
+          acc[i] ^= mc_mul(t, t2, s0, s1, s2);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        uint32_t v = acc[i];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (lane == db + u) v = G[i][u];
+        R[i] = v;
+      }
+    };
+
+    for (int p = 0; p < NP; p++) {
+      if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1)) || !mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+      if (p >= 1) apply(p - 1);
+      if ((p >> 1) == q && (p & 1) == half) {  // my rows are panel p's: R_p out
+        const int slot = p % kMc2Slots;
+        gu64* dst = pub + (size_t)p * kMc2PanelGran;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int r = 4 * (w & 3) + i;
+          lds.rp[slot][r][lane] = R[i];
+          __hip_atomic_store(dst + r * 64 + lane, ((unsigned long long)epoch << 32) | R[i], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      const int pn = p + 1;
+      if (pn < NP && (pn >> 1) == q && (pn & 1) == half) {  // next panel's block for the chain
+        const int slot = pn % kMc2Slots;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int r = 4 * (w & 3) + i;
+          if (lane >= 4 * p && lane < 4 * p + 4) lds.mb[slot][r][lane - 4 * p] = R[i];
+          if (lane >= 4 * pn && lane < 4 * pn + 4) lds.mb[slot][r][4 + lane - 4 * pn] = R[i];
+        }
+      }
+      mc2_signal(&lds.rows_done, lane);
+    }
+    ok = mc2_wait(lds, &lds.chain_cnt, 8 * NP) && mc2_wait(lds, &lds.rows_done, 8 * (NP + 1));
+    if (ok) {
+      apply(NP - 1);
+      uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int gr = 32 * q + 4 * w + i;
+        if (gr >= k) continue;
+        uint8_t* row = out + (size_t)gr * args.out_pitch + k;
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+          if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(R[i] >> (8 * b));
+      }
+    }
+  } else {
+    // ================= chain waves =================
+    const int cw = w - 8;
+    if (cw == 0) __builtin_amdgcn_s_setprio(3);
+    int unpublished = 2 * q;  // the first owned panel whose S_p is not out yet
+    for (int p = 0; p < NP; p++) {
+      const int slot = p % kMc2Slots;
+      gu64* base = pub + (size_t)p * kMc2PanelGran;
+      // every chain wave finished panel p - 1 (no wave runs ahead: the count
+      // then means exactly that)
+      if (!mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+      if ((p >> 1) == q) {
+        if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
+        if (cw == 0) {
+          const int t = lane >> 2, d = lane & 3;
+          uint32_t blk = lds.mb[slot][t][4 + d];
+          if (p >= 1) {
+            const int ps = (p - 1) % kMc2Slots;
+            uint32_t mrow[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) mrow[u] = lds.mb[slot][t][u];
+            lds.ft[t][d] = mc2_small(lds.tab, 0u, mrow, lds.sp[ps], d);  // F = M x S_{p-1}
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            uint32_t frow[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) frow[u] = lds.ft[t][u];
+            // block ^= F x R_{p-1}[:, panel p]
+            uint32_t acc = blk;
+#pragma unroll 4
+            for (int c = 0; c < 16; c++) {
+              const uint32_t m = (frow[c >> 2] >> (8 * (c & 3))) & 0xffu;
+              const uint4 tt = lds.tab[2 * m];
+              const uint32_t tt2 = lds.tab[2 * m + 1].x;
+              const uint32_t xv = lds.rp[ps][c][4 * p + d];
+              acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+            }
+            blk = acc;
+          }
+          lds.pan[t][d] = blk;
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          uint32_t sval = 0;
+          int srow = 0;
+          if (!mc2_panel_gj(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow)) {
+            __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            __hip_atomic_store(base + 16 * 64 + srow * 4 + d, ((unsigned long long)epoch << 32) | sval,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unpublished = p + 1;
+          }
+        }
+        if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        mc2_signal(&lds.chain_cnt, lane);
+      } else {
+        // another workgroup's panel: R_p (rows 2cw, 2cw + 1) and S_p (wave 0) into LDS
+        const gu64* src = base + (size_t)(2 * cw) * 64 + lane;
+        uint64_t a = 0, b = 0, s = 0;
+        bool seen_fail = false, timeout = false;
+        for (int spins = 0;; spins++) {
+          a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cw == 0) s = __hip_atomic_load(base + 16 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t ta = (uint32_t)(a >> 32), tb2 = (uint32_t)(b >> 32), ts = cw == 0 ? (uint32_t)(s >> 32) : epoch;
+          const bool okv = (ta & ~kMcFail) == epoch && (tb2 & ~kMcFail) == epoch && (ts & ~kMcFail) == epoch;
+          const bool anyfail = __builtin_amdgcn_ballot_w64(((ta == (epoch | kMcFail)) | (tb2 == (epoch | kMcFail)) |
+                                                            (ts == (epoch | kMcFail)))) != 0;
+          if (anyfail) {
+            seen_fail = true;
+            break;
+          }
+          if (__builtin_amdgcn_ballot_w64(!okv) == 0) break;
+          if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            seen_fail = true;
+            break;
+          }
+          if (spins > kMcSpinMax) {
+            timeout = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (seen_fail || timeout) {
+          __hip_atomic_store(&lds.fail, timeout ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          break;
+        }
+        if (!mc2_wait(lds, &lds.rows_done, 8 * p)) break;  // the slot's last readers are done
+        lds.rp[slot][2 * cw][lane] = (uint32_t)a;
+        lds.rp[slot][2 * cw + 1][lane] = (uint32_t)b;
+        if (cw == 0) lds.sp[slot][lane >> 2][lane & 3] = (uint32_t)s;
+        mc2_signal(&lds.chain_cnt, lane);
+      }
+    }
+    ok = __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+    if (!ok && cw == 0) {
+      // owned panels whose S_p is not out: FAIL on R_p and S_p, so that
+      // every later workgroup stops too
+      for (int p = unpublished; p < 2 * q + 2 && p < NP; p++) {
+        gu64* base = pub + (size_t)p * kMc2PanelGran;
+        for (int r = 0; r < 16; r++)
+          __hip_atomic_store(base + r * 64 + lane, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(base + 16 * 64 + lane, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) args.counts[g * P + q] = lds.fail == 0 ? 1 : 0;
 }
 
 }  // namespace
@@ -1020,16 +1446,30 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   return full;
 }
 
+// KODR_ELIM_MC: 2 (default) the pipelined kernel, 1 the first multi-workgroup
+// kernel, 0 one workgroup per decoder (A/B knob)
+static int elim_mc_mode() {
+  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 2;
+  return mc;
+}
+
 bool gf_elim_mc_taken(const ElimArgs& args, int G) {
-  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 1;  // A/B knob
-  return mc && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
+  return elim_mc_mode() && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
          G * gf_elim_mc_groups(args.k) <= kElimMcMaxBlocks;
+}
+
+size_t gf_elim_mc_pub_bytes(int k, int G) {
+  const size_t P = (size_t)gf_elim_mc_groups(k);
+  return (size_t)G * std::max<size_t>(P * 32 * 64, 2 * P * kMc2PanelGran) * 8;
 }
 
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
   if (G <= kElimMaxGens && args.k >= 2 && args.k <= 256 && gf_elim_mc_taken(args, G)) {
-    hipLaunchKernelGGL(gf_elim_mc_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(64 * kMcWaves), 0, stream, args);
+    if (elim_mc_mode() == 1)
+      hipLaunchKernelGGL(gf_elim_mc_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(64 * kMcWaves), 0, stream, args);
+    else
+      hipLaunchKernelGGL(gf_elim_mc2_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(1024), 0, stream, args);
     return hipGetLastError();
   }
   if (G > kElimMaxGens || args.k < 2 || args.k > 256 || args.out_pitch % 4 ||

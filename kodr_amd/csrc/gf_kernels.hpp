@@ -125,7 +125,7 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 // host then takes kodr's route); the decoder's T is valid when all are 1.
 constexpr int kElimMcMaxBlocks = 256;
 inline int gf_elim_mc_groups(int k) { return (k + 31) / 32; }
-inline size_t gf_elim_mc_pub_bytes(int k, int G) { return (size_t)G * gf_elim_mc_groups(k) * 32 * 64 * 8; }
+size_t gf_elim_mc_pub_bytes(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 
 // ---- bit-sliced path (gf_bs.hip) ----
