@@ -12,6 +12,7 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <new>
 #include <string>
@@ -102,6 +103,9 @@ struct rlnc_ctx {
   std::vector<uint8_t> elim_host;  // its read-back (grown once, never zero-filled)
   std::vector<uint8_t> elim_hin;   // host side of elim_in (grown once)
   DevBuf gtmat[2];           // grouped GetPieces: transforms of one chunk, alternating per chunk
+  uint8_t* elim_pin = nullptr;      // gf_elim_mc2's direct output: status words + T rows (pinned, coherent)
+  uint8_t* elim_pin_dev = nullptr;  // ... as the device sees it
+  size_t elim_pin_cap = 0;
   DevBuf elim_pub;           // gf_elim_mc's hand-off granules (zeroed when allocated)
   uint32_t elim_epoch = 0;   // gf_elim_mc's launch tag, one per launch
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
@@ -482,6 +486,8 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->elim_tab.release();
   ctx->elim_out.release();
   ctx->elim_pub.release();
+  if (ctx->elim_pin) (void)hipHostFree(ctx->elim_pin);
+  ctx->elim_pin = nullptr;
   ctx->gtmat[0].release();
   ctx->gtmat[1].release();
   if (ctx->side) {
@@ -1793,6 +1799,51 @@ void elim_counts(const kodr_amd::ElimArgs& a, size_t nc, bool mc, const uint8_t*
 }
 constexpr size_t kElimHdr = 4 * kodr_amd::kElimMcMaxBlocks;  // counts / status words ahead of the states
 
+// the pinned, device-mapped buffer gf_elim_mc2 writes its status words and T
+// rows into ("direct"), grown as needed and zeroed when allocated
+int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->elim_pin_cap) return RLNC_OK;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  if (ctx->elim_pin) (void)hipHostFree(ctx->elim_pin);
+  ctx->elim_pin = nullptr;
+  ctx->elim_pin_cap = 0;
+  HIPC(hipHostMalloc((void**)&ctx->elim_pin, bytes, hipHostMallocCoherent));
+  memset(ctx->elim_pin, 0, bytes);
+  HIPC(hipHostGetDevicePointer((void**)&ctx->elim_pin_dev, ctx->elim_pin, 0));
+  ctx->elim_pin_cap = bytes;
+  return RLNC_OK;
+}
+
+// A direct launch's results: the host polls the status words in pinned
+// memory (each workgroup stores its word after its T rows, system-scope
+// release) instead of synchronising the stream and copying; cnt[i] = k when
+// every workgroup of decoder i is done, else 0 (kodr's route on the host).
+// A launch that never reports within 2 s is waited for on the stream once.
+int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt) {
+  const int P = kodr_amd::gf_elim_mc_groups(a.k);
+  const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
+  const size_t nw = nc * (size_t)P;
+  const auto t0 = std::chrono::steady_clock::now();
+  bool synced = false;
+  for (size_t i = 0;;) {
+    while (i < nw && (st[i] & 0x7fffffffu) == a.epoch) i++;
+    if (i == nw) break;
+    if (!synced && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      HIPC(hipStreamSynchronize(ctx->stream));
+      synced = true;
+      continue;
+    }
+    if (synced) break;  // finished without reporting: the host route
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (size_t i = 0; i < nc; i++) {
+    bool ok = true;
+    for (int q = 0; q < P; q++) ok = ok && st[i * P + q] == a.epoch;
+    cnt[i] = ok ? a.k : 0;
+  }
+  return RLNC_OK;
+}
+
 }  // namespace
 
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_t* const* rows,
@@ -1964,6 +2015,15 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.k = (int)k;
     TRY(ctx_elim_mc(ctx, k, nc, &a));
     const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nc);
+    const bool direct = kodr_amd::gf_elim_mc_direct(a, (int)nc);
+    if (direct) {  // T and status straight into pinned host memory
+      TRY(ctx_elim_pin(ctx, hdr + nc * k * k));
+      a.direct = 1;
+      a.out = ctx->elim_pin_dev + hdr;
+      a.out_pitch = k;
+      a.out_gen_stride = k * k;
+      a.counts = reinterpret_cast<int*>(ctx->elim_pin_dev);
+    }
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
       TRY(launch_copies());
@@ -1980,7 +2040,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
 #else
     const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
 #endif
-    if (tonly) {
+    std::vector<int> cntv(nc);
+    const uint8_t* tstates = hostp + hdr;  // T rows (tonly: k x k per decoder) or whole states
+    if (direct) {
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data()));
+      tstates = ctx->elim_pin + hdr;
+    } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
       HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
     } else {
@@ -1997,8 +2062,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     }
 #endif
     if (timing) tt3 = tnow();
-    std::vector<int> cntv(nc);
-    elim_counts(a, nc, mc, hostp, cntv.data());
+    if (!direct) elim_counts(a, nc, mc, hostp, cntv.data());
     const int* cnt = cntv.data();
     // the states into the decoders' host mirrors: independent per decoder,
     // memory-bound (a 256 x 520-byte arena each), so spread over host threads.
@@ -2010,11 +2074,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       size_t c = (size_t)std::max(cnt[i], 0);
       bool ok = false;
       if (c == k && cont)
-        ok = tonly ? d->core.load_continued(hostp + hdr + i * k * k, k, true)
-                   : d->core.load_continued(hostp + hdr + i * ostride, opitch, false);
+        ok = tonly ? d->core.load_continued(tstates + i * k * k, k, true)
+                   : d->core.load_continued(tstates + i * ostride, opitch, false);
       else if (c && !cont)
-        ok = tonly ? c == k && d->core.load_inverse(hostp + hdr + i * k * k, k)
-                   : d->core.load_rref(hostp + hdr + i * ostride, opitch, c);
+        ok = tonly ? c == k && d->core.load_inverse(tstates + i * k * k, k)
+                   : d->core.load_rref(tstates + i * ostride, opitch, c);
       got[i] = ok ? c - r : 0;
     });
     for (size_t i = 0; i < nc; i++) {
@@ -2178,22 +2242,37 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       a.k = (int)k;
       TRY(ctx_elim_mc(ctx, k, nc, &a));
       const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nc);
+      const bool direct = kodr_amd::gf_elim_mc_direct(a, (int)nc);
+      if (direct) {
+        TRY(ctx_elim_pin(ctx, hdr + nc * k * k));
+        a.direct = 1;
+        a.out = ctx->elim_pin_dev + hdr;
+        a.out_pitch = k;
+        a.out_gen_stride = k * k;
+        a.counts = reinterpret_cast<int*>(ctx->elim_pin_dev);
+      }
       HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
       TRY(join());
       const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
-      HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
-      if (tonly)
-        HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
-      else
-        HIPC(ctx->stage.d2h(hostp + hdr, nc * ostride, ctx->elim_out.p + hdr, nc * ostride, nc * ostride, 1,
-                            ctx->stream));
       std::vector<int> cntv(nc);
-      elim_counts(a, nc, mc, hostp, cntv.data());
+      const uint8_t* tstates = hostp + hdr;
+      if (direct) {
+        TRY(elim_direct_wait(ctx, a, nc, cntv.data()));
+        tstates = ctx->elim_pin + hdr;
+      } else {
+        HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
+        if (tonly)
+          HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
+        else
+          HIPC(ctx->stage.d2h(hostp + hdr, nc * ostride, ctx->elim_out.p + hdr, nc * ostride, nc * ostride, 1,
+                              ctx->stream));
+        elim_counts(a, nc, mc, hostp, cntv.data());
+      }
       const int* cnt = cntv.data();
       HostPool::get().run(nc, [&](size_t i) {
         rlnc_decoder* d = ds[el[c0 + i]];
         if (cnt[i] != (int)k) return;  // M singular: the host flush below
-        const uint8_t* st = tonly ? hostp + hdr + i * k * k : hostp + hdr + i * ostride;
+        const uint8_t* st = tonly ? tstates + i * k * k : tstates + i * ostride;
         const size_t sp = tonly ? k : opitch;
         const bool ok = d->core.received() == 0
                             ? (tonly ? d->core.load_inverse(st, sp) : d->core.load_rref(st, sp, k))

@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       for (int i = 0; i < 4; i++) {
         const int gr = 32 * q + 4 * w + i;
         if (gr >= k) continue;
-        uint8_t* row = out + (size_t)gr * args.out_pitch + k;
+        uint8_t* row = out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k);
 #pragma unroll
         for (int b = 0; b < 4; b++)
           if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(R[i] >> (8 * b));
@@ -1389,8 +1389,17 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       }
     }
   }
+  if (args.direct) __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
   __syncthreads();
-  if (tid == 0) args.counts[g * P + q] = lds.fail == 0 ? 1 : 0;
+  if (tid == 0) {
+    if (args.direct) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      __hip_atomic_store(&args.counts[g * P + q], (int)(lds.fail == 0 ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      args.counts[g * P + q] = lds.fail == 0 ? 1 : 0;
+    }
+  }
 }
 
 }  // namespace
@@ -1457,6 +1466,8 @@ bool gf_elim_mc_taken(const ElimArgs& args, int G) {
   return elim_mc_mode() && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
          G * gf_elim_mc_groups(args.k) <= kElimMcMaxBlocks;
 }
+
+bool gf_elim_mc_direct(const ElimArgs& args, int G) { return gf_elim_mc_taken(args, G) && elim_mc_mode() == 2; }
 
 size_t gf_elim_mc_pub_bytes(int k, int G) {
   const size_t P = (size_t)gf_elim_mc_groups(k);

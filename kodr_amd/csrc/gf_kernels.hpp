@@ -107,6 +107,11 @@ struct ElimArgs {
   // when allocated) and this launch's tag (1 .. 2^31 - 1, a new one per launch)
   uint64_t* pub;
   uint32_t epoch;
+  // gf_elim_mc2 only ("direct"): T rows at out + row * out_pitch (no [I]
+  // part), and the status words counts[g * groups + q] = epoch (done) or
+  // epoch | 0x80000000 (failed), stored with system-scope release after the
+  // workgroup's T rows, so a host polling pinned memory can read them early
+  int direct;
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;
@@ -127,6 +132,8 @@ constexpr int kElimMcMaxBlocks = 256;
 inline int gf_elim_mc_groups(int k) { return (k + 31) / 32; }
 size_t gf_elim_mc_pub_bytes(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
+// true when gf_elim_mc_taken and the launch honours args.direct (mc2)
+bool gf_elim_mc_direct(const ElimArgs& args, int G);
 
 // ---- bit-sliced path (gf_bs.hip) ----
 // dst = src with every 32-byte block of rows [0, rows) x [0, round_up(ncols,
