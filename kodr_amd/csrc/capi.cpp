@@ -1353,12 +1353,37 @@ int dec_check(rlnc_decoder* d, size_t vlen, const uint8_t* piece, size_t plen) {
 
 int dec_progress(rlnc_decoder* d, long only);
 
+extern "C++" {
+template <class F>
+int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read);
+}
+
+// One decoder's elimination goes to the GPU (gf_elim_mc2, many workgroups)
+// instead of the host when its n new rows complete the rank of a state of
+// kept rows (fresh or continued: the full-batch case) and k is at least
+// KODR_ROUTE_MIN_K (default kRouteMinK, where the GPU measured faster).
+constexpr size_t kRouteMinK = 128;
+bool dec_route_gpu(const rlnc_decoder* d, size_t n) {
+  const char* e = getenv("KODR_ROUTE_MIN_K");  // read per call: tests switch it to keep host references
+  const size_t min_k = e ? (size_t)atol(e) : kRouteMinK;
+  const size_t k = d->core.piece_count(), r = d->core.received();
+  return d->ctx && k >= min_k && k <= 256 && n >= 2 && d->core.rank() == r && r + n >= k &&
+         kodr_amd::gf_elim_mc_enabled();
+}
+
 // the queued coding vectors through kodr's elimination as one batch.  They
 // were queued only while useful + queued < k, and each row raises the row
 // count by at most one, so the rank can complete only at the last of them and
 // add_many accepts all (none is refused as "all useful pieces received").
+// A queue that completes the rank of a large decoder is eliminated on the GPU
+// (dec_route_gpu); a singular one stays queued for the host.
 void dec_flush_coef(rlnc_decoder* d) {
   if (!d->npend) return;
+  if (dec_route_gpu(d, d->npend)) {
+    rlnc_decoder* one = d;
+    (void)dec_elim_queues_gpu(&one, 1, [] { return RLNC_OK; });
+    if (!d->npend) return;
+  }
   size_t used = 0;
   (void)d->core.add_many(d->pend_v.data(), d->core.piece_count(), d->npend, &used);
   d->npend = 0;
@@ -1685,8 +1710,11 @@ int dec_batch_post(rlnc_decoder* d, const uint8_t* rows, size_t pitch, bool dev,
 
 }  // namespace
 
-int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
-                            size_t piece_len, int is_device, size_t* consumed) {
+}  // extern "C"
+namespace {
+// rlnc_decoder_add_pieces with kodr's elimination on the host
+int dec_add_pieces_host(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch, size_t piece_len,
+                        int is_device, size_t* consumed) {
   if (!d || !rows || !consumed) return RLNC_ERR_INVALID_ARGUMENT;
   *consumed = 0;
   if (!count) return RLNC_OK;
@@ -1724,6 +1752,20 @@ int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, 
   if (n && d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
   *consumed = n;
   return st;
+}
+}  // namespace
+extern "C" {
+
+// Batched AddPiece: device rows that complete the rank of a large decoder go
+// through the GPU elimination (rlnc_decoder_add_pieces_gpu), the rest through
+// kodr's algorithm on the host.  Same state either way.
+int rlnc_decoder_add_pieces(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pitch,
+                            size_t piece_len, int is_device, size_t* consumed) {
+  if (d && rows && consumed && count && is_device && d->ctx && pitch >= d->core.piece_count() + piece_len) {
+    TRY(dec_flush(d));
+    if (dec_route_gpu(d, count)) return rlnc_decoder_add_pieces_gpu(d, rows, count, pitch, piece_len, consumed);
+  }
+  return dec_add_pieces_host(d, rows, count, pitch, piece_len, is_device, consumed);
 }
 
 namespace {
@@ -1890,7 +1932,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     const bool cont = r >= 1 && r < k && d->core.rank() == r && r + counts[g] >= k;
     const bool ok = k >= 2 && k <= 256 && counts[g] >= 2 && (r == 0 || cont);
     if (!ok) {
-      status[g] = rlnc_decoder_add_pieces(d, rows[g], counts[g], pitch, piece_len, 1, &consumed[g]);
+      status[g] = dec_add_pieces_host(d, rows[g], counts[g], pitch, piece_len, 1, &consumed[g]);
       continue;
     }
     if ((status[g] = dec_check(d, k, rows[g] + k, piece_len)) != RLNC_OK) continue;
@@ -2124,82 +2166,22 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* d, const uint8_t* rows, size_t cou
   return st;
 }
 
-// The lazy queues of G decoders (one AddPiece call per piece) eliminated
-// together: every decoder whose queued vectors complete its rank from a
-// state of kept rows -- fresh (r = 0) or continued -- in one GPU launch per
-// kElimMaxGens, from M = [its r coefficient rows ; the queued vectors], all on
-// the host already (one upload); the others, and any singular M, through
-// the host flush their next state read would run.  Every decoder's borrowed
-// device pieces are gathered by one launch beside the elimination.  Same
-// state as G host flushes.
-int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
-  if (!ds || !G || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
+}  // extern "C"
+namespace {
+// The lazy AddPiece queues of G decoders (one context, one piece_count)
+// through the GPU elimination: every decoder whose queued vectors complete
+// its rank from a state of kept rows (fresh or continued) in one launch per
+// elim_chunk decoders, from M = [its r coefficient rows ; the queued vectors]
+// (one upload); a singular M, and the decoders that do not qualify, keep
+// their queues (the host flush takes them).  before_read runs after the
+// launch and before the results are read (the grouped flush joins its gather
+// there).
+template <class F>
+int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read) {
   rlnc_ctx* ctx = ds[0]->ctx;
-  if (!ctx) return RLNC_ERR_NO_DEVICE;
   const size_t k = ds[0]->core.piece_count();
-  for (size_t g = 0; g < G; g++)
-    if (!ds[g] || ds[g]->ctx != ctx || ds[g]->core.piece_count() != k) return RLNC_ERR_INVALID_ARGUMENT;
-  {  // each decoder once: their host mirrors are loaded concurrently below
-    std::vector<const rlnc_decoder*> u(ds, ds + G);
-    std::sort(u.begin(), u.end());
-    if (std::adjacent_find(u.begin(), u.end()) != u.end()) return RLNC_ERR_INVALID_ARGUMENT;
-  }
   TRY(set_dev(ctx));
-  // the borrowed device pieces of every decoder (of the first one's piece
-  // length) in ONE gather launch from uploaded source / destination tables,
-  // on the side stream beside the elimination
-  std::vector<const void*> gsrc, gdst;
-  std::vector<rlnc_decoder*> gdec;
-  size_t gL = 0;
-  for (size_t g = 0; g < G; g++) {
-    rlnc_decoder* d = ds[g];
-    if (d->pend_src.empty()) continue;
-    if (!gL) gL = d->L;
-    if (d->L != gL) continue;  // dec_flush below
-    TRY(dec_reserve_rows(d, d->pend_row0 + d->pend_src.size(), d->pend_row0));
-    gdec.push_back(d);
-  }
-  // every receive buffer is in place: the queues move into the tables
-  for (rlnc_decoder* d : gdec) {
-    for (size_t j = 0; j < d->pend_src.size(); j++) {
-      gsrc.push_back(d->pend_src[j]);
-      gdst.push_back(d->recv.p + (d->pend_row0 + j) * d->pitch);
-    }
-    d->pend_src.clear();
-  }
-  bool gjoined = true;
-  // an error return joins too: the context stream must not run past a gather
-  // that still reads gtab and writes receive rows
-  auto join_guard = on_scope_exit([&] {
-    if (!gjoined) (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
-  });
-  if (!gsrc.empty()) {
-    const size_t nr = gsrc.size();
-    std::vector<const void*> tab(gsrc);
-    tab.insert(tab.end(), gdst.begin(), gdst.end());
-    ctx->gtab.bind(ctx->device, ctx->stream);
-    TRY(ctx->gtab.reserve(tab.size() * sizeof(void*)));
-    const size_t tb = tab.size() * sizeof(void*);
-    HIPC(ctx->stage.h2d(ctx->gtab.p, tb, reinterpret_cast<const uint8_t*>(tab.data()), tb, tb, 1, ctx->stream));
-    hipStream_t gs = ctx->stream;
-    if (add_side_stream()) {
-      TRY(ctx_side(ctx));
-      HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the tables and any grown receive buffers first
-      HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
-      gs = ctx->side;
-      gjoined = false;
-    }
-    const auto* src = reinterpret_cast<const uint8_t* const*>(ctx->gtab.p);
-    const auto* dst = reinterpret_cast<uint8_t* const*>(ctx->gtab.p + nr * sizeof(void*));
-    for (size_t r0 = 0; r0 < nr; r0 += 65535)
-      HIPC(kodr_amd::gather_rows(src + r0, nullptr, 0, std::min<size_t>(65535, nr - r0), gL, gs, dst + r0));
-    if (!gjoined) HIPC(hipEventRecord(ctx->side_done, ctx->side));
-  }
-  auto join = [&]() -> int {  // everything after this point on the context stream sees the gathered rows
-    if (!gjoined) HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));
-    gjoined = true;
-    return RLNC_OK;
-  };
+  auto join = before_read;
   std::vector<size_t> el;
   for (size_t g = 0; g < G; g++) {
     const rlnc_decoder* d = ds[g];
@@ -2281,6 +2263,89 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
       });
     }
   }
+  return RLNC_OK;
+}
+
+}  // namespace
+extern "C" {
+
+// The lazy queues of G decoders (one AddPiece call per piece) eliminated
+// together: every decoder whose queued vectors complete its rank from a
+// state of kept rows -- fresh (r = 0) or continued -- in one GPU launch per
+// kElimMaxGens, from M = [its r coefficient rows ; the queued vectors], all on
+// the host already (one upload); the others, and any singular M, through
+// the host flush their next state read would run.  Every decoder's borrowed
+// device pieces are gathered by one launch beside the elimination.  Same
+// state as G host flushes.
+int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
+  if (!ds || !G || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
+  rlnc_ctx* ctx = ds[0]->ctx;
+  if (!ctx) return RLNC_ERR_NO_DEVICE;
+  const size_t k = ds[0]->core.piece_count();
+  for (size_t g = 0; g < G; g++)
+    if (!ds[g] || ds[g]->ctx != ctx || ds[g]->core.piece_count() != k) return RLNC_ERR_INVALID_ARGUMENT;
+  {  // each decoder once: their host mirrors are loaded concurrently below
+    std::vector<const rlnc_decoder*> u(ds, ds + G);
+    std::sort(u.begin(), u.end());
+    if (std::adjacent_find(u.begin(), u.end()) != u.end()) return RLNC_ERR_INVALID_ARGUMENT;
+  }
+  TRY(set_dev(ctx));
+  // the borrowed device pieces of every decoder (of the first one's piece
+  // length) in ONE gather launch from uploaded source / destination tables,
+  // on the side stream beside the elimination
+  std::vector<const void*> gsrc, gdst;
+  std::vector<rlnc_decoder*> gdec;
+  size_t gL = 0;
+  for (size_t g = 0; g < G; g++) {
+    rlnc_decoder* d = ds[g];
+    if (d->pend_src.empty()) continue;
+    if (!gL) gL = d->L;
+    if (d->L != gL) continue;  // dec_flush below
+    TRY(dec_reserve_rows(d, d->pend_row0 + d->pend_src.size(), d->pend_row0));
+    gdec.push_back(d);
+  }
+  // every receive buffer is in place: the queues move into the tables
+  for (rlnc_decoder* d : gdec) {
+    for (size_t j = 0; j < d->pend_src.size(); j++) {
+      gsrc.push_back(d->pend_src[j]);
+      gdst.push_back(d->recv.p + (d->pend_row0 + j) * d->pitch);
+    }
+    d->pend_src.clear();
+  }
+  bool gjoined = true;
+  // an error return joins too: the context stream must not run past a gather
+  // that still reads gtab and writes receive rows
+  auto join_guard = on_scope_exit([&] {
+    if (!gjoined) (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
+  });
+  if (!gsrc.empty()) {
+    const size_t nr = gsrc.size();
+    std::vector<const void*> tab(gsrc);
+    tab.insert(tab.end(), gdst.begin(), gdst.end());
+    ctx->gtab.bind(ctx->device, ctx->stream);
+    TRY(ctx->gtab.reserve(tab.size() * sizeof(void*)));
+    const size_t tb = tab.size() * sizeof(void*);
+    HIPC(ctx->stage.h2d(ctx->gtab.p, tb, reinterpret_cast<const uint8_t*>(tab.data()), tb, tb, 1, ctx->stream));
+    hipStream_t gs = ctx->stream;
+    if (add_side_stream()) {
+      TRY(ctx_side(ctx));
+      HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the tables and any grown receive buffers first
+      HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
+      gs = ctx->side;
+      gjoined = false;
+    }
+    const auto* src = reinterpret_cast<const uint8_t* const*>(ctx->gtab.p);
+    const auto* dst = reinterpret_cast<uint8_t* const*>(ctx->gtab.p + nr * sizeof(void*));
+    for (size_t r0 = 0; r0 < nr; r0 += 65535)
+      HIPC(kodr_amd::gather_rows(src + r0, nullptr, 0, std::min<size_t>(65535, nr - r0), gL, gs, dst + r0));
+    if (!gjoined) HIPC(hipEventRecord(ctx->side_done, ctx->side));
+  }
+  auto join = [&]() -> int {  // everything after this point on the context stream sees the gathered rows
+    if (!gjoined) HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));
+    gjoined = true;
+    return RLNC_OK;
+  };
+  TRY(dec_elim_queues_gpu(ds, G, join));
   TRY(join());
   for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
   return RLNC_OK;

@@ -1467,6 +1467,8 @@ bool gf_elim_mc_taken(const ElimArgs& args, int G) {
          G * gf_elim_mc_groups(args.k) <= kElimMcMaxBlocks;
 }
 
+bool gf_elim_mc_enabled() { return elim_mc_mode() != 0; }
+
 bool gf_elim_mc_direct(const ElimArgs& args, int G) { return gf_elim_mc_taken(args, G) && elim_mc_mode() == 2; }
 
 size_t gf_elim_mc_pub_bytes(int k, int G) {

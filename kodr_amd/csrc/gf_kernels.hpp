@@ -134,6 +134,7 @@ size_t gf_elim_mc_pub_bytes(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 // true when gf_elim_mc_taken and the launch honours args.direct (mc2)
 bool gf_elim_mc_direct(const ElimArgs& args, int G);
+bool gf_elim_mc_enabled();  // KODR_ELIM_MC != 0
 
 // ---- bit-sliced path (gf_bs.hip) ----
 // dst = src with every 32-byte block of rows [0, rows) x [0, round_up(ncols,

@@ -86,6 +86,14 @@ def _rows(ctx, V, P, L):
     return d, pitch
 
 
+@pytest.fixture(autouse=True)
+def host_references(monkeypatch):
+    # the reference decoders here run kodr's elimination on the host:
+    # rlnc_decoder_add_pieces and the lazy flush would otherwise route large
+    # full batches to the GPU elimination themselves (capi.cpp dec_route_gpu)
+    monkeypatch.setenv("KODR_ROUTE_MIN_K", "100000")
+
+
 def _same(a, b):
     assert a.state() == b.state()
     assert np.array_equal(a.coefficients(), b.coefficients())
@@ -357,3 +365,45 @@ def test_gpu_elimination_continued_batches(gpu_ctx, k):
     gpu_ctx.synchronize()
     for d in bufs:
         gpu_ctx.free(d)
+
+
+@pytest.mark.parametrize("kind", ["dense", "systematic", "first_zero", "tiny"])
+@pytest.mark.parametrize("k", [128, 200, 256])
+def test_routed_single_decoder_vs_oracle(gpu_ctx, monkeypatch, kind, k):
+    """rlnc_decoder_add_pieces (device rows) and lazy AddPiece flushes route a
+    large decoder's full batch to the multi-workgroup GPU elimination
+    (capi.cpp dec_route_gpu); singular blocks fall back to the host.  Both
+    entry points against the oracle's literal decoder: return code, rows
+    consumed, counters, coefficients and decoded pieces."""
+    monkeypatch.setenv("KODR_ROUTE_MIN_K", "128")
+    rng = np.random.default_rng(k * 7 + len(kind))
+    L = 64
+    P = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    n = k + 3
+    V = _vectors(rng, kind, n, k)
+    drows, pitch = _rows(gpu_ctx, V, P, L)
+    ref = oracle.Decoder(k)
+    C = oracle.encode(P, V)
+    sts = [ref.add(V[i], C[i]) for i in range(n)]
+    exp_n = next((i for i, s_ in enumerate(sts) if s_ != 0), n)
+    lib = _lib.lib()
+    # batched
+    bat = Dec(gpu_ctx, k)
+    c = ctypes.c_size_t()
+    st = lib.rlnc_decoder_add_pieces(bat.h, ctypes.c_void_p(drows), n, pitch, L, 1, ctypes.byref(c))
+    assert (st, c.value) == (sts[exp_n] if exp_n < n else 0, exp_n)
+    # one AddPiece call per piece (lazy queue, flushed when it completes the rank)
+    pw = Dec(gpu_ctx, k)
+    got = []
+    for i in range(n):
+        v = np.ascontiguousarray(V[i])
+        got.append(lib.rlnc_decoder_add_piece_device(pw.h, v.ctypes.data_as(U8P), k, drows + i * pitch + k, L))
+    assert got == sts
+    for d in (bat, pw):
+        assert d.state() == (ref.useful(), ref.received(), ref.required(), ref.is_decoded())
+        assert np.array_equal(d.coefficients(), ref.coeffs())
+        if ref.is_decoded():
+            s1, out = d.get_all()
+            assert s1 == 0 and np.array_equal(out, P)
+    gpu_ctx.synchronize()
+    gpu_ctx.free(drows)
