@@ -1801,6 +1801,8 @@ int ctx_elim_tables(rlnc_ctx* ctx) {
 // launch's epoch (a new tag per launch; the buffer is zeroed when it is
 // allocated and when the tags wrap)
 int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
+  static const int variant = getenv("KODR_MC2_VARIANT") ? atoi(getenv("KODR_MC2_VARIANT")) : 0;
+  a->variant = variant;
   const size_t bytes = kodr_amd::gf_elim_mc_pub_bytes((int)k, (int)nc);
   ctx->elim_pub.bind(ctx->device, ctx->stream);
   const uint8_t* before = ctx->elim_pub.p;

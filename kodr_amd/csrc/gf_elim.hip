@@ -1058,6 +1058,8 @@ struct ElimMc2Lds {
   uint32_t fw[8][4][4];            // row wave w: G of its rows
   uint32_t ft[16][4];              // chain: F of the block rows
   uint32_t pan[16][4];             // chain: the block to invert
+  uint32_t part[8][16][4];         // chain: the chain waves' partial products (split variant)
+  int chain_sync;                  // chain-wave rounds (split variant: 8 per round)
   int rows_done;                   // row-wave iterations finished (8 per panel, 8 for the start)
   int chain_cnt;                   // chain-wave iterations finished (8 per panel)
   int fail;                        // 1 singular / FAIL seen, 2 timeout
@@ -1082,6 +1084,15 @@ __device__ __forceinline__ void mc2_signal(int* ctr, int lane) {
 
 // mc_panel_gj's algorithm on an LDS block, S to `s_out` ([16][4]), its rows
 // also kept in registers for publishing (returns false if singular)
+// lane (t, d) gets dword d of block row tp: four v_readlane and a select,
+// instead of a ds_bpermute round trip
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int tp, int d) {
+  const uint32_t a0 = __builtin_amdgcn_readlane(v, 4 * tp), a1 = __builtin_amdgcn_readlane(v, 4 * tp + 1);
+  const uint32_t a2 = __builtin_amdgcn_readlane(v, 4 * tp + 2), a3 = __builtin_amdgcn_readlane(v, 4 * tp + 3);
+  return d == 0 ? a0 : d == 1 ? a1 : d == 2 ? a2 : a3;
+}
+
+template <bool RL>
 __device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab, const uint32_t (*pan)[4],
                                              uint32_t (*s_out)[4], int lane, uint32_t* s_val, int* s_row) {
   const int t = lane >> 2, d = lane & 3;
@@ -1101,7 +1112,8 @@ __device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab
     const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
     const uint4 ti = itab[2 * dp];
     const uint32_t ti2 = itab[2 * dp + 1].x;
-    const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
+    const uint32_t Pp = RL ? row_bcast(P, tp, d) : bperm(P, tp * 4 + d);
+    const uint32_t Tp = RL ? row_bcast(Tr, tp, d) : bperm(Tr, tp * 4 + d);
     const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
     const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
     if (t == tp) {
@@ -1120,18 +1132,21 @@ __device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab
   return true;
 }
 
-// out[t][d] = base ^ sum_c M[t][c] x X[c][d], one wave, lane (t, d): M rows
-// are 4 dwords (16 bytes), X rows 4 dwords
+// out[t][d] = base ^ sum_c M[t][c] x X[c][d], one wave, lane (t, d): the M
+// row (4 dwords, 16 bytes) and X rows (4 dwords) in LDS
 __device__ __forceinline__ uint32_t mc2_small(const uint4* tab, uint32_t base, const uint32_t* mrow,
                                               const uint32_t (*x)[4], int d) {
   uint32_t acc = base;
-#pragma unroll 4
-  for (int c = 0; c < 16; c++) {
-    const uint32_t m = (mrow[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    const uint4 t = tab[2 * m];
-    const uint32_t t2 = tab[2 * m + 1].x;
-    const uint32_t xv = x[c][d];
-    acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+  for (int cq = 0; cq < 4; cq++) {
+    const uint32_t mw = mrow[cq];
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) {
+      const uint32_t m = (mw >> (8 * cc)) & 0xffu;
+      const uint4 t = tab[2 * m];
+      const uint32_t t2 = tab[2 * m + 1].x;
+      const uint32_t xv = x[4 * cq + cc][d];
+      acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+    }
   }
   return acc;
 }
@@ -1154,6 +1169,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   if (tid == 0) {
     lds.rows_done = 0;
     lds.chain_cnt = 0;
+    lds.chain_sync = 0;
     lds.fail = 0;
   }
   __syncthreads();
@@ -1186,13 +1202,9 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
     auto apply = [&](int pa) {
       const int slot = pa % kMc2Slots, db = 4 * pa;
       const bool own = (pa >> 1) == q && (pa & 1) == half;
-      uint32_t G[4][4];
-      if (own) {
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-#pragma unroll
-          for (int u = 0; u < 4; u++) G[i][u] = __builtin_amdgcn_readfirstlane(lds.sp[slot][4 * (w & 3) + i][u]);
-      } else {
+      // G of the 4 rows: the panel's S rows (own) or F (in lds.fw)
+      const uint32_t(*Gp)[4] = own ? &lds.sp[slot][4 * (w & 3)] : lds.fw[w];
+      if (!own) {
         // F of the 4 rows: lane (cg, i, u) sums c = 4 cg .. 4 cg + 3, then
         // the four groups are folded (lanes 16 and 32 apart)
         if (lane >= db && lane < db + 4)
@@ -1214,34 +1226,30 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         acc ^= bperm(acc, lane ^ 32);
         if (lane < 16) lds.fw[w][i][u] = acc;
         __builtin_amdgcn_s_waitcnt(0xc07f);
-#pragma unroll
-        for (int i2 = 0; i2 < 4; i2++)
-#pragma unroll
-          for (int u2 = 0; u2 < 4; u2++) G[i2][u2] = __builtin_amdgcn_readfirstlane(lds.fw[w][i2][u2]);
       }
       uint32_t acc[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
-#pragma unroll 2
-      for (int c = 0; c < 16; c++) {
-        const uint32_t x = lds.rp[slot][c][lane];
-        const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+      for (int cq = 0; cq < 4; cq++) {
+        uint32_t gw[4];  // dword cq of each row's G (wave-uniform)
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t f = (G[i][c >> 2] >> (8 * (c & 3))) & 0xffu;
-          const uint4 t = lds.tab[2 * f];
-          const uint32_t t2 = lds.tab[2 * f + 1].x;
-          acc[i] ^= mc_mul(t, t2, s0, s1, s2);
+        for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          const uint32_t x = lds.rp[slot][4 * cq + cc][lane];
+          const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
+            const uint4 t = lds.tab[2 * f];
+            const uint32_t t2 = lds.tab[2 * f + 1].x;
+            acc[i] ^= mc_mul(t, t2, s0, s1, s2);
+          }
         }
       }
+      const int u = lane - db;  // the panel columns take G
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        uint32_t v = acc[i];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (lane == db + u) v = G[i][u];
-        R[i] = v;
-      }
+      for (int i = 0; i < 4; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
     };
 
     for (int p = 0; p < NP; p++) {
@@ -1289,6 +1297,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
     const int cw = w - 8;
     if (cw == 0) __builtin_amdgcn_s_setprio(3);
     int unpublished = 2 * q;  // the first owned panel whose S_p is not out yet
+    int nsync = 0;            // chain_sync rounds so far (split variant)
     for (int p = 0; p < NP; p++) {
       const int slot = p % kMc2Slots;
       gu64* base = pub + (size_t)p * kMc2PanelGran;
@@ -1297,28 +1306,65 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       if (!mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
       if ((p >> 1) == q) {
         if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
+        const bool split = (args.variant & 1) && p >= 1;
+        if (split) {
+          // the block's two small products with their 16 terms split over the
+          // 8 chain waves (2 each), partials folded through LDS
+          const int t = lane >> 2, d = lane & 3, ps = (p - 1) % kMc2Slots;
+          const int c0 = 2 * cw;
+          uint32_t acc = 0;
+#pragma unroll
+          for (int cc = 0; cc < 2; cc++) {  // F = M x S_{p-1}
+            const uint32_t m = (lds.mb[slot][t][c0 >> 2] >> (8 * ((c0 + cc) & 3))) & 0xffu;
+            const uint4 tt = lds.tab[2 * m];
+            const uint32_t tt2 = lds.tab[2 * m + 1].x;
+            const uint32_t xv = lds.sp[ps][c0 + cc][d];
+            acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+          }
+          lds.part[cw][t][d] = acc;
+          mc2_signal(&lds.chain_sync, lane);
+          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
+          uint32_t fdw = 0;  // dword c0 / 4 of F's row t: the bytes of this wave's two terms
+#pragma unroll
+          for (int j = 0; j < 8; j++) fdw ^= lds.part[j][t][c0 >> 2];
+          uint32_t acc2 = 0;
+#pragma unroll
+          for (int cc = 0; cc < 2; cc++) {  // block ^= F x R_{p-1}[:, panel p]
+            const uint32_t m = (fdw >> (8 * ((c0 + cc) & 3))) & 0xffu;
+            const uint4 tt = lds.tab[2 * m];
+            const uint32_t tt2 = lds.tab[2 * m + 1].x;
+            const uint32_t xv = lds.rp[ps][c0 + cc][4 * p + d];
+            acc2 ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+          }
+          // every wave has read part[] (its F dword) before anyone overwrites it
+          mc2_signal(&lds.chain_sync, lane);
+          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
+          lds.part[cw][t][d] = acc2;
+          mc2_signal(&lds.chain_sync, lane);
+          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
+        }
         if (cw == 0) {
           const int t = lane >> 2, d = lane & 3;
           uint32_t blk = lds.mb[slot][t][4 + d];
-          if (p >= 1) {
+          if (split) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) blk ^= lds.part[j][t][d];
+          } else if (p >= 1) {
             const int ps = (p - 1) % kMc2Slots;
-            uint32_t mrow[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) mrow[u] = lds.mb[slot][t][u];
-            lds.ft[t][d] = mc2_small(lds.tab, 0u, mrow, lds.sp[ps], d);  // F = M x S_{p-1}
+            lds.ft[t][d] = mc2_small(lds.tab, 0u, lds.mb[slot][t], lds.sp[ps], d);  // F = M x S_{p-1}
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            uint32_t frow[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) frow[u] = lds.ft[t][u];
             // block ^= F x R_{p-1}[:, panel p]
             uint32_t acc = blk;
-#pragma unroll 4
-            for (int c = 0; c < 16; c++) {
-              const uint32_t m = (frow[c >> 2] >> (8 * (c & 3))) & 0xffu;
-              const uint4 tt = lds.tab[2 * m];
-              const uint32_t tt2 = lds.tab[2 * m + 1].x;
-              const uint32_t xv = lds.rp[ps][c][4 * p + d];
-              acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+            for (int cq = 0; cq < 4; cq++) {
+              const uint32_t fw = lds.ft[t][cq];
+#pragma unroll
+              for (int cc = 0; cc < 4; cc++) {
+                const uint32_t m = (fw >> (8 * cc)) & 0xffu;
+                const uint4 tt = lds.tab[2 * m];
+                const uint32_t tt2 = lds.tab[2 * m + 1].x;
+                const uint32_t xv = lds.rp[ps][4 * cq + cc][4 * p + d];
+                acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+              }
             }
             blk = acc;
           }
@@ -1326,7 +1372,10 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
           __builtin_amdgcn_s_waitcnt(0xc07f);
           uint32_t sval = 0;
           int srow = 0;
-          if (!mc2_panel_gj(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow)) {
+          const bool inv_ok = (args.variant & 2)
+                                  ? mc2_panel_gj<true>(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow)
+                                  : mc2_panel_gj<false>(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow);
+          if (!inv_ok) {
             __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
             __hip_atomic_store(base + 16 * 64 + srow * 4 + d, ((unsigned long long)epoch << 32) | sval,

@@ -112,6 +112,8 @@ struct ElimArgs {
   // epoch | 0x80000000 (failed), stored with system-scope release after the
   // workgroup's T rows, so a host polling pinned memory can read them early
   int direct;
+  int variant;  // gf_elim_mc2 tuning bits (KODR_MC2_VARIANT): 1 split the block's small
+                // products over the chain waves, 2 pivot-row broadcast by v_readlane
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;
