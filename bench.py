@@ -34,6 +34,23 @@ K_PIECES, L_BYTES = 256, 131072          # 32 MiB / 256 pieces
 HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+class host_elimination:
+    """The comparisons' host legs run kodr's elimination on the host:
+    rlnc_decoder_add_pieces and the lazy AddPiece flush would otherwise take
+    the GPU elimination themselves for large full batches (capi.cpp
+    dec_route_gpu, KODR_ROUTE_MIN_K read per call)."""
+
+    def __enter__(self):
+        self.prev = os.environ.get("KODR_ROUTE_MIN_K")
+        os.environ["KODR_ROUTE_MIN_K"] = "100000"
+
+    def __exit__(self, *exc):
+        if self.prev is None:
+            os.environ.pop("KODR_ROUTE_MIN_K", None)
+        else:
+            os.environ["KODR_ROUTE_MIN_K"] = self.prev
+
+
 def setbytes(k, L, padding=0):
     # benches/full/encoder_test.go:53  SetBytes(total + padding + CodedPieceLen)
     return k * L + padding + (k + L)
@@ -1167,10 +1184,11 @@ def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
             ctx.synchronize()
             t0 = time.perf_counter()
             if mode == "host":
-                for g in range(G):
-                    c = ctypes.c_size_t()
-                    st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g], n, pitch, L, 1, ctypes.byref(c))
-                    ok = ok and st in (0, 3)
+                with host_elimination():
+                    for g in range(G):
+                        c = ctypes.c_size_t()
+                        st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g], n, pitch, L, 1, ctypes.byref(c))
+                        ok = ok and st in (0, 3)
             else:
                 cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
                 errors.check(L_.rlnc_decoders_add_pieces_gpu((ctypes.c_void_p * G)(*[x.value for x in decs]), G,
@@ -1232,8 +1250,9 @@ def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
             if mode == "gpu":
                 errors.check(L_.rlnc_decoders_flush_gpu(darr, G))
             else:
-                for h in decs:
-                    L_.rlnc_decoder_is_decoded(h)
+                with host_elimination():
+                    for h in decs:
+                        L_.rlnc_decoder_is_decoded(h)
             t2 = time.perf_counter()
             for h, v, p_ in args[k * G:]:
                 if add(h, v, k, p_, L) not in (0, 3):
@@ -1303,11 +1322,12 @@ def batched_elim_rounds(ctx, L_, errors, rng, k=256, G=32, L=256, rounds=4, reps
                 t0 = time.perf_counter()
                 cnt = cuts[r + 1] - cuts[r]
                 if mode == "host":
-                    for g in range(G):
-                        c = ctypes.c_size_t()
-                        st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g] + cuts[r] * pitch, cnt, pitch, L, 1,
-                                                        ctypes.byref(c))
-                        ok = ok and st in (0, 3)
+                    with host_elimination():
+                        for g in range(G):
+                            c = ctypes.c_size_t()
+                            st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g] + cuts[r] * pitch, cnt, pitch, L, 1,
+                                                            ctypes.byref(c))
+                            ok = ok and st in (0, 3)
                 else:
                     cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
                     errors.check(L_.rlnc_decoders_add_pieces_gpu(
