@@ -1377,9 +1377,23 @@ bool dec_route_gpu(const rlnc_decoder* d, size_t n) {
 // add_many accepts all (none is refused as "all useful pieces received").
 // A queue that completes the rank of a large decoder is eliminated on the GPU
 // (dec_route_gpu); a singular one stays queued for the host.
+// a systematic-looking queue (one of its first rows a unit vector) stays on
+// the host, whose solver copies such rows (DecoderCore::solve_systematic_batch);
+// the GPU's block pivots would find its blocks singular
+bool queue_looks_systematic(const rlnc_decoder* d) {
+  const size_t k = d->core.piece_count();
+  for (size_t i = 0; i < std::min<size_t>(d->npend, 4); i++) {
+    const uint8_t* v = d->pend_v.data() + i * k;
+    size_t nz = 0;
+    for (size_t j = 0; j < k && nz < 2; j++) nz += v[j] != 0;
+    if (nz == 1) return true;
+  }
+  return false;
+}
+
 void dec_flush_coef(rlnc_decoder* d) {
   if (!d->npend) return;
-  if (dec_route_gpu(d, d->npend)) {
+  if (dec_route_gpu(d, d->npend) && !queue_looks_systematic(d)) {
     rlnc_decoder* one = d;
     (void)dec_elim_queues_gpu(&one, 1, [] { return RLNC_OK; });
     if (!d->npend) return;
