@@ -1361,8 +1361,9 @@ int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read);
 // One decoder's elimination goes to the GPU (gf_elim_mc2, many workgroups)
 // instead of the host when its n new rows complete the rank of a state of
 // kept rows (fresh or continued: the full-batch case) and k is at least
-// KODR_ROUTE_MIN_K (default kRouteMinK, where the GPU measured faster).
-constexpr size_t kRouteMinK = 128;
+// KODR_ROUTE_MIN_K (default kRouteMinK: the route is off by default while the
+// single-decoder GPU elimination measures slower than the host).
+constexpr size_t kRouteMinK = 257;
 bool dec_route_gpu(const rlnc_decoder* d, size_t n) {
   const char* e = getenv("KODR_ROUTE_MIN_K");  // read per call: tests switch it to keep host references
   const size_t min_k = e ? (size_t)atol(e) : kRouteMinK;
@@ -2113,10 +2114,14 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
 #ifdef KODR_ELIM_TIMING
     if (const char* dump = getenv("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
       if (FILE* fp = fopen(dump, "wb")) {
-        fwrite(hostp, 1, hdr + nc * ostride, fp);
+        if (direct)
+          fwrite(ctx->elim_pin, 1, hdr + nc * k * k, fp);
+        else
+          fwrite(hostp, 1, hdr + nc * ostride, fp);
         fclose(fp);
       }
       for (size_t i = 0; i < nc; i++) memset(hostp + i * sizeof(int), 0, sizeof(int));
+      for (size_t i = 0; i < nc; i++) cntv[i] = 0;  // the stamps overwrote T: kodr's route on the host
     }
 #endif
     if (timing) tt3 = tnow();

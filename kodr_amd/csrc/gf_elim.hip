@@ -1159,6 +1159,25 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   const int k = args.k;
   const uint32_t epoch = args.epoch;
   gu64* pub = (gu64*)args.pub + (size_t)g * NP * kMc2PanelGran;
+#ifdef KODR_ELIM_TIMING
+  // tuning build: s_memrealtime (100 MHz) stamps by lane 0 of row wave 0 and
+  // chain wave 0, into this workgroup's 1 KiB of the T region (no result):
+  // chain [4 p + j]: panel p's start, rows ready / polled, small products
+  // done / slot free, end; row wave [64 + p] iteration p done, [80] entry,
+  // [81] rows loaded, [82] last apply done, [83] rows out
+  gu64* const tsout = (gu64*)(args.out + (size_t)g * args.out_gen_stride + (size_t)q * 1024);
+#define MC2_STAMP(i)                                                                                \
+  do {                                                                                              \
+    if (lane == 0)                                                                                  \
+      __hip_atomic_store(tsout + (i), (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                                \
+  } while (0)
+#else
+#define MC2_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+  if (w == 0) MC2_STAMP(80);
 
   for (int i = tid; i < 256 * 2; i += 1024) {
     const uint32_t* a = args.tables + 4 * i;
@@ -1198,6 +1217,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
 #pragma unroll
       for (int i = 0; i < 4; i++) lds.mb[0][4 * w + i][4 + lane] = R[i];
     mc2_signal(&lds.rows_done, lane);
+    if (w == 0) MC2_STAMP(81);
 
     auto apply = [&](int pa) {
       const int slot = pa % kMc2Slots, db = 4 * pa;
@@ -1277,8 +1297,16 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         }
       }
       mc2_signal(&lds.rows_done, lane);
+      if (w == 0) MC2_STAMP(64 + p);
     }
     ok = mc2_wait(lds, &lds.chain_cnt, 8 * NP) && mc2_wait(lds, &lds.rows_done, 8 * (NP + 1));
+#ifdef KODR_ELIM_TIMING
+    if (ok) {
+      apply(NP - 1);
+      if (w == 0) MC2_STAMP(82);
+    }
+    ok = false;
+#endif
     if (ok) {
       apply(NP - 1);
       uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
@@ -1304,8 +1332,10 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       // every chain wave finished panel p - 1 (no wave runs ahead: the count
       // then means exactly that)
       if (!mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+      if (cw == 0) MC2_STAMP(4 * p);
       if ((p >> 1) == q) {
         if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
+        if (cw == 0) MC2_STAMP(4 * p + 1);
         const bool split = (args.variant & 1) && p >= 1;
         if (split) {
           // the block's two small products with their 16 terms split over the
@@ -1370,6 +1400,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
           }
           lds.pan[t][d] = blk;
           __builtin_amdgcn_s_waitcnt(0xc07f);
+          MC2_STAMP(4 * p + 2);
           uint32_t sval = 0;
           int srow = 0;
           const bool inv_ok = (args.variant & 2)
@@ -1382,6 +1413,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             unpublished = p + 1;
           }
+          MC2_STAMP(4 * p + 3);
         }
         if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
         mc2_signal(&lds.chain_cnt, lane);
@@ -1417,11 +1449,14 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
           __hip_atomic_store(&lds.fail, timeout ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           break;
         }
+        if (cw == 0) MC2_STAMP(4 * p + 1);
         if (!mc2_wait(lds, &lds.rows_done, 8 * p)) break;  // the slot's last readers are done
+        if (cw == 0) MC2_STAMP(4 * p + 2);
         lds.rp[slot][2 * cw][lane] = (uint32_t)a;
         lds.rp[slot][2 * cw + 1][lane] = (uint32_t)b;
         if (cw == 0) lds.sp[slot][lane >> 2][lane & 3] = (uint32_t)s;
         mc2_signal(&lds.chain_cnt, lane);
+        if (cw == 0) MC2_STAMP(4 * p + 3);
       }
     }
     ok = __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
@@ -1438,6 +1473,8 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       }
     }
   }
+  if (w == 0) MC2_STAMP(83);
+#undef MC2_STAMP
   if (args.direct) __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
   __syncthreads();
   if (tid == 0) {
