@@ -1,0 +1,297 @@
+// Critical-path probe for gf_elim_mc2_kernel's chain (measurement only, not
+// part of the library): one 1024-thread workgroup; chain wave 8 runs the
+// owned-panel work of the kernel -- the two small products that bring a
+// 16 x 16 block up to date with the previous panel, then its inversion --
+// ITER times on random data staged in LDS, stamping s_memtime around each
+// phase.  The other 15 waves either exit (mode 0), poll an LDS word with
+// s_sleep 1 as mc2_wait does (mode 1), or run row-update work like the row
+// waves' apply (mode 2, waves 0-7) while 9-15 poll (the kernel's situation).
+// Variants of each phase are compared on the same inputs; S of every
+// iteration is checked against a host Gauss-Jordan.
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I kodr_amd/csrc tools/probe/chain_probe.hip -o tools/probe/chain_probe
+#include "../../kodr_amd/csrc/gf_elim.hip"
+
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+namespace kodr_amd {
+namespace {
+
+struct ProbeIn {  // one iteration's data (dwords)
+  uint32_t mb[16][8];  // block rows: panel p - 1 columns (0-3), panel p columns (4-7)
+  uint32_t sp[16][4];  // S_{p-1}
+  uint32_t rp[16][64]; // R_{p-1} (p = 1: its panel p columns are dwords 4-7)
+};
+
+template <int SMV, int GJV>
+__global__ __launch_bounds__(1024) void chain_probe(const uint32_t* tables, const ProbeIn* in, int iters, int mode,
+                                                    unsigned long long* stats, uint32_t* s_out) {
+  __shared__ ElimMc2Lds lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int i = tid; i < 256 * 2; i += 1024) {
+    const uint32_t* a = tables + 4 * i;
+    const uint32_t* b = tables + kElimInvTables + 4 * i;
+    lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
+    lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
+  }
+  if (tid == 0) lds.fail = 0;
+  if (tid == 0) lds.chain_cnt = 0;
+  __syncthreads();
+  if (w != 8) {
+    if (mode == 0) return;
+    if (mode == 2 && w < 8) {
+      uint32_t R[4] = {(uint32_t)lane, (uint32_t)lane * 3u, (uint32_t)lane * 5u, (uint32_t)lane * 7u};
+      uint32_t g = 0x01020304u * (uint32_t)(w + 1);
+      while (__hip_atomic_load(&lds.chain_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+#pragma unroll
+        for (int cc = 0; cc < 16; cc++) {
+          const uint32_t x = lds.rp[cc % 3][cc][lane];
+          const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const uint32_t f = __builtin_amdgcn_readfirstlane((g >> (8 * i)) & 0xffu);
+            const uint4 t = lds.tab[2 * f];
+            const uint32_t t2 = lds.tab[2 * f + 1].x;
+            R[i] ^= mc_mul(t, t2, s0, s1, s2);
+          }
+          g = g * 1664525u + 1013904223u;
+        }
+      }
+      if (R[0] == 0x12345678u && R[1] == R[2]) lds.fail = 7;  // keep the work
+      return;
+    }
+    for (int spins = 0; spins < (1 << 22); spins++) {
+      if (__hip_atomic_load(&lds.chain_cnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return;
+  }
+  __builtin_amdgcn_s_setprio(3);
+  const int t = lane >> 2, d = lane & 3;
+  unsigned long long c_small = 0, c_gj = 0;
+  int fails = 0;
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), m0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; it++) {
+    const ProbeIn& x = in[it];
+    // stage: slot 1 = this block's mb, slot 0 = the previous panel's S / R
+    for (int i = lane; i < 16 * 8; i += 64) lds.mb[1][i >> 3][i & 7] = x.mb[i >> 3][i & 7];
+    lds.sp[0][lane >> 2][lane & 3] = x.sp[lane >> 2][lane & 3];
+    for (int r = 0; r < 16; r++) lds.rp[0][r][lane] = x.rp[r][lane];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const int p = 1, slot = 1, ps = 0;
+    uint32_t r0[16], r1[16], r2[16];  // SMV 2: R's selectors before S_{p-1} is there
+    if (SMV == 2 || SMV == 3) mc3_pre_r(lds.rp[ps], 4 * p, lane, r0, r1, r2);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long a0 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t blk = lds.mb[slot][t][4 + d];
+    if (SMV == 0) {  // as gf_elim_mc2_kernel (not split)
+      lds.ft[t][d] = mc2_small(lds.tab, 0u, lds.mb[slot][t], lds.sp[ps], d);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      uint32_t acc = blk;
+      for (int cq = 0; cq < 4; cq++) {
+        const uint32_t fw = lds.ft[t][cq];
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          const uint32_t m = (fw >> (8 * cc)) & 0xffu;
+          const uint4 tt = lds.tab[2 * m];
+          const uint32_t tt2 = lds.tab[2 * m + 1].x;
+          const uint32_t xv = lds.rp[ps][4 * cq + cc][4 * p + d];
+          acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+        }
+      }
+      blk = acc;
+    } else if (SMV == 1) {
+      blk = mc3_block_update(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], lds.rp[ps], 4 * p, lane);
+    } else if (SMV == 2) {
+      blk = mc3_block_update_pre(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], r0, r1, r2, lane);
+    } else if (SMV == 3) {
+      blk = mc3_block_update_b(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], r0, r1, r2, lane);
+    } else {
+      blk = mc3_block_update_c(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], lds.rp[ps], 4 * p, lane);
+    }
+    lds.pan[t][d] = blk;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long a1 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t sval = 0;
+    int srow = 0;
+    bool ok;
+    if (GJV == 0)
+      ok = mc2_panel_gj<false>(lds.tab, lds.itab, lds.pan, lds.sp[2], lane, &sval, &srow);
+    else if (GJV == 1)
+      ok = mc2_panel_gj<true>(lds.tab, lds.itab, lds.pan, lds.sp[2], lane, &sval, &srow);
+    else if (GJV == 2)
+      ok = mc3_panel_gj(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    else if (GJV == 3)
+      ok = mc3_gj_circ(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    if (GJV == 5) ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    uint32_t Pr[4], Sr[4];
+    if (GJV == 4) {  // (t, d) layout -> one row per lane, then the row-form inversion
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t v = bperm(blk, 4 * (lane & 15) + q);  // all lanes active: a disabled source reads 0
+        Pr[q] = lane < 16 ? v : 0u;
+      }
+      ok = mc3_gj_rows(lds.tab, lds.itab, Pr, lane, Sr, &srow);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long a2 = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    c_small += a1 - a0;
+    c_gj += a2 - a1;
+    if (!ok) fails++;
+    // S by rows into s_out: lane (t, d) holds S row srow, dword d
+    if (GJV == 4) {
+      if (lane < 16)
+        for (int q = 0; q < 4; q++) s_out[(size_t)it * 64 + srow * 4 + q] = ok ? Sr[q] : 0u;
+    } else {
+      s_out[(size_t)it * 64 + srow * 4 + d] = ok ? sval : 0u;
+    }
+    s_out[(size_t)iters * 64 + (size_t)it * 64 + lane] = blk;  // the block it inverted (host check)
+  }
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime(), m1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    __hip_atomic_store(&lds.chain_cnt, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    stats[0] = c_small;
+    stats[1] = c_gj;
+    stats[2] = r1 - r0;
+    stats[3] = m1 - m0;
+    stats[4] = (unsigned long long)fails;
+  }
+}
+
+}  // namespace
+}  // namespace kodr_amd
+
+using namespace kodr_amd;
+
+static unsigned gmul(unsigned a, unsigned b) {
+  unsigned r = 0;
+  while (b) {
+    if (b & 1) r ^= a;
+    a <<= 1;
+    if (a & 0x100) a ^= 0x11D;
+    b >>= 1;
+  }
+  return r;
+}
+static unsigned ginv(unsigned a) {
+  for (unsigned b = 1; b < 256; b++)
+    if (gmul(a, b) == 1) return b;
+  return 0;
+}
+static uint8_t byte_of(const uint32_t* row, int c) { return (uint8_t)(row[c >> 2] >> (8 * (c & 3))); }
+
+// block_p as of p - 1 on the host: blk ^ (M x S) x R[:, panel p]
+static void host_block(const ProbeIn& x, uint8_t out[16][16]) {
+  for (int t = 0; t < 16; t++) {
+    uint8_t F[16] = {};
+    for (int u = 0; u < 16; u++) {
+      unsigned a = 0;
+      for (int c = 0; c < 16; c++) a ^= gmul(byte_of(x.mb[t], c), byte_of(x.sp[c], u));
+      F[u] = (uint8_t)a;
+    }
+    for (int v = 0; v < 16; v++) {
+      unsigned a = byte_of(x.mb[t], 16 + v);
+      for (int c = 0; c < 16; c++) a ^= gmul(F[c], byte_of(x.rp[c], 16 + v));
+      out[t][v] = (uint8_t)a;
+    }
+  }
+}
+static bool host_inv(const uint8_t in[16][16], uint8_t S[16][16]) {
+  uint8_t A[16][32];
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 32; j++) A[i][j] = j < 16 ? in[i][j] : (j - 16 == i);
+  for (int c = 0; c < 16; c++) {
+    int p = -1;
+    for (int r = c; r < 16; r++)
+      if (A[r][c]) { p = r; break; }
+    if (p < 0) return false;
+    for (int j = 0; j < 32; j++) std::swap(A[p][j], A[c][j]);
+    const unsigned iv = ginv(A[c][c]);
+    for (int j = 0; j < 32; j++) A[c][j] = (uint8_t)gmul(A[c][j], iv);
+    for (int r = 0; r < 16; r++)
+      if (r != c && A[r][c]) {
+        const unsigned f = A[r][c];
+        for (int j = 0; j < 32; j++) A[r][j] ^= (uint8_t)gmul(f, A[c][j]);
+      }
+  }
+  for (int i = 0; i < 16; i++)
+    for (int j = 0; j < 16; j++) S[i][j] = A[i][16 + j];
+  return true;
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+template <int SMV, int GJV>
+static int run(const char* name, const uint32_t* dtab, const ProbeIn* din, const std::vector<ProbeIn>& hin, int iters,
+               int mode, unsigned long long* dstats, uint32_t* dS) {
+  hipLaunchKernelGGL((chain_probe<SMV, GJV>), dim3(1), dim3(1024), 0, 0, dtab, din, iters, mode, dstats, dS);
+  CK(hipDeviceSynchronize());
+  hipLaunchKernelGGL((chain_probe<SMV, GJV>), dim3(1), dim3(1024), 0, 0, dtab, din, iters, mode, dstats, dS);
+  CK(hipDeviceSynchronize());
+  unsigned long long st[5];
+  CK(hipMemcpy(st, dstats, sizeof st, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> S((size_t)iters * 128);
+  CK(hipMemcpy(S.data(), dS, S.size() * 4, hipMemcpyDeviceToHost));
+  int bad = 0, sing = 0;
+  for (int it = 0; it < iters; it++) {
+    uint8_t blk[16][16], Sh[16][16];
+    host_block(hin[it], blk);
+    bool blk_ok = true;
+    for (int t = 0; t < 16; t++)
+      for (int v = 0; v < 16; v++) blk_ok &= byte_of(&S[(size_t)iters * 64 + (size_t)it * 64 + 4 * t], v) == blk[t][v];
+    if (!blk_ok) { bad++; continue; }
+    if (!host_inv(blk, Sh)) { sing++; continue; }
+    for (int t = 0; t < 16; t++)
+      for (int v = 0; v < 16; v++)
+        if (byte_of(&S[(size_t)it * 64 + 4 * t], v) != Sh[t][v]) { bad++; t = 16; break; }
+  }
+  const double clk = (double)st[3] / ((double)st[2] / 100.0);  // MHz
+  printf("%-22s mode %d: small %7.0f cyc, gj %7.0f cyc per panel (%.2f + %.2f us at %.0f MHz), fails %llu, "
+         "singular %d, wrong %d\n",
+         name, mode, (double)st[0] / iters, (double)st[1] / iters, st[0] / (double)iters / clk,
+         st[1] / (double)iters / clk, clk, st[4], sing, bad);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 512;
+  std::vector<uint32_t> tabs(kElimInvTables + 256 * 8);
+  elim_tables(tabs.data());
+  std::vector<ProbeIn> hin(iters);
+  uint64_t s = 0x6b6f6472ull;
+  auto rnd = [&] { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (uint32_t)s; };
+  for (auto& x : hin) {
+    for (auto& r : x.mb) for (auto& v : r) v = rnd();
+    for (auto& r : x.sp) for (auto& v : r) v = rnd();
+    for (auto& r : x.rp) for (auto& v : r) v = rnd();
+  }
+  uint32_t* dtab;
+  ProbeIn* din;
+  unsigned long long* dstats;
+  uint32_t* dS;
+  CK(hipMalloc(&dtab, tabs.size() * 4));
+  CK(hipMalloc(&din, hin.size() * sizeof(ProbeIn)));
+  CK(hipMalloc(&dstats, 64));
+  CK(hipMalloc(&dS, (size_t)iters * 128 * 4));
+  CK(hipMemcpy(dtab, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(din, hin.data(), hin.size() * sizeof(ProbeIn), hipMemcpyHostToDevice));
+  for (int mode = 0; mode < 3; mode += 2) {
+    run<0, 0>("mc2 small / gj", dtab, din, hin, iters, mode, dstats, dS);
+    run<2, 3>("pre-R update / circ gj", dtab, din, hin, iters, mode, dstats, dS);
+    run<3, 5>("batched update / gj v5", dtab, din, hin, iters, mode, dstats, dS);
+    run<4, 5>("batched-c update / gj v5", dtab, din, hin, iters, mode, dstats, dS);
+  }
+  return 0;
+}
