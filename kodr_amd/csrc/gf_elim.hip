@@ -1025,6 +1025,19 @@ __global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args
   if (tid == 0) args.counts[g * P + q] = ok ? 1 : 0;
 }
 
+// one state row's bytes [0, k) from a row register (lane = dword): a dword
+// store where the row is 4-byte aligned and the dword lies below k (pinned
+// host memory takes whole coalesced writes), bytes otherwise
+__device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane, int k) {
+  if (((uintptr_t)row & 3) == 0 && 4 * lane + 3 < k) {
+    *reinterpret_cast<uint32_t*>(row + 4 * lane) = v;
+    return;
+  }
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+    if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(v >> (8 * b));
+}
+
 // ---- mc2: the same inversion, pipelined inside each workgroup -------------
 // Panels of 16 columns (NP = 2P); workgroup q owns panels 2q ("A rows", its
 // local rows 0-15) and 2q + 1 ("B rows", 16-31).  In-place block
@@ -1074,6 +1087,19 @@ __device__ __forceinline__ bool mc2_wait(ElimMc2Lds& lds, int* ctr, int target) 
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
+  }
+}
+// mc2_wait without s_sleep, for hand-offs between chain waves a few hundred
+// cycles apart
+__device__ __forceinline__ bool mc3_spin(ElimMc2Lds& lds, int* ctr, int target) {
+  for (int spins = 0;; spins++) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    if (spins > 64 * kMcSpinMax) {
+      __hip_atomic_store(&lds.fail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    if ((spins & 255) == 255 && __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+      return false;
   }
 }
 // this wave's LDS writes first, then one count
@@ -1641,6 +1667,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         if (lane < 16) lds.fw[w][i][u] = acc;
         __builtin_amdgcn_s_waitcnt(0xc07f);
       }
+      if (w == 0) MC2_STAMP(112 + pa);  // F of the rows known (pa <= 15: index <= 127)
       uint32_t acc[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
@@ -1648,6 +1675,30 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         uint32_t gw[4];  // dword cq of each row's G (wave-uniform)
 #pragma unroll
         for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
+        if (args.variant & 16) {
+          // the 16 (uniform) table reads and 4 data reads of these columns
+          // first, then the arithmetic: one LDS round trip per 4 columns
+          uint4 tt[4][4];
+          uint32_t t2[4][4], xs[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            xs[cc] = lds.rp[slot][4 * cq + cc][lane];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
+              tt[cc][i] = lds.tab[2 * f];
+              t2[cc][i] = lds.tab[2 * f + 1].x;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
+          }
+          continue;
+        }
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
           const uint32_t x = lds.rp[slot][4 * cq + cc][lane];
@@ -1668,6 +1719,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
 
     for (int p = 0; p < NP; p++) {
       if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1)) || !mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+      if (w == 0) MC2_STAMP(96 + p);
       if (p >= 1) apply(p - 1);
       if ((p >> 1) == q && (p & 1) == half) {  // my rows are panel p's: R_p out
         const int slot = p % kMc2Slots;
@@ -1708,16 +1760,13 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       for (int i = 0; i < 4; i++) {
         const int gr = 32 * q + 4 * w + i;
         if (gr >= k) continue;
-        uint8_t* row = out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k);
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-          if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(R[i] >> (8 * b));
+        mc_store_row(out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k), R[i], lane, k);
       }
     }
   } else {
     // ================= chain waves =================
     const int cw = w - 8;
-    if (cw == 0) __builtin_amdgcn_s_setprio(3);
+    if (cw == 0 || ((args.variant & 32) && cw < 4)) __builtin_amdgcn_s_setprio(3);
     int unpublished = 2 * q;  // the first owned panel whose S_p is not out yet
     int nsync = 0;            // chain_sync rounds so far (split variant)
     for (int p = 0; p < NP; p++) {
@@ -1731,6 +1780,56 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
         if (cw == 0) MC2_STAMP(4 * p + 1);
         const bool split = (args.variant & 1) && p >= 1;
+        const bool split4 = (args.variant & 32) && p >= 1;
+        if (split4 && cw < 4) {
+          // the block update over chain waves 0-3 (on four SIMDs), four
+          // terms of each product per wave, partials folded through LDS
+          // behind tight-spin counters (no s_sleep): F's four partials go to
+          // every wave, the second product's to wave 0
+          const int t = lane >> 2, d = lane & 3, ps = (p - 1) % kMc2Slots;
+          uint32_t m[4];
+          const uint32_t mw4 = lds.mb[slot][t][cw];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) m[cc] = (mw4 >> (8 * cc)) & 0xffu;
+          uint32_t acc = 0;
+          {
+            uint4 tt[4];
+            uint32_t t2[4], xv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) {
+              tt[cc] = lds.tab[2 * m[cc]];
+              t2[cc] = lds.tab[2 * m[cc] + 1].x;
+              xv[cc] = lds.sp[ps][4 * cw + cc][d];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) acc ^= gmul4(tt[cc], t2[cc], sel0(xv[cc]), sel1(xv[cc]), sel2(xv[cc]));
+          }
+          lds.part[cw][t][d] = acc;
+          mc2_signal(&lds.chain_sync, lane);
+          nsync += 2;
+          if (!mc3_spin(lds, &lds.chain_sync, 4 * (nsync - 1))) break;
+          const uint32_t F = lds.part[0][t][d] ^ lds.part[1][t][d] ^ lds.part[2][t][d] ^ lds.part[3][t][d];
+          const uint32_t fw = quad_bcast(F, cw);  // F[t][4 cw .. 4 cw + 3]
+          uint32_t acc2 = 0;
+          {
+            uint4 tt[4];
+            uint32_t t2[4], xv[4];
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) {
+              const uint32_t f = (fw >> (8 * cc)) & 0xffu;
+              tt[cc] = lds.tab[2 * f];
+              t2[cc] = lds.tab[2 * f + 1].x;
+              xv[cc] = lds.rp[ps][4 * cw + cc][4 * p + d];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int cc = 0; cc < 4; cc++) acc2 ^= gmul4(tt[cc], t2[cc], sel0(xv[cc]), sel1(xv[cc]), sel2(xv[cc]));
+          }
+          lds.part[4 + cw][t][d] = acc2;
+          mc2_signal(&lds.chain_sync, lane);
+          if (cw == 0 && !mc3_spin(lds, &lds.chain_sync, 4 * nsync)) break;
+        }
         if (split) {
           // the block's two small products with their 16 terms split over the
           // 8 chain waves (2 each), partials folded through LDS
@@ -1770,7 +1869,9 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         if (cw == 0) {
           const int t = lane >> 2, d = lane & 3;
           uint32_t blk = lds.mb[slot][t][4 + d];
-          if (split) {
+          if (split4) {
+            blk ^= lds.part[4][t][d] ^ lds.part[5][t][d] ^ lds.part[6][t][d] ^ lds.part[7][t][d];
+          } else if (split) {
 #pragma unroll
             for (int j = 0; j < 8; j++) blk ^= lds.part[j][t][d];
           } else if (p >= 1 && (args.variant & 8)) {  // batched operand reads
@@ -1891,6 +1992,427 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   }
 }
 
+// ---- mc4: a chain workgroup beside one row workgroup per 16-row panel ------
+// The same block Gauss-Jordan in L form as gf_elim_mc2_kernel, with the two
+// roles on different CUs, so that the critical path -- bring panel p's 16 x
+// 16 block up to date with panel p - 1, invert it -- never leaves one
+// workgroup and never shares a SIMD with the row updates:
+//  * row workgroup r (blockIdx.x = r < NP) holds rows 16 r .. 16 r + 15
+//    (4 waves x 4 rows, lane = dword) and applies every panel j in order
+//    from S_j (the chain's) and R_j (panel j's rows as of j - 1, from row
+//    workgroup j; its own when r = j); after apply(j) it publishes R_r when
+//    r = j + 1 and MB_r = its rows' columns of panels r - 1 and r when
+//    r = j + 2 (both "as of r - 1 / r - 2", what the chain and the other
+//    row workgroups need next);
+//  * the chain workgroup (blockIdx.x = NP): wave 1 stages MB_p and R_{p-1}'s
+//    panel-p columns (both as of p - 2) into LDS as they appear; wave 0 updates
+//    the block with S_{p-1} (two 16-term products, mc4_block_update), inverts
+//    it (mc3_gj_v5) and publishes S_p.
+// The row data the chain needs for panel p leaves the row workgroups one
+// panel earlier (after apply(p - 2)), so the chain waits on them only when a
+// row workgroup's hand-off and apply take longer than one chain step.
+// Hand-offs are 8-byte {data, epoch} granules (agent-scope relaxed stores,
+// polled with agent-scope loads), as in mc / mc2; a singular block publishes
+// FAIL on every later S_p, and a workgroup that sees FAIL publishes FAIL on
+// its own slots and stops, so every workgroup ends; spins are bounded.
+// Results are direct only: T rows into out (pinned host memory) and one
+// status word per workgroup, counts[g * (NP + 1) + x].
+constexpr int kMc4Threads = 256;
+constexpr int kMc4SGran = 64, kMc4RGran = 16 * 64, kMc4MGran = 16 * 8;
+
+struct ElimMc4Lds {
+  uint4 tab[256 * 2];
+  uint4 itab[256 * 2];      // chain only
+  uint32_t rp[16][64];      // row workgroup: R_j
+  uint32_t sp[16][4];       // row workgroup: S_j
+  uint32_t mw[4][4][4];     // row wave w: its rows' panel-j columns (multipliers)
+  uint32_t fw[4][4][4];     // row wave w: F of its rows
+  uint32_t cmb[2][16][8];   // chain: MB_p by slot p % 2 (M: dwords 0-3, X: 4-7)
+  uint32_t crq[2][16][4];   // chain: R_{p-1}'s panel-p columns
+  uint4 csel[2][16][4];     // chain: selectors (sel0, sel1, sel2) of S_p's dwords, slot p % 2
+  uint4 crsel[2][16][4];    // chain: selectors of the staged R_{p-1} columns
+  int staged, consumed, fail;
+};
+
+__device__ __forceinline__ size_t mc4_pub_words(int NP) {
+  return (size_t)NP * (kMc4SGran + kMc4RGran + kMc4MGran);
+}
+
+// polls N granules per lane (at src[i * stride]) until every tag is this
+// launch's epoch: 0 (values in v), 1 a FAIL tag (or the workgroup's fail
+// word) seen, 2 timeout
+template <int N>
+__device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t epoch, uint32_t* v, const int* lfail) {
+  for (int spins = 0;; spins++) {
+    bool okv = true, anyf = false;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      const uint64_t x = __hip_atomic_load(src + (size_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t tg = (uint32_t)(x >> 32);
+      okv = okv && tg == epoch;
+      anyf = anyf || tg == (epoch | kMcFail);
+      v[i] = (uint32_t)x;
+    }
+    if (__builtin_amdgcn_ballot_w64(anyf)) return 1;
+    if (__builtin_amdgcn_ballot_w64(!okv) == 0) return 0;
+    if (lfail && __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 1;
+    if (spins > kMcSpinMax) return 2;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void mc4_put(gu64* dst, uint32_t epoch, uint32_t v) {
+  __hip_atomic_store(dst, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mc4_put_fail(gu64* dst, uint32_t epoch) {
+  __hip_atomic_store(dst, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// waits for an LDS counter of the mc4 chain workgroup (bounded; false on a
+// fail word or a timeout)
+__device__ __forceinline__ bool mc4_wait(int* ctr, int target, int* lfail) {
+  for (int spins = 0;; spins++) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    if (__hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (spins > 64 * kMcSpinMax) {
+      __hip_atomic_store(lfail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+  }
+}
+
+// acc ^ sum over 8 terms of (tables of m[c]) x data whose selectors are
+// precomputed (sp[c * ss] = {sel0, sel1, sel2, -}): three LDS reads and five
+// VALU per term
+__device__ __forceinline__ uint32_t mc4_dot8s(const uint4* tab, uint32_t acc, const uint32_t* m, const uint4* sp,
+                                              int ss) {
+  uint4 tt[8], sv[8];
+  uint32_t t2[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    tt[c] = tab[2 * m[c]];
+    t2[c] = tab[2 * m[c] + 1].x;
+    sv[c] = sp[c * ss];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < 8; c++) acc ^= gmul4(tt[c], t2[c], sv[c].x, sv[c].y, sv[c].z);
+  return acc;
+}
+__device__ __forceinline__ uint4 mc4_sel(uint32_t v) { return make_uint4(sel0(v), sel1(v), sel2(v), 0u); }
+
+// the chain's block update from precomputed selectors of S_{p-1} (ssel) and
+// of R_{p-1}'s panel-p columns (rsel), both [16][4]
+__device__ __forceinline__ uint32_t mc4_block_update_s(const uint4* tab, uint32_t blk, const uint32_t* mrow,
+                                                       const uint4 (*ssel)[4], const uint4 (*rsel)[4], int lane) {
+  const int d = lane & 3;
+  uint32_t mw[4], m[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
+#pragma unroll
+  for (int c = 0; c < 16; c++) m[c] = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+  uint32_t F = mc4_dot8s(tab, 0u, m, &ssel[0][d], 4);
+  F = mc4_dot8s(tab, F, m + 8, &ssel[8][d], 4);
+  uint32_t fw[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
+#pragma unroll
+  for (int c = 0; c < 16; c++) m[c] = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+  const uint32_t acc = mc4_dot8s(tab, blk, m, &rsel[0][d], 4);
+  return mc4_dot8s(tab, acc, m + 8, &rsel[8][d], 4);
+}
+
+// RPW rows per row wave (4 waves per workgroup): 16 or 8 rows per row
+// workgroup; gridDim.x = NP * 16 / (4 RPW) row workgroups + the chain
+template <int RPW>
+__global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args) {
+  __shared__ ElimMc4Lds lds;
+  constexpr int RW = 4 * RPW;
+  const int x = blockIdx.x, g = blockIdx.y, NRW = gridDim.x - 1, NP = NRW * RW / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = args.k;
+  const uint32_t epoch = args.epoch;
+  gu64* const base = (gu64*)args.pub + (size_t)g * mc4_pub_words(NP);
+  gu64* const pubS = base;
+  gu64* const pubR = base + (size_t)NP * kMc4SGran;
+  gu64* const pubM = pubR + (size_t)NP * kMc4RGran;
+  const bool chain = x == NRW;
+#ifdef KODR_ELIM_TIMING
+  // tuning build: s_memrealtime stamps by lane 0 into workgroup x's 1 KiB of
+  // the T region (no result): chain [p] staged, [16 + p] block updated,
+  // [32 + p] S_p out, staging wave [48 + p]; row workgroup [j] R_j / S_j in
+  // LDS, [16 + j] apply(j) done; [96] entry, [97] tables in LDS
+  gu64* const tsout = (gu64*)(args.out + (size_t)g * args.out_gen_stride + (size_t)x * 1024);
+#define MC4_STAMP(i)                                                                                          \
+  do {                                                                                                        \
+    if (lane == 0)                                                                                            \
+      __hip_atomic_store(tsout + (i), (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,  \
+                         __HIP_MEMORY_SCOPE_SYSTEM);                                                          \
+  } while (0)
+#else
+#define MC4_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+  if (w == 0) MC4_STAMP(96);
+  for (int i = tid; i < 256 * 2; i += kMc4Threads) {
+    const uint32_t* a = args.tables + 4 * i;
+    lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
+    if (chain) {
+      const uint32_t* b = args.tables + kElimInvTables + 4 * i;
+      lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
+    }
+  }
+  if (tid == 0) {
+    lds.staged = 0;
+    lds.consumed = 0;
+    lds.fail = 0;
+  }
+  __syncthreads();
+  if (w == 0) MC4_STAMP(97);
+
+  if (chain) {
+    const int t = lane >> 2, d = lane & 3;
+    if (w == 1) {
+      // ---- staging wave: MB_p and R_{p-1}'s panel-p columns into LDS ----
+      for (int p = 0; p < NP; p++) {
+        const int slot = p & 1;
+        if (p >= 2 && !mc4_wait(&lds.consumed, p - 1, &lds.fail)) break;  // the slot's last readers are done
+        uint32_t v[2];
+        int st = 0;
+        // dword dw of original row gr (rows past k: identity padding)
+        auto orig = [&](int gr, int dw) -> uint32_t {
+          if (gr >= k) return gr >> 2 == dw ? 1u << (8 * (gr & 3)) : 0u;
+          const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
+          uint32_t o = 0;
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (4 * dw + b < k) o |= (uint32_t)src[4 * dw + b] << (8 * b);
+          return o;
+        };
+        if (p == 0) {  // panels 0 and 1 start from the input rows ("as of -1"): no hand-off
+          lds.cmb[slot][t][4 + d] = orig(t, d);
+        } else if (p == 1) {
+          lds.cmb[slot][t][d] = orig(16 + t, d);
+          lds.cmb[slot][t][4 + d] = orig(16 + t, 4 + d);
+          const uint32_t rq = orig(t, 4 + d);
+          lds.crq[slot][t][d] = rq;
+          lds.crsel[slot][t][d] = mc4_sel(rq);
+        } else {
+          const gu64* mb = pubM + (size_t)p * kMc4MGran + t * 8 + d;
+          st = mc4_poll<2>(mb, 4, epoch, v, &lds.fail);
+          if (st == 0) {
+            lds.cmb[slot][t][d] = v[0];
+            lds.cmb[slot][t][4 + d] = v[1];
+            st = mc4_poll<1>(pubR + (size_t)(p - 1) * kMc4RGran + t * 64 + 4 * p + d, 0, epoch, v, &lds.fail);
+            if (st == 0) {
+              lds.crq[slot][t][d] = v[0];
+              lds.crsel[slot][t][d] = mc4_sel(v[0]);
+            }
+          }
+        }
+        if (st) {
+          __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&lds.staged, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        MC4_STAMP(48 + p);
+      }
+      return;
+    }
+    // ---- wave 0: update the block, invert it, publish S_p ----
+    if (w != 0) return;
+    __builtin_amdgcn_s_setprio(3);
+    int p = 0;
+    for (; p < NP; p++) {
+      const int slot = p & 1;
+      if (!mc4_wait(&lds.staged, p + 1, &lds.fail)) break;
+      MC4_STAMP(p);
+      uint32_t blk = lds.cmb[slot][t][4 + d];
+      if (p >= 1)
+        blk = mc4_block_update_s(lds.tab, blk, lds.cmb[slot][t], lds.csel[slot ^ 1], lds.crsel[slot], lane);
+      MC4_STAMP(16 + p);
+      uint32_t sval = 0;
+      int srow = 0;
+      if (!mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow)) {
+        __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      mc4_put(pubS + (size_t)p * kMc4SGran + 4 * srow + d, epoch, sval);
+      lds.csel[slot][srow][d] = mc4_sel(sval);
+      MC4_STAMP(32 + p);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&lds.consumed, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+#ifdef KODR_ELIM_TIMING
+    const bool ok = false;
+#else
+    const bool ok = p == NP;
+#endif
+    for (int q = p; q < NP; q++) mc4_put_fail(pubS + (size_t)q * kMc4SGran + lane, epoch);  // every later S_p
+    if (lane == 0) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);
+      __hip_atomic_store(&args.counts[g * (NRW + 1) + NRW], (int)(ok ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    return;
+  }
+
+  // ================= row workgroup x: rows RW x + RPW w + i =================
+  const int row0 = RW * x, pr = row0 / 16, lo = row0 - 16 * pr;  // its panel, offset in it
+  uint32_t R[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; i++) {
+    const int gr = row0 + RPW * w + i;
+    uint32_t v = 0;
+    if (gr < k) {
+      const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
+    } else if (gr >> 2 == lane) {
+      v = 1u << (8 * (gr & 3));  // padding rows: identity (the matrix stays [[C, 0], [0, I]])
+    }
+    R[i] = v;
+  }
+  // what the workgroup owes after apply(j) (j = -1: the loaded rows)
+  auto publish = [&](int j) {
+    const int lr = lo + RPW * w;  // local row (in the panel) of R[0]
+    if (pr == j + 1) {  // R_pr: the panel's rows as of pr - 1
+      gu64* dst = pubR + (size_t)pr * kMc4RGran + lr * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < RPW; i++) mc4_put(dst + i * 64, epoch, R[i]);
+    }
+    if (pr == j + 2) {  // MB_pr: columns of panels pr - 1 and pr as of pr - 2
+      const int u = lane - 4 * (pr - 1);
+      if (u >= 0 && u < 8) {
+        gu64* dst = pubM + (size_t)pr * kMc4MGran + lr * 8 + u;
+#pragma unroll
+        for (int i = 0; i < RPW; i++) mc4_put(dst + i * 8, epoch, R[i]);
+      }
+    }
+  };
+  publish(-1);
+  int j = 0;
+  for (; j < NP; j++) {
+    // R_j (all 16 rows, from the hand-off slots, this workgroup's own
+    // included) and S_j into LDS: wave w polls rows 4 w .. 4 w + 3, wave 0 S_j
+    {
+      uint32_t v[4];
+      const int st = mc4_poll<4>(pubR + (size_t)j * kMc4RGran + (4 * w) * 64 + lane, 64, epoch, v, &lds.fail);
+      if (st) {
+        __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds.rp[4 * w + i][lane] = v[i];
+      }
+    }
+    if (w == 0) {
+      uint32_t v[1];
+      const int st = mc4_poll<1>(pubS + (size_t)j * kMc4SGran + lane, 0, epoch, v, &lds.fail);
+      if (st)
+        __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      else
+        lds.sp[lane >> 2][lane & 3] = v[0];
+    }
+    __syncthreads();
+    if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+    if (w == 0) MC4_STAMP(j);
+    // apply(j): the panel's own rows become S_j x R_j with S_j in the panel
+    // columns; the others take F = (panel-j bytes) x S_j, row ^= F x R_j,
+    // panel columns := F
+    const int db = 4 * j;
+    const bool own = pr == j;
+    const uint32_t(*Gp)[4] = own ? &lds.sp[lo + RPW * w] : lds.fw[w];
+    if (!own) {
+      // F of the RPW rows: lane (cg, i, u) sums terms c in group cg (16 / G
+      // of them), the G groups folded by ds_bpermute
+      constexpr int G = 16 / RPW, TPG = 16 / G;  // groups, terms per group
+      if (lane >= db && lane < db + 4)
+#pragma unroll
+        for (int i = 0; i < RPW; i++) lds.mw[w][i][lane - db] = R[i];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      const int u = lane & 3, i = (lane >> 2) % RPW, cg = (lane >> 2) / RPW;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int cc = 0; cc < TPG; cc++) {
+        const int c = TPG * cg + cc;
+        const uint32_t m = (lds.mw[w][i][c >> 2] >> (8 * (c & 3))) & 0xffu;
+        const uint4 tt = lds.tab[2 * m];
+        const uint32_t tt2 = lds.tab[2 * m + 1].x;
+        const uint32_t xv = lds.sp[c][u];
+        acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+      }
+#pragma unroll
+      for (int sft = 4 * RPW; sft < 64; sft <<= 1) acc ^= bperm(acc, lane ^ sft);
+      if (lane < 4 * RPW) lds.fw[w][i][u] = acc;
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+    }
+    uint32_t acc[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; i++) acc[i] = own ? 0u : R[i];
+#pragma unroll
+    for (int cq = 0; cq < 4; cq++) {
+      uint32_t gw[RPW];
+#pragma unroll
+      for (int i = 0; i < RPW; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
+      uint4 tt[4][RPW];
+      uint32_t t2[4][RPW], xs[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) {
+        xs[cc] = lds.rp[4 * cq + cc][lane];
+#pragma unroll
+        for (int i = 0; i < RPW; i++) {
+          const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
+          tt[cc][i] = lds.tab[2 * f];
+          t2[cc][i] = lds.tab[2 * f + 1].x;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int cc = 0; cc < 4; cc++) {
+        const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+#pragma unroll
+        for (int i = 0; i < RPW; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
+      }
+    }
+    const int u = lane - db;
+#pragma unroll
+    for (int i = 0; i < RPW; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
+    publish(j);
+    if (w == 0) MC4_STAMP(16 + j);
+    __syncthreads();  // rp / sp / mw / fw are rewritten next iteration
+  }
+#ifdef KODR_ELIM_TIMING
+  j = -1;  // the stamps overwrote T: report failure, kodr's route on the host
+#endif
+  const bool ok = j == NP;
+  if (!ok) {  // every slot this workgroup still owes (or has put) gets FAIL, so its consumers stop
+    const int lr = lo + RPW * w;
+    for (int i = 0; i < RPW; i++) mc4_put_fail(pubR + (size_t)pr * kMc4RGran + (lr + i) * 64 + lane, epoch);
+    if (pr >= 1 && lane < 8)
+      for (int i = 0; i < RPW; i++) mc4_put_fail(pubM + (size_t)pr * kMc4MGran + (lr + i) * 8 + lane, epoch);
+  } else {
+    uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+#pragma unroll
+    for (int i = 0; i < RPW; i++) {
+      const int gr = row0 + RPW * w + i;
+      if (gr >= k) continue;
+      mc_store_row(out + (size_t)gr * args.out_pitch, R[i], lane, k);
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
+  __syncthreads();
+  if (tid == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    __hip_atomic_store(&args.counts[g * (NRW + 1) + x], (int)(ok ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#undef MC4_STAMP
+}
+
 }  // namespace
 
 void elim_tables(uint32_t* host_out) {
@@ -1944,8 +2466,9 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   return full;
 }
 
-// KODR_ELIM_MC: 2 (default) the pipelined kernel, 1 the first multi-workgroup
-// kernel, 0 one workgroup per decoder (A/B knob)
+// KODR_ELIM_MC: 2 (default) the pipelined kernel, 4 the chain workgroup
+// beside per-panel row workgroups, 1 the first multi-workgroup kernel, 0 one
+// workgroup per decoder (A/B knob)
 static int elim_mc_mode() {
   static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 2;
   return mc;
@@ -1958,9 +2481,23 @@ bool gf_elim_mc_taken(const ElimArgs& args, int G) {
 
 bool gf_elim_mc_enabled() { return elim_mc_mode() != 0; }
 
-bool gf_elim_mc_direct(const ElimArgs& args, int G) { return gf_elim_mc_taken(args, G) && elim_mc_mode() == 2; }
+bool gf_elim_mc_direct(const ElimArgs& args, int G) {
+  return gf_elim_mc_taken(args, G) && (elim_mc_mode() == 2 || elim_mc_mode() == 4);
+}
+
+// mc4 rows per row wave (KODR_MC4_RPW: 4 = 16 rows per row workgroup, 2
+// (default) = 8)
+static int mc4_rows_per_wave() {
+  static const int rpw = getenv("KODR_MC4_RPW") && atoi(getenv("KODR_MC4_RPW")) == 4 ? 4 : 2;
+  return rpw;
+}
+
+int gf_elim_mc_groups(int k) {
+  return elim_mc_mode() == 4 ? (k + 15) / 16 * (16 / (4 * mc4_rows_per_wave())) + 1 : (k + 31) / 32;
+}
 
 size_t gf_elim_mc_pub_bytes(int k, int G) {
+  if (elim_mc_mode() == 4) return (size_t)G * (size_t)((k + 15) / 16) * (kMc4SGran + kMc4RGran + kMc4MGran) * 8;
   const size_t P = (size_t)gf_elim_mc_groups(k);
   return (size_t)G * std::max<size_t>(P * 32 * 64, 2 * P * kMc2PanelGran) * 8;
 }
@@ -1968,7 +2505,15 @@ size_t gf_elim_mc_pub_bytes(int k, int G) {
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
   if (G <= kElimMaxGens && args.k >= 2 && args.k <= 256 && gf_elim_mc_taken(args, G)) {
-    if (elim_mc_mode() == 1)
+    if (elim_mc_mode() == 4) {
+      if (!args.direct) return hipErrorInvalidValue;  // mc4 reports directly only
+      if (mc4_rows_per_wave() == 4)
+        hipLaunchKernelGGL(gf_elim_mc4_kernel<4>, dim3(gf_elim_mc_groups(args.k), G), dim3(kMc4Threads), 0, stream,
+                           args);
+      else
+        hipLaunchKernelGGL(gf_elim_mc4_kernel<2>, dim3(gf_elim_mc_groups(args.k), G), dim3(kMc4Threads), 0, stream,
+                           args);
+    } else if (elim_mc_mode() == 1)
       hipLaunchKernelGGL(gf_elim_mc_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(64 * kMcWaves), 0, stream, args);
     else
       hipLaunchKernelGGL(gf_elim_mc2_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(1024), 0, stream, args);

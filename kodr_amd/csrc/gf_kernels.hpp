@@ -131,7 +131,9 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 // counts[g * groups + q] = 1 (done) or 0 (a singular block or a timeout: the
 // host then takes kodr's route); the decoder's T is valid when all are 1.
 constexpr int kElimMcMaxBlocks = 256;
-inline int gf_elim_mc_groups(int k) { return (k + 31) / 32; }
+// workgroups per decoder: ceil(k / 32) (gf_elim_mc / mc2), or one per 16-row
+// panel plus the chain workgroup (mc4, KODR_ELIM_MC=4)
+int gf_elim_mc_groups(int k);
 size_t gf_elim_mc_pub_bytes(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 // true when gf_elim_mc_taken and the launch honours args.direct (mc2)

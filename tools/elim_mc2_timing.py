@@ -56,7 +56,8 @@ for g in sorted({0, G - 1}):
             own = "own" if p >> 1 == q else "   "
             c = st[q, 4 * p:4 * p + 4]
             print(f"    panel {p:2d} {own}: start {rel(c[0]):7.2f} ready {rel(c[1]):7.2f} mid {rel(c[2]):7.2f} "
-                  f"end {rel(c[3]):7.2f} | rows iter done {rel(st[q, 64 + p]):7.2f}")
+                  f"end {rel(c[3]):7.2f} | rows wake {rel(st[q, 96 + p]):7.2f} F {rel(st[q, 112 + p - 1]) if p else 0.0:7.2f} "
+                  f"iter done {rel(st[q, 64 + p]):7.2f}")
     # the critical path: each panel's S out (owner's end) after the previous
     ends = [rel(st[p >> 1, 4 * p + 3]) for p in range(NP)]
     print("  S_p out:", " ".join(f"{e:6.2f}" for e in ends))
