@@ -1532,9 +1532,8 @@ __device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, u
                                           int* s_row) {
   const int t = lane >> 2, d = lane & 3;
   uint64_t cand = 0x1111111111111111ull;
+  uint64_t pinv = 0;  // nibble tp = the slot (column) row tp pivoted: SALU only
   bool fail = false;
-  uint32_t selA = 0, selB = 0, mskA = 0;
-  int mycol = 0;
 #pragma unroll
   for (int c = 0; c < 16; c++) {
     const int cd = c >> 2, cb = 8 * (c & 3);
@@ -1546,6 +1545,7 @@ __device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, u
     const int pl = (int)__builtin_ctzll(m | (1ull << 60));  // a failed column picks lane 60 (result unused)
     const int tp = pl >> 2;
     cand &= ~(1ull << pl);
+    pinv |= (uint64_t)c << (4 * tp);
     const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
     const uint4 ti = itab[2 * dp];
     const uint32_t ti2 = itab[2 * dp + 1].x;
@@ -1553,21 +1553,22 @@ __device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, u
     const uint32_t inv = (ti.x >> 8) & 0xffu;
     const uint32_t Q = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp)) ^ (d == cd ? inv << cb : 0u);
     const uint32_t upd = P ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
-    const bool piv = t == tp;
-    P = piv ? (d == cd ? Q ^ (1u << cb) : Q) : upd;
-    mycol = piv ? c : mycol;
-    const int ob = 8 * (tp & 3);
-    const bool mine = d == (tp >> 2);  // output byte tp (of every S row) comes from slot c
-    if (c < 8) {
-      selA |= mine ? (uint32_t)c << ob : 0u;
-      mskA |= mine ? 0xffu << ob : 0u;
-    } else {
-      selB |= mine ? (uint32_t)(c - 8) << ob : 0u;
-    }
+    P = t == tp ? Q ^ (d == cd ? 1u << cb : 0u) : upd;
+  }
+  // S row c = the slots of row pi(c) with output byte j from slot pi^-1(j) =
+  // nibble j of pinv; row t pivoted column nibble t
+  uint32_t selA = 0, selB = 0, mskA = 0;
+  const uint32_t pq = (uint32_t)(pinv >> (16 * d));  // nibbles 4d .. 4d + 3: this lane's output bytes
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t sl = (pq >> (4 * b)) & 15u;
+    selA |= (sl & 7u) << (8 * b);
+    selB |= (sl & 7u) << (8 * b);
+    mskA |= sl < 8 ? 0xffu << (8 * b) : 0u;
   }
   const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
   *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
-  *s_row = mycol;
+  *s_row = (int)((pinv >> (4 * t)) & 15u);
   return !fail;
 }
 
