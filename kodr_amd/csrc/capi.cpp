@@ -1358,12 +1358,13 @@ template <class F>
 int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read);
 }
 
-// One decoder's elimination goes to the GPU (gf_elim_mc2, many workgroups)
-// instead of the host when its n new rows complete the rank of a state of
-// kept rows (fresh or continued: the full-batch case) and k is at least
-// KODR_ROUTE_MIN_K (default kRouteMinK: the route is off by default while the
-// single-decoder GPU elimination measures slower than the host).
-constexpr size_t kRouteMinK = 257;
+// One decoder's elimination goes to the GPU (gf_elim_mc4: a chain workgroup
+// beside row workgroups) instead of the host when its n new rows complete the
+// rank of a state of kept rows (fresh or continued: the full-batch case) and
+// k is at least KODR_ROUTE_MIN_K (default kRouteMinK, from where the GPU
+// route measured at least as fast as the host's: 87 against 86 us at k = 224,
+// 92-96 against 104-107 us at k = 256, profiles/r04/elim_modes/).
+constexpr size_t kRouteMinK = 224;
 bool dec_route_gpu(const rlnc_decoder* d, size_t n) {
   const char* e = getenv("KODR_ROUTE_MIN_K");  // read per call: tests switch it to keep host references
   const size_t min_k = e ? (size_t)atol(e) : kRouteMinK;
@@ -1816,7 +1817,9 @@ int ctx_elim_tables(rlnc_ctx* ctx) {
 // launch's epoch (a new tag per launch; the buffer is zeroed when it is
 // allocated and when the tags wrap)
 int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
-  static const int variant = getenv("KODR_MC2_VARIANT") ? atoi(getenv("KODR_MC2_VARIANT")) : 0;
+  // mc2 tuning bits (gf_kernels.hpp); default 28: the circular block inversion,
+  // batched block update and batched row updates
+  static const int variant = getenv("KODR_MC2_VARIANT") ? atoi(getenv("KODR_MC2_VARIANT")) : 28;
   a->variant = variant;
   const size_t bytes = kodr_amd::gf_elim_mc_pub_bytes((int)k, (int)nc);
   ctx->elim_pub.bind(ctx->device, ctx->stream);
@@ -1836,7 +1839,7 @@ int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
 // launch's workgroups resident at once
 size_t elim_chunk(size_t k, size_t n) {
   size_t c = std::min<size_t>(n, kodr_amd::kElimMaxGens);
-  if (k >= 2 && k <= 256) c = std::min<size_t>(c, kodr_amd::kElimMcMaxBlocks / kodr_amd::gf_elim_mc_groups((int)k));
+  if (k >= 2 && k <= 256) c = std::min<size_t>(c, (size_t)kodr_amd::gf_elim_mc_max_gens((int)k));
   return std::max<size_t>(c, 1);
 }
 
@@ -1845,7 +1848,7 @@ size_t elim_chunk(size_t k, size_t n) {
 // kernel reports done, else 0)
 void elim_counts(const kodr_amd::ElimArgs& a, size_t nc, bool mc, const uint8_t* hdr, int* cnt) {
   const int* c = reinterpret_cast<const int*>(hdr);
-  const int P = kodr_amd::gf_elim_mc_groups(a.k);
+  const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   for (size_t i = 0; i < nc; i++) {
     if (!mc) {
       cnt[i] = c[i];
@@ -1879,7 +1882,7 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // every workgroup of decoder i is done, else 0 (kodr's route on the host).
 // A launch that never reports within 2 s is waited for on the stream once.
 int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt) {
-  const int P = kodr_amd::gf_elim_mc_groups(a.k);
+  const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
   const size_t nw = nc * (size_t)P;
   const auto t0 = std::chrono::steady_clock::now();

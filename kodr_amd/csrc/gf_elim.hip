@@ -2467,23 +2467,13 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   return full;
 }
 
-// KODR_ELIM_MC: 2 (default) the pipelined kernel, 4 the chain workgroup
-// beside per-panel row workgroups, 1 the first multi-workgroup kernel, 0 one
-// workgroup per decoder (A/B knob)
+// KODR_ELIM_MC: 0 one workgroup per decoder, 1 the first multi-workgroup
+// kernel, 2 mc2, 4 mc4, 3 (default) mc4 when the launch's decoders fit it
+// (G * groups <= kElimMcMaxBlocks: one decoder at k = 256 takes 33
+// workgroups) else mc2 (measured: profiles/r04/elim_modes/)
 static int elim_mc_mode() {
-  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 2;
+  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 3;
   return mc;
-}
-
-bool gf_elim_mc_taken(const ElimArgs& args, int G) {
-  return elim_mc_mode() && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
-         G * gf_elim_mc_groups(args.k) <= kElimMcMaxBlocks;
-}
-
-bool gf_elim_mc_enabled() { return elim_mc_mode() != 0; }
-
-bool gf_elim_mc_direct(const ElimArgs& args, int G) {
-  return gf_elim_mc_taken(args, G) && (elim_mc_mode() == 2 || elim_mc_mode() == 4);
 }
 
 // mc4 rows per row wave (KODR_MC4_RPW: 4 = 16 rows per row workgroup, 2
@@ -2492,32 +2482,54 @@ static int mc4_rows_per_wave() {
   static const int rpw = getenv("KODR_MC4_RPW") && atoi(getenv("KODR_MC4_RPW")) == 4 ? 4 : 2;
   return rpw;
 }
+static int mc4_groups(int k) { return (k + 15) / 16 * (16 / (4 * mc4_rows_per_wave())) + 1; }
+static int mc2_groups(int k) { return (k + 31) / 32; }
 
-int gf_elim_mc_groups(int k) {
-  return elim_mc_mode() == 4 ? (k + 15) / 16 * (16 / (4 * mc4_rows_per_wave())) + 1 : (k + 31) / 32;
+// the multi-workgroup kernel a launch of G decoders takes (0: none)
+static int mc_kernel_for(int k, int G) {
+  const int m = elim_mc_mode();
+  if (m == 3) return G * mc4_groups(k) <= kElimMcMaxBlocks ? 4 : 2;
+  return m;
+}
+
+int gf_elim_mc_groups(int k, int G) { return mc_kernel_for(k, G) == 4 ? mc4_groups(k) : mc2_groups(k); }
+
+int gf_elim_mc_max_gens(int k) { return std::max(1, kElimMcMaxBlocks / mc2_groups(k)); }
+
+bool gf_elim_mc_taken(const ElimArgs& args, int G) {
+  return elim_mc_mode() && args.pub && args.epoch && args.epoch < kMcFail && gf_elim_blocked(args, G) &&
+         G * gf_elim_mc_groups(args.k, G) <= kElimMcMaxBlocks;
+}
+
+bool gf_elim_mc_enabled() { return elim_mc_mode() != 0; }
+
+bool gf_elim_mc_direct(const ElimArgs& args, int G) {
+  const int m = mc_kernel_for(args.k, G);
+  return gf_elim_mc_taken(args, G) && (m == 2 || m == 4);
 }
 
 size_t gf_elim_mc_pub_bytes(int k, int G) {
-  if (elim_mc_mode() == 4) return (size_t)G * (size_t)((k + 15) / 16) * (kMc4SGran + kMc4RGran + kMc4MGran) * 8;
-  const size_t P = (size_t)gf_elim_mc_groups(k);
+  if (mc_kernel_for(k, G) == 4) return (size_t)G * (size_t)((k + 15) / 16) * (kMc4SGran + kMc4RGran + kMc4MGran) * 8;
+  const size_t P = (size_t)mc2_groups(k);
   return (size_t)G * std::max<size_t>(P * 32 * 64, 2 * P * kMc2PanelGran) * 8;
 }
 
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
   if (G <= kElimMaxGens && args.k >= 2 && args.k <= 256 && gf_elim_mc_taken(args, G)) {
-    if (elim_mc_mode() == 4) {
+    const int m = mc_kernel_for(args.k, G);
+    const dim3 grid(gf_elim_mc_groups(args.k, G), G);
+    if (m == 4) {
       if (!args.direct) return hipErrorInvalidValue;  // mc4 reports directly only
       if (mc4_rows_per_wave() == 4)
-        hipLaunchKernelGGL(gf_elim_mc4_kernel<4>, dim3(gf_elim_mc_groups(args.k), G), dim3(kMc4Threads), 0, stream,
-                           args);
+        hipLaunchKernelGGL(gf_elim_mc4_kernel<4>, grid, dim3(kMc4Threads), 0, stream, args);
       else
-        hipLaunchKernelGGL(gf_elim_mc4_kernel<2>, dim3(gf_elim_mc_groups(args.k), G), dim3(kMc4Threads), 0, stream,
-                           args);
-    } else if (elim_mc_mode() == 1)
-      hipLaunchKernelGGL(gf_elim_mc_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(64 * kMcWaves), 0, stream, args);
-    else
-      hipLaunchKernelGGL(gf_elim_mc2_kernel, dim3(gf_elim_mc_groups(args.k), G), dim3(1024), 0, stream, args);
+        hipLaunchKernelGGL(gf_elim_mc4_kernel<2>, grid, dim3(kMc4Threads), 0, stream, args);
+    } else if (m == 1) {
+      hipLaunchKernelGGL(gf_elim_mc_kernel, grid, dim3(64 * kMcWaves), 0, stream, args);
+    } else {
+      hipLaunchKernelGGL(gf_elim_mc2_kernel, grid, dim3(1024), 0, stream, args);
+    }
     return hipGetLastError();
   }
   if (G > kElimMaxGens || args.k < 2 || args.k > 256 || args.out_pitch % 4 ||

@@ -112,8 +112,11 @@ struct ElimArgs {
   // epoch | 0x80000000 (failed), stored with system-scope release after the
   // workgroup's T rows, so a host polling pinned memory can read them early
   int direct;
-  int variant;  // gf_elim_mc2 tuning bits (KODR_MC2_VARIANT): 1 split the block's small
-                // products over the chain waves, 2 pivot-row broadcast by v_readlane
+  int variant;  // gf_elim_mc2 tuning bits (KODR_MC2_VARIANT, default 28): 1 split the
+                // block's small products over the 8 chain waves, 2 pivot-row broadcast
+                // by v_readlane, 4 circular-form branch-free block inversion
+                // (mc3_gj_v5), 8 batched block update, 16 batched row updates, 32 the
+                // block update over 4 chain waves
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;
@@ -131,9 +134,11 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 // counts[g * groups + q] = 1 (done) or 0 (a singular block or a timeout: the
 // host then takes kodr's route); the decoder's T is valid when all are 1.
 constexpr int kElimMcMaxBlocks = 256;
-// workgroups per decoder: ceil(k / 32) (gf_elim_mc / mc2), or one per 16-row
-// panel plus the chain workgroup (mc4, KODR_ELIM_MC=4)
-int gf_elim_mc_groups(int k);
+// workgroups per decoder of the multi-workgroup kernel a launch of G
+// decoders takes: ceil(k / 32) (gf_elim_mc / mc2), or one per 8 rows plus the
+// chain workgroup (mc4); and the most decoders one such launch takes
+int gf_elim_mc_groups(int k, int G);
+int gf_elim_mc_max_gens(int k);
 size_t gf_elim_mc_pub_bytes(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 // true when gf_elim_mc_taken and the launch honours args.direct (mc2)

@@ -15,4 +15,5 @@ for P in "$P1" "$P2"; do
   timeout -s KILL 120 rocprofv3 --pmc $P -d "$OUT/p$i" -o run --output-format csv -- python3 "$R/bench.py" \
     --steps 20 --warmup 5 --no-extras --no-cpu-baseline --no-encode-decode > "$OUT/p$i.log" 2>&1 || { tail -5 "$OUT/p$i.log"; exit 1; }
 done
-python3 "$R/tools/pmc_sq.py" "$OUT" "true>" | tee "$OUT/summary.txt"
+# the grouped launches are gf_bs_kernel<KW, 0, true, N>
+python3 "$R/tools/pmc_sq.py" "$OUT" ", true, " | tee "$OUT/summary.txt"
