@@ -281,10 +281,13 @@ class RoundTripStep:
          full/decoder.go:50-66 row by row, same state;
       3. ONE grouped GetPieces (rlnc_decoders_get_pieces_device) writes the
          G decoded generations to device memory; HIP events around it;
-      4. the decoders are destroyed (their buffers go back to the pool).
-    Decoder construction sits in the step (host only, microseconds); kodr's
-    decoder bench builds its decoder outside the timer
-    (benches/full/decoder_test.go:71-94)."""
+      4. the next step's G decoders are constructed while GetPieces runs
+         (host only), then this step's decoders are destroyed (their buffers
+         go back to the pool; the destroy synchronises the stream: the step
+         ends with the GPU's work).
+    Decoder construction stays inside the timed steps (each step constructs
+    the next one's; the first warmup step its own); kodr's decoder bench
+    builds its decoder outside the timer (benches/full/decoder_test.go:71-94)."""
 
     def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2):
         import ctypes
@@ -310,17 +313,24 @@ class RoundTripStep:
         self.counts = (ctypes.c_size_t * G)(*([n] * G))
         self.ev = [ctx.event() for _ in range(4)]
         self.t_enc, self.t_add, self.t_get, self.ok = [], [], [], True
+        self.next_decs = None
+
+    def _decoders(self):
+        import ctypes
+        decs = []
+        for g in range(self.G):
+            h = ctypes.c_void_p()
+            self.errors.check(self.L_.rlnc_decoder_create(self.ctx.handle, self.k, ctypes.byref(h)))
+            decs.append(h)
+        return decs
 
     def step(self, i, timed=True):
         import ctypes
         from kodr_amd import device as kdev
         ctx, L_, errors, G, k, L = self.ctx, self.L_, self.errors, self.G, self.k, self.L
         s_ = i % len(self.dW)
-        decs = []
-        for g in range(G):
-            h = ctypes.c_void_p()
-            errors.check(L_.rlnc_decoder_create(ctx.handle, k, ctypes.byref(h)))
-            decs.append(h)
+        decs = self.next_decs if self.next_decs is not None else self._decoders()
+        self.next_decs = None
         darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
         e = self.ev
         ctx.record(e[0])
@@ -335,6 +345,7 @@ class RoundTripStep:
         errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
         ctx.record(e[3])
         self.ok = self.ok and all(st in (0, 3) for st in sts) and all(c == k for c in cons)
+        self.next_decs = self._decoders()    # the next step's, on the host while GetPieces runs
         for x in decs:
             L_.rlnc_decoder_destroy(x)        # synchronises the stream: the step ends here
         if timed:
@@ -362,6 +373,9 @@ class RoundTripStep:
         return self.G * (self.n * setbytes(self.k, self.L) + self.k * (self.k + self.L))
 
     def close(self):
+        for x in self.next_decs or []:
+            self.L_.rlnc_decoder_destroy(x)
+        self.next_decs = None
         for p_ in self.dV + self.dW + [self.dO]:
             self.ctx.free(p_)
 

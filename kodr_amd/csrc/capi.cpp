@@ -108,8 +108,12 @@ struct rlnc_ctx {
   size_t elim_pin_cap = 0;
   DevBuf elim_pub;           // gf_elim_mc's hand-off granules (zeroed when allocated)
   uint32_t elim_epoch = 0;   // gf_elim_mc's launch tag, one per launch
+  DevBuf elim_tdev;          // fresh decoders' T rows (k x k each) as the last batched GPU AddPiece left them
+  uint64_t tdev_seq = 0;     // ... one number per such call
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
+  hipEvent_t rows_ready = nullptr; // ... the rows' producer work (recorded beside side_done)
+  hipStream_t aux = nullptr;       // small downloads that must not queue behind the side copies
 };
 
 struct rlnc_encoder {
@@ -143,6 +147,10 @@ struct rlnc_recoder {
 struct rlnc_decoder {
   rlnc_ctx* ctx = nullptr;   // may be null: coefficient side only
   DecoderCore core;
+  // this decoder's T (k x k, pitch k) in ctx->elim_tdev, valid while
+  // ctx->tdev_seq == tdev_seq (the GPU elimination of a fresh full batch)
+  const uint8_t* tdev = nullptr;
+  uint64_t tdev_seq = 0;
   size_t L = 0, pitch = 0;
   bool have_len = false;
   DevBuf recv;               // received pieces, row i = piece i, pitch
@@ -490,10 +498,15 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->elim_pin = nullptr;
   ctx->gtmat[0].release();
   ctx->gtmat[1].release();
+  if (ctx->aux) {
+    (void)hipStreamSynchronize(ctx->aux);
+    (void)hipStreamDestroy(ctx->aux);
+  }
   if (ctx->side) {
     (void)hipStreamSynchronize(ctx->side);
     (void)hipStreamDestroy(ctx->side);
     (void)hipEventDestroy(ctx->side_done);
+    (void)hipEventDestroy(ctx->rows_ready);
   }
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1292,7 +1305,9 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
   if (!d) return RLNC_OK;
   if (d->ctx) {
     (void)hipSetDevice(d->ctx->device);
-    (void)hipStreamSynchronize(d->ctx->stream);
+    // the buffers go back to the stream-ordered pool; the host's own state
+    // waits for the stream (a query first: an idle stream costs no round trip)
+    if (hipStreamQuery(d->ctx->stream) != hipSuccess) (void)hipStreamSynchronize(d->ctx->stream);
   }
   d->recv.release();
   d->tmat.release();
@@ -1797,6 +1812,16 @@ int ctx_side(rlnc_ctx* ctx) {
   if (ctx->side) return RLNC_OK;
   HIPC(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HIPC(hipEventCreateWithFlags(&ctx->side_done, hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&ctx->rows_ready, hipEventDisableTiming));
+  return RLNC_OK;
+}
+
+// a stream for small reads of rows whose producers are ordered before
+// ctx->rows_ready, and that must not wait for the copies queued after it
+int ctx_aux_after_rows(rlnc_ctx* ctx, hipStream_t* st) {
+  if (!ctx->aux) HIPC(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  HIPC(hipStreamWaitEvent(ctx->aux, ctx->rows_ready, 0));
+  *st = ctx->aux;
   return RLNC_OK;
 }
 
@@ -1983,6 +2008,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   };
   if (side) {
     HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the rows' producer work, ordered before the copies
+    HIPC(hipEventRecord(ctx->rows_ready, ctx->stream));
     HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
   } else {
     TRY(launch_copies());
@@ -2085,6 +2111,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       a.out_pitch = k;
       a.out_gen_stride = k * k;
       a.counts = reinterpret_cast<int*>(ctx->elim_pin_dev);
+      if (!cont && c0 == 0) {  // fresh decoders: T on the device too, for a grouped GetPieces
+        ctx->elim_tdev.bind(ctx->device, ctx->stream);
+        TRY(ctx->elim_tdev.reserve(gpu.size() * k * k));
+        ctx->tdev_seq++;
+      }
+      if (!cont) a.out_dev = ctx->elim_tdev.p + c0 * k * k;
     }
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
@@ -2134,6 +2166,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // memory-bound (a 256 x 520-byte arena each), so spread over host threads.
     // got[i] = rows of the batch accepted
     std::vector<size_t> got(nc);
+    const double tl0 = timing ? tnow() : 0;
     HostPool::get().run(nc, [&](size_t i) {
       rlnc_decoder* d = ds[gpu[c0 + i]];
       const size_t r = base[gpu[c0 + i]];
@@ -2146,7 +2179,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
         ok = tonly ? c == k && d->core.load_inverse(tstates + i * k * k, k)
                    : d->core.load_rref(tstates + i * ostride, opitch, c);
       got[i] = ok ? c - r : 0;
+      const bool on_dev = ok && c == k && !cont && a.out_dev;
+      d->tdev = on_dev ? a.out_dev + i * k * k : nullptr;
+      d->tdev_seq = on_dev ? ctx->tdev_seq : 0;
     });
+    if (timing) fprintf(stderr, "add_pieces_gpu: states loaded %.1f us (%zu decoders)\n", tnow() - tl0, nc);
     for (size_t i = 0; i < nc; i++) {
       const size_t g = gpu[c0 + i];
       rlnc_decoder* d = ds[g];
@@ -2161,7 +2198,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
         } else {
           const size_t rest = counts[g] - c;
           d->hvecs.resize(rest * k);
-          HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, ctx->stream));
+          // the vectors of a batch the GPU left (a singular panel block): read
+          // on a stream that does not wait for the rows' copies beside it
+          hipStream_t vs = ctx->stream;
+          if (side) TRY(ctx_aux_after_rows(ctx, &vs));
+          HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, vs));
           size_t m = 0;
           st = d->core.add_many(d->hvecs.data(), k, rest, &m);
           n += m;
@@ -2455,10 +2496,15 @@ constexpr size_t kGroupGetChunk = 16;
 
 int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* d_out, size_t out_pitch) {
   if (!ds || !G || !d_out || !ds[0]) return RLNC_ERR_INVALID_ARGUMENT;
+  static const int timing = getenv("KODR_ADD_TIMING") ? atoi(getenv("KODR_ADD_TIMING")) : 0;
+  const auto tnow = [] { return std::chrono::duration<double, std::micro>(
+                             std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tg[6] = {timing ? tnow() : 0, 0, 0, 0, 0, 0};
   rlnc_decoder* d0 = ds[0];
   for (size_t g = 0; g < G; g++)
     if (!ds[g]) return RLNC_ERR_INVALID_ARGUMENT;
   for (size_t g = 0; g < G; g++) TRY(dec_flush(ds[g]));
+  if (timing) tg[1] = tnow();
   for (size_t g = 0; g < G; g++)  // full/decoder.go:84-86 for any of them before anything else
     if (!ds[g]->core.is_decoded()) return RLNC_ERR_MORE_USEFUL_PIECES_REQUIRED;
   for (size_t g = 0; g < G; g++) {
@@ -2467,7 +2513,12 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
     if (d->ctx != d0->ctx || d->L != d0->L || d->core.piece_count() != d0->core.piece_count())
       return RLNC_ERR_INVALID_ARGUMENT;
   }
-  const size_t L = d0->L, rows = d0->core.rank(), recv = d0->core.received(), pitch = d0->pitch;
+  const size_t L = d0->L, rows = d0->core.rank(), pitch = d0->pitch;
+  // decoders that received different numbers of rows (a dependent piece
+  // counts) share one launch over the largest: T padded with zero columns,
+  // whose twin rows are never read arithmetically (coefficient 0)
+  size_t recv = 0;
+  for (size_t g = 0; g < G; g++) recv = std::max(recv, ds[g]->core.received());
   if (out_pitch < L || out_pitch % 16) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(set_dev(d0->ctx));
   rlnc_ctx* ctx = d0->ctx;
@@ -2491,14 +2542,40 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
     bool grouped = n > 1;
     for (size_t i = 0; i < n && grouped; i++) {
       const rlnc_decoder* d = ds[g0 + i];
-      grouped = d->core.received() == recv && d->core.rank() == rows && d->pitch == pitch;
+      grouped = d->core.rank() == rows && d->pitch == pitch && d->recv_rows >= recv;
+    }
+    // every T of the chunk where the GPU elimination left it, consecutive
+    // (the decoders of one batched GPU AddPiece, in its order): no host
+    // transform and no upload
+    bool dev_t = grouped && recv == d0->core.piece_count();
+    for (size_t i = 0; i < n && dev_t; i++) {
+      const rlnc_decoder* d = ds[g0 + i];
+      dev_t = d->tdev && d->tdev_seq == ctx->tdev_seq && d->core.received() == recv &&
+              d->tdev == ds[g0]->tdev + i * tsz;
+    }
+    if (dev_t) {
+      for (size_t i = 0; i < n; i++) {
+        rlnc_decoder* d = ds[g0 + i];
+        TRY(dec_extend_twin(d));
+        d->last_gf_rows = rows;
+        d->last_copy_rows = 0;
+        d->last_bs = true;
+        xs[i] = d->recv_bs.p;
+      }
+      const kodr_amd::GemmGroupArgs grp{(int)n, xs, tsz, ostride};
+      HIPC(kodr_amd::gf_gemm_bs(ds[g0]->tdev, recv, rows, recv, xs[0], pitch, d_out + g0 * ostride, out_pitch, L,
+                                ctx->device, ctx->stream, false, &grp));
+      continue;
     }
     // the transforms, one decoder per host task (disjoint slices of hT)
     std::vector<uint8_t> unit(n, 0);
     if (grouped)
       HostPool::get().run(n, [&](size_t i) {
         uint8_t* t = hT.data() + i * tsz;
+        const size_t ri = ds[g0 + i]->core.received();
         ds[g0 + i]->core.copy_transform(t, recv);
+        if (ri < recv)
+          for (size_t r = 0; r < rows; r++) memset(t + r * recv + ri, 0, recv - ri);
         for (size_t r = 0; r < rows && !unit[i]; r++, t += recv) {  // a unit row is a copy: per-decoder route
           size_t nz = 0, last = 0;
           for (size_t j = 0; j < recv && nz < 2; j++)
@@ -2506,6 +2583,7 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
           unit[i] = nz == 1 && t[last] == 1;
         }
       });
+    if (timing) tg[2] = tnow();
     for (size_t i = 0; i < n && grouped; i++) grouped = !unit[i];
     if (!grouped) {
       for (size_t i = 0; i < n; i++)
@@ -2521,11 +2599,16 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
       xs[i] = d->recv_bs.p;
     }
     uint8_t* dT = ctx->gtmat[(g0 / kGroupGetChunk) & 1].p;
+    if (timing) tg[3] = tnow();
     HIPC(ctx->stage.h2d(dT, n * tsz, hT.data(), n * tsz, n * tsz, 1, ctx->stream));
+    if (timing) tg[4] = tnow();
     const kodr_amd::GemmGroupArgs grp{(int)n, xs, tsz, ostride};
     HIPC(kodr_amd::gf_gemm_bs(dT, recv, rows, recv, xs[0], pitch, d_out + g0 * ostride, out_pitch, L, ctx->device,
                               ctx->stream, false, &grp));
   }
+  if (timing)
+    fprintf(stderr, "get_pieces grouped G=%zu: flush %.1f us, checks+transforms %.1f, twins %.1f, T upload %.1f, "
+            "launch %.1f\n", G, tg[1] - tg[0], tg[2] - tg[1], tg[3] - tg[2], tg[4] - tg[3], tnow() - tg[4]);
   return RLNC_OK;
 }
 

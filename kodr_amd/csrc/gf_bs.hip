@@ -131,24 +131,40 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
   t[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
-// copy_bitslice_kernel over several row sets at once (blockIdx.y = set)
+// copy_bitslice_kernel over several row sets at once (blockIdx.y = set), two
+// lanes per 32-byte block: lane pair (2j, 2j + 1) reads and writes its
+// block's halves (16 bytes per lane, contiguous over the wave: one 1 KiB
+// request per instruction instead of two half-used ones), swaps them by DPP,
+// bit-slices the whole block in both lanes and stores its half of the planes
 __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
                                                                    int nblk) {
   const int y = blockIdx.y;
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  const int r = (int)(i / (size_t)nblk), b = (int)(i % (size_t)nblk);
-  if (r >= g.rows[y]) return;
-  const uint4* q = reinterpret_cast<const uint4*>(g.src[y] + (size_t)r * spitch + (size_t)b * kBsBlock);
-  const size_t off = (size_t)r * dpitch + (size_t)b * kBsBlock;
-  const uint4 a = q[0], c = q[1];
-  uint4* p = reinterpret_cast<uint4*>(g.dst[y] + off);
-  p[0] = a;
-  p[1] = c;
-  uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // half-block index
+  const size_t hb = (size_t)nblk * 2;
+  const int r = (int)(i / hb), hi = (int)(i % hb), h = hi & 1;
+  const bool live = r < g.rows[y];
+  // every lane takes part in the swap (a disabled DPP source reads 0)
+  uint4 a = make_uint4(0u, 0u, 0u, 0u);
+  const size_t off = (size_t)r * dpitch + (size_t)hi * 16;
+  if (live) {
+    a = *reinterpret_cast<const uint4*>(g.src[y] + (size_t)r * spitch + (size_t)hi * 16);
+    *reinterpret_cast<uint4*>(g.dst[y] + off) = a;
+  }
+  // the partner lane's half (quad_perm [1, 0, 3, 2])
+  const uint32_t ox = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false);
+  const uint32_t oy = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.y, 0xb1, 0xf, 0xf, false);
+  const uint32_t oz = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false);
+  const uint32_t ow = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false);
+  if (!live) return;
+  uint32_t d[8];
+  if (h == 0) {
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = ox; d[5] = oy; d[6] = oz; d[7] = ow;
+  } else {
+    d[0] = ox; d[1] = oy; d[2] = oz; d[3] = ow; d[4] = a.x; d[5] = a.y; d[6] = a.z; d[7] = a.w;
+  }
   bitslice32(d);
-  uint4* t = reinterpret_cast<uint4*>(g.dbs[y] + off);
-  t[0] = make_uint4(d[0], d[1], d[2], d[3]);
-  t[1] = make_uint4(d[4], d[5], d[6], d[7]);
+  *reinterpret_cast<uint4*>(g.dbs[y] + off) =
+      h == 0 ? make_uint4(d[0], d[1], d[2], d[3]) : make_uint4(d[4], d[5], d[6], d[7]);
 }
 
 // The bodies' only home: this kernel exports the absolute address of body
@@ -833,7 +849,7 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
       return hipErrorInvalidValue;
     maxr = g.rows[i] > maxr ? g.rows[i] : maxr;
   }
-  const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk;
+  const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
   hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)((total + 255) / 256), (unsigned)n), dim3(256), 0,
                      stream, g, spitch, dpitch, (int)nblk);

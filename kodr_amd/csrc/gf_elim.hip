@@ -1762,6 +1762,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         const int gr = 32 * q + 4 * w + i;
         if (gr >= k) continue;
         mc_store_row(out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k), R[i], lane, k);
+        if (args.out_dev) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
       }
     }
   } else {
@@ -2402,6 +2403,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
       const int gr = row0 + RPW * w + i;
       if (gr >= k) continue;
       mc_store_row(out + (size_t)gr * args.out_pitch, R[i], lane, k);
+      if (args.out_dev) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
     }
   }
   __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first

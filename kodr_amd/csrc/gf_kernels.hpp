@@ -112,6 +112,9 @@ struct ElimArgs {
   // epoch | 0x80000000 (failed), stored with system-scope release after the
   // workgroup's T rows, so a host polling pinned memory can read them early
   int direct;
+  // mc2 / mc4 only (optional): the T rows of a finished decoder also to
+  // device memory, out_dev + g * k * k + row * k (GetPieces reads them there)
+  uint8_t* out_dev;
   int variant;  // gf_elim_mc2 tuning bits (KODR_MC2_VARIANT, default 28): 1 split the
                 // block's small products over the 8 chain waves, 2 pivot-row broadcast
                 // by v_readlane, 4 circular-form branch-free block inversion

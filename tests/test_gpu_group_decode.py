@@ -106,6 +106,26 @@ def test_grouped_get_mixed_falls_back(gpu_ctx):
             _lib.lib().rlnc_decoder_destroy(h)
 
 
+def test_grouped_get_mixed_received(gpu_ctx):
+    # a decoder that received a dependent piece (k + 1 received, rank k)
+    # shares the grouped launch: its T is padded with a zero column
+    rng = np.random.default_rng(93)
+    k, L = 64, 8192
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(4)]
+    hs = [_decoder(gpu_ctx, P, rng, extra=3, dup=(g == 2)) for g, P in enumerate(gens)]
+    try:
+        assert _lib.lib().rlnc_decoder_received(hs[2]) == k + 1
+        assert _lib.lib().rlnc_decoder_received(hs[0]) == k
+        st, got = _grouped_get(gpu_ctx, hs, k, L, L)
+        assert st == 0
+        for g in range(4):
+            assert np.array_equal(got[g], gens[g]), g
+            assert _stats(hs[g]) == (k, 0, True), g   # every decoder in the one bit-sliced launch
+    finally:
+        for h in hs:
+            _lib.lib().rlnc_decoder_destroy(h)
+
+
 def test_grouped_get_not_decoded(gpu_ctx):
     rng = np.random.default_rng(5)
     k, L = 16, 1024
