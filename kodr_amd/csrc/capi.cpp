@@ -1842,10 +1842,6 @@ int ctx_elim_tables(rlnc_ctx* ctx) {
 // launch's epoch (a new tag per launch; the buffer is zeroed when it is
 // allocated and when the tags wrap)
 int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
-  // mc2 tuning bits (gf_kernels.hpp); default 28: the circular block inversion,
-  // batched block update and batched row updates
-  static const int variant = getenv("KODR_MC2_VARIANT") ? atoi(getenv("KODR_MC2_VARIANT")) : 28;
-  a->variant = variant;
   const size_t bytes = kodr_amd::gf_elim_mc_pub_bytes((int)k, (int)nc);
   ctx->elim_pub.bind(ctx->device, ctx->stream);
   const uint8_t* before = ctx->elim_pub.p;
@@ -2526,6 +2522,9 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
   const bool bs = G > 1 && rows >= kBsMinRows && !few_narrow_rows(rows, recv, L) && (pitch % 32) == 0 &&
                   bs_chunk_rows(rows, std::max<size_t>(recv, 1), pitch, L) >= recv && kodr_amd::bs_ready(ctx->device);
   if (!bs) {
+    if (timing)
+      fprintf(stderr, "get_pieces grouped G=%zu: per decoder (rows %zu, recv %zu, pitch %zu, chunk rows %zu)\n", G,
+              rows, recv, pitch, bs_chunk_rows(rows, std::max<size_t>(recv, 1), pitch, L));
     for (size_t g = 0; g < G; g++) TRY(rlnc_decoder_get_pieces_device(ds[g], d_out + g * ostride, out_pitch));
     return RLNC_OK;
   }
@@ -2565,6 +2564,7 @@ int rlnc_decoders_get_pieces_device(rlnc_decoder* const* ds, size_t G, uint8_t* 
       const kodr_amd::GemmGroupArgs grp{(int)n, xs, tsz, ostride};
       HIPC(kodr_amd::gf_gemm_bs(ds[g0]->tdev, recv, rows, recv, xs[0], pitch, d_out + g0 * ostride, out_pitch, L,
                                 ctx->device, ctx->stream, false, &grp));
+      if (timing) fprintf(stderr, "get_pieces grouped: chunk %zu (%zu) T on the device %.1f us\n", g0, n, tnow() - tg[1]);
       continue;
     }
     // the transforms, one decoder per host task (disjoint slices of hT)

@@ -709,53 +709,26 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
   if (tid == 0) args.counts[g] = c;
 }
 
-// ---- FULL batches on several workgroups per decoder ("mc") ---------------
-// One decoder's k <= 256 rows are split into P = ceil(k / 32) groups of 32
-// rows, a workgroup each (16 waves: rows 2w and 2w + 1, lane = dword), so the
-// k^3 GF MACs of the inversion run on P CUs instead of one.  Padded to
-// K' = 32 P with identity rows and columns, the matrix is inverted in place
-// by block Gauss-Jordan ("Y" form: after a group's step its 32 columns hold
-// the inverse-in-progress, the columns of later groups the reduced
-// coefficients; T columns are indexed by arrival, so the result is C^-1
-// itself, the state kodr reaches: [I | C^-1], see the FULL case above):
-//  * group q's step, by its own workgroup, in two 16-wide sub-panels: the
-//    16 x 16 block of the sub-panel's rows is inverted by panel_gj (S), the
-//    sub-panel's rows become S x (rows with the block replaced by I), and the
-//    other 16 rows drop the sub-panel columns (row ^= m x new rows).  The 32
-//    rows it ends with are group q's pivot rows N_q; they are published.
-//  * every other workgroup, for every group in order, takes N_q and drops
-//    group q's columns from its rows: m = the row's 32 bytes there, those
-//    bytes zeroed, row ^= m x N_q.
-// Hand-off (MI355X_MICROARCH.md, hand-off price list, granule form R2): N_q
-// goes out as 8-byte {data, tag} granules, each ONE agent-scope relaxed store
-// (global_store_dwordx2 sc1); a consumer re-reads its granules with sc1 loads
-// until every tag is this launch's epoch.  No fence, no flag.  A singular
-// block publishes its group with the FAIL bit; a workgroup that sees one
-// publishes its own group the same way (if it has not yet) and stops, so
-// every workgroup ends; spins are bounded.  Every workgroup writes its status
-// word (1 done, 0 failed) last.  All G * P workgroups must be resident at once
-// (kElimMcMaxBlocks, one 1024-thread workgroup per CU).
-constexpr int kMcWaves = 16;
+// ---- FULL batches on several workgroups per decoder (mc2, mc4) -----------
+// One decoder's inversion split over several workgroups (below: mc2, the
+// chain and the rows of 32-row groups in one workgroup each; mc4, the chain
+// on a workgroup of its own beside 8-row row workgroups).  Both hand data
+// between workgroups the same way (MI355X_MICROARCH.md, hand-off price list,
+// granule form R2): 8-byte {data, tag} granules, each ONE agent-scope
+// relaxed store (global_store_dwordx2 sc1); a consumer re-reads its granules
+// with sc1 loads until every tag is this launch's epoch.  No fence, no flag.
+// A singular panel block publishes FAIL; a workgroup that sees one publishes
+// FAIL on what it still owes and stops, so every workgroup ends; spins are
+// bounded.  Every workgroup writes its status word last.  All of a launch's
+// workgroups must be resident at once (kElimMcMaxBlocks).  (Round 4's first
+// multi-workgroup kernel, 32-row groups handing finished pivot rows to each
+// other with no overlap between groups, is superseded by these two: 200 vs
+// 153 (mc2) and 59 (mc4) us for one k = 256 decoder.)
 constexpr uint32_t kMcFail = 0x80000000u;
 constexpr int kMcSpinMax = 1 << 20;  // >= ~1 s of polling: only a lost workgroup gets there
 
-struct ElimMcLds {
-  uint4 tab[256 * 2];     // the [256][8]-dword tables as 16-byte rows (as ElimBlkLds)
-  uint4 itab[256 * 2];    // the same for inv(f): a pivot's normalization from LDS (a workgroup
-                          // runs only 32 pivots, so scalar-cache reads of them would mostly miss)
-  uint32_t nq[32][64];    // a consumed group's pivot rows; in the own step, a sub-panel's new rows
-  uint32_t prow[16][64];  // the sub-panel's rows before the step
-  uint32_t pan[16][4];    // its 16 x 16 block
-  uint32_t sd[16][4];     // S = block^-1 by rows: S[c][u] = byte u % 4 of sd[c][u / 4]
-  int fail;               // 1 singular / FAIL seen, 2 timeout
-};
-
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-__device__ __forceinline__ void mc_tab(const ElimMcLds& lds, uint32_t f, uint4& t, uint32_t& t2) {
-  t = lds.tab[2 * f];
-  t2 = lds.tab[2 * f + 1].x;
-}
 __device__ __forceinline__ uint32_t mc_mul(const uint4& t, uint32_t t2, uint32_t s0, uint32_t s1, uint32_t s2) {
   return __builtin_amdgcn_perm(t.y, t.x, s0) ^ __builtin_amdgcn_perm(t.w, t.z, s1) ^
          __builtin_amdgcn_perm(t2, t2, s2);
@@ -769,260 +742,6 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int cd) {
     case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xaa, 0xf, 0xf, false);
     default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xff, 0xf, 0xf, false);
   }
-}
-
-// The 16 x 16 block inversion for the mc kernel: pan (written by other waves,
-// behind a barrier) -> sd = block^-1, or fail = 1.  One wave, lane (t, d) =
-// dword d of block row t: P (block) and Tr (the identity it turns into S).
-// Gauss-Jordan with row pivoting (the lowest unpicked row with a non-zero
-// entry), arranged so that one step waits for one dependent LDS lookup:
-//  * the row's multiplier f = byte c of its own row (a DPP quad broadcast),
-//    whose tables are gathered at once, before the pivot is known;
-//  * the pivot (ballot), its entry dp and the tables of inv(dp) (gf256.go:77-86);
-//  * the pivot row normalized, Pn = inv(dp) x row_p (broadcast by bpermute,
-//    issued beside the table read), then row ^= f x Pn; the pivot row
-//    becomes Pn (for it f x Pn would be the raw row).
-__device__ __forceinline__ void mc_panel_gj(ElimMcLds& lds, int lane) {
-  const int t = lane >> 2, d = lane & 3;
-  uint32_t P = lds.pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
-  uint32_t used = 0;  // rows picked so far (uniform)
-  int mycol = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const int cd = c >> 2, cb = 8 * (c & 3);
-    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
-    uint4 tf;
-    uint32_t tf2;
-    mc_tab(lds, f, tf, tf2);
-    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
-    if (m == 0) {
-      if (lane == 0) lds.fail = 1;
-      return;
-    }
-    const int pl = __builtin_ctzll(m), tp = pl >> 2;
-    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
-    const uint4 ti = lds.itab[2 * dp];  // tables of inv(dp)
-    const uint32_t ti2 = lds.itab[2 * dp + 1].x;
-    const uint32_t Pp = bperm(P, tp * 4 + d), Tp = bperm(Tr, tp * 4 + d);
-    const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
-    const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
-    if (t == tp) {
-      P = Pn;
-      Tr = Tn;
-      mycol = c;
-    } else {
-      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
-      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
-    }
-    used |= 1u << tp;
-  }
-  lds.sd[mycol][d] = Tr;
-}
-
-__device__ __forceinline__ void mc_publish(gu64* dst, uint32_t tag, uint32_t r0, uint32_t r1) {
-  __hip_atomic_store(dst, ((unsigned long long)tag << 32) | r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(dst + 64, ((unsigned long long)tag << 32) | r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(64 * kMcWaves) void gf_elim_mc_kernel(ElimArgs args) {
-  __shared__ ElimMcLds lds;
-  const int q = blockIdx.x, g = blockIdx.y, P = gridDim.x;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k = args.k;
-  const uint32_t epoch = args.epoch;
-  gu64* pub = (gu64*)args.pub + (size_t)g * P * 32 * 64;
-
-#ifdef KODR_ELIM_TIMING
-  // tuning build: s_memrealtime (100 MHz, chip-wide) stamps, stored by
-  // thread 0 straight into this workgroup's first out row (no result):
-  // [0] entry, [1] rows loaded, [2 + gp] after group gp's step, [2 + P] end,
-  // [3 + P + 3 s + j] inside the own step (sub-panel s: block inverted, new
-  // rows, other rows updated)
-  uint64_t* const tsout = reinterpret_cast<uint64_t*>(args.out + (size_t)g * args.out_gen_stride +
-                                                      (size_t)(32 * q) * args.out_pitch);
-  if (tid == 0) tsout[0] = __builtin_amdgcn_s_memrealtime();
-#define MC_STAMP(i)                                                \
-  do {                                                             \
-    if (tid == 0) tsout[i] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define MC_STAMP(i) \
-  do {              \
-  } while (0)
-#endif
-  for (int i = tid; i < 256 * 2; i += 64 * kMcWaves) {
-    const uint32_t* a = args.tables + 4 * i;
-    const uint32_t* b = args.tables + kElimInvTables + 4 * i;
-    lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
-    lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
-  }
-  if (tid == 0) lds.fail = 0;
-
-  // rows 32q + 2w + i: C (padded with identity rows and columns past k)
-  uint32_t R[2];
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    const int gr = 32 * q + 2 * w + i;
-    uint32_t v = 0;
-    if (gr < k) {
-      const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
-    } else if (gr >> 2 == lane) {
-      v = 1u << (8 * (gr & 3));
-    }
-    R[i] = v;
-  }
-  __syncthreads();
-  MC_STAMP(1);
-
-  bool published = false;
-  for (int gp = 0; gp < P; gp++) {
-    if (gp == q) {
-      // ---- own step: two 16-wide sub-panels on this workgroup's rows ----
-#pragma unroll
-      for (int s = 0; s < 2; s++) {
-        const int db = 8 * q + 4 * s;  // the sub-panel's first dword (lane)
-        const bool blk = (w >> 3) == s;  // waves 8s .. 8s + 7 hold its rows
-        if (blk) {
-#pragma unroll
-          for (int i = 0; i < 2; i++) {
-            const int lr = 2 * (w - 8 * s) + i;
-            lds.prow[lr][lane] = R[i];
-            if (lane >= db && lane < db + 4) lds.pan[lr][lane - db] = R[i];
-          }
-        }
-        __syncthreads();
-        if (w == 0) mc_panel_gj(lds, lane);
-        __syncthreads();
-        MC_STAMP(3 + P + 3 * s);
-        if (lds.fail) break;  // uniform
-        {  // new row c = w: sum_u S[c][u] x row u, the block replaced by S[c]
-          uint32_t acc = 0;
-#pragma unroll
-          for (int u4 = 0; u4 < 4; u4++) {
-            const uint32_t sw = __builtin_amdgcn_readfirstlane(lds.sd[w][u4]);
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              const uint32_t x = lds.prow[4 * u4 + e][lane];
-              uint4 t;
-              uint32_t t2;
-              mc_tab(lds, (sw >> (8 * e)) & 0xffu, t, t2);
-              acc ^= mc_mul(t, t2, sel0(x), sel1(x), sel2(x));
-            }
-          }
-          if (lane >= db && lane < db + 4) acc = lds.sd[w][lane - db];
-          lds.nq[w][lane] = acc;
-        }
-        __syncthreads();
-        MC_STAMP(4 + P + 3 * s);
-        if (blk) {
-#pragma unroll
-          for (int i = 0; i < 2; i++) R[i] = lds.nq[2 * (w - 8 * s) + i][lane];
-        } else {
-          uint32_t F[2][4];
-#pragma unroll
-          for (int i = 0; i < 2; i++)
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) F[i][qd] = __builtin_amdgcn_readlane(R[i], db + qd);
-          if (lane >= db && lane < db + 4) R[0] = R[1] = 0;
-#pragma unroll
-          for (int c = 0; c < 16; c++) {
-            const uint32_t x = lds.nq[c][lane];
-            const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-              uint4 t;
-              uint32_t t2;
-              mc_tab(lds, (F[i][c >> 2] >> (8 * (c & 3))) & 0xffu, t, t2);
-              R[i] ^= mc_mul(t, t2, s0, s1, s2);
-            }
-          }
-        }
-        __syncthreads();
-        MC_STAMP(5 + P + 3 * s);
-      }
-      if (lds.fail) break;
-      mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch, R[0], R[1]);
-      published = true;
-      MC_STAMP(2 + gp);
-      continue;
-    }
-    // ---- another group's pivot rows: take them, drop its columns ----
-    {
-      const gu64* src = pub + ((size_t)gp * 32 + 2 * w) * 64 + lane;
-      int spins = 0;
-      uint64_t a, b;
-      for (;;) {
-        a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t ta = (uint32_t)(a >> 32), tb2 = (uint32_t)(b >> 32);
-        const bool ok = (ta & ~kMcFail) == epoch && (tb2 & ~kMcFail) == epoch;
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
-          if (__builtin_amdgcn_ballot_w64(((ta | tb2) & kMcFail) != 0) && lane == 0) lds.fail = 1;
-          break;
-        }
-        if (++spins > kMcSpinMax) {
-          if (lane == 0) lds.fail = 2;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      lds.nq[2 * w][lane] = (uint32_t)a;
-      lds.nq[2 * w + 1][lane] = (uint32_t)b;
-    }
-    __syncthreads();
-    if (lds.fail) break;  // uniform
-    {
-      const int db = 8 * gp;
-      uint32_t F[2][8];
-#pragma unroll
-      for (int i = 0; i < 2; i++)
-#pragma unroll
-        for (int qd = 0; qd < 8; qd++) F[i][qd] = __builtin_amdgcn_readlane(R[i], db + qd);
-      if (lane >= db && lane < db + 8) R[0] = R[1] = 0;
-#pragma unroll
-      for (int c = 0; c < 32; c++) {
-        const uint32_t x = lds.nq[c][lane];
-        const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-          uint4 t;
-          uint32_t t2;
-          mc_tab(lds, (F[i][c >> 2] >> (8 * (c & 3))) & 0xffu, t, t2);
-          R[i] ^= mc_mul(t, t2, s0, s1, s2);
-        }
-      }
-    }
-    __syncthreads();
-    MC_STAMP(2 + gp);
-  }
-  MC_STAMP(2 + P);
-#ifdef KODR_ELIM_TIMING
-  if (tid == 0) args.counts[g * P + q] = 0;
-  return;
-#endif
-#undef MC_STAMP
-  const bool ok = lds.fail == 0;
-  if (!ok && !published)  // a later group waits for this one: tell it
-    mc_publish(pub + ((size_t)q * 32 + 2 * w) * 64 + lane, epoch | kMcFail, 0u, 0u);
-  if (ok) {  // T rows (pivot column order = row order), [C^-1] at byte k of each out row
-    uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      const int gr = 32 * q + 2 * w + i;
-      if (gr >= k) continue;
-      uint8_t* row = out + (size_t)gr * args.out_pitch + k;
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(R[i] >> (8 * b));
-    }
-  }
-  __syncthreads();
-  if (tid == 0) args.counts[g * P + q] = ok ? 1 : 0;
 }
 
 // one state row's bytes [0, k) from a row register (lane = dword): a dword
@@ -1055,7 +774,7 @@ __device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane,
 //    from rows as of panel p - 2, so it does not wait for the row waves'
 //    apply of p - 1), inverts it (mc2_panel_gj) and publishes S_p; for any
 //    other panel the chain waves poll R_p and S_p into LDS.
-// Hand-offs between workgroups as in gf_elim_mc_kernel (granules tagged with
+// Hand-offs between workgroups as described above (granules tagged with
 // the launch epoch, FAIL bit; bounded spins); three LDS slots per panel
 // buffer so a slot is rewritten only after both roles are two panels on.
 constexpr int kMc2Slots = 3;
@@ -1069,10 +788,6 @@ struct ElimMc2Lds {
   uint32_t mb[kMc2Slots][16][8];   // owned panel p: its rows' panel p - 1 (dwords 0-3) and panel p (4-7) columns, as of panel p - 2
   uint32_t mw[8][4][4];            // row wave w: its rows' columns of the panel it applies (the multipliers)
   uint32_t fw[8][4][4];            // row wave w: G of its rows
-  uint32_t ft[16][4];              // chain: F of the block rows
-  uint32_t pan[16][4];             // chain: the block to invert
-  uint32_t part[8][16][4];         // chain: the chain waves' partial products (split variant)
-  int chain_sync;                  // chain-wave rounds (split variant: 8 per round)
   int rows_done;                   // row-wave iterations finished (8 per panel, 8 for the start)
   int chain_cnt;                   // chain-wave iterations finished (8 per panel)
   int fail;                        // 1 singular / FAIL seen, 2 timeout
@@ -1089,396 +804,10 @@ __device__ __forceinline__ bool mc2_wait(ElimMc2Lds& lds, int* ctr, int target) 
     __builtin_amdgcn_s_sleep(1);
   }
 }
-// mc2_wait without s_sleep, for hand-offs between chain waves a few hundred
-// cycles apart
-__device__ __forceinline__ bool mc3_spin(ElimMc2Lds& lds, int* ctr, int target) {
-  for (int spins = 0;; spins++) {
-    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
-    if (spins > 64 * kMcSpinMax) {
-      __hip_atomic_store(&lds.fail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return false;
-    }
-    if ((spins & 255) == 255 && __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-      return false;
-  }
-}
 // this wave's LDS writes first, then one count
 __device__ __forceinline__ void mc2_signal(int* ctr, int lane) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// mc_panel_gj's algorithm on an LDS block, S to `s_out` ([16][4]), its rows
-// also kept in registers for publishing (returns false if singular)
-// lane (t, d) gets dword d of block row tp: four v_readlane and a select,
-// instead of a ds_bpermute round trip
-__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int tp, int d) {
-  const uint32_t a0 = __builtin_amdgcn_readlane(v, 4 * tp), a1 = __builtin_amdgcn_readlane(v, 4 * tp + 1);
-  const uint32_t a2 = __builtin_amdgcn_readlane(v, 4 * tp + 2), a3 = __builtin_amdgcn_readlane(v, 4 * tp + 3);
-  return d == 0 ? a0 : d == 1 ? a1 : d == 2 ? a2 : a3;
-}
-
-template <bool RL>
-__device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab, const uint32_t (*pan)[4],
-                                             uint32_t (*s_out)[4], int lane, uint32_t* s_val, int* s_row) {
-  const int t = lane >> 2, d = lane & 3;
-  uint32_t P = pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
-  uint32_t used = 0;
-  int mycol = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const int cd = c >> 2, cb = 8 * (c & 3);
-    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
-    const uint4 tf = tab[2 * f];
-    const uint32_t tf2 = tab[2 * f + 1].x;
-    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
-    if (m == 0) return false;
-    const int pl = __builtin_ctzll(m), tp = pl >> 2;
-    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
-    const uint4 ti = itab[2 * dp];
-    const uint32_t ti2 = itab[2 * dp + 1].x;
-    const uint32_t Pp = RL ? row_bcast(P, tp, d) : bperm(P, tp * 4 + d);
-    const uint32_t Tp = RL ? row_bcast(Tr, tp, d) : bperm(Tr, tp * 4 + d);
-    const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
-    const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
-    if (t == tp) {
-      P = Pn;
-      Tr = Tn;
-      mycol = c;
-    } else {
-      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
-      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
-    }
-    used |= 1u << tp;
-  }
-  s_out[mycol][d] = Tr;
-  *s_val = Tr;
-  *s_row = mycol;
-  return true;
-}
-
-// out[t][d] = base ^ sum_c M[t][c] x X[c][d], one wave, lane (t, d): the M
-// row (4 dwords, 16 bytes) and X rows (4 dwords) in LDS
-__device__ __forceinline__ uint32_t mc2_small(const uint4* tab, uint32_t base, const uint32_t* mrow,
-                                              const uint32_t (*x)[4], int d) {
-  uint32_t acc = base;
-  for (int cq = 0; cq < 4; cq++) {
-    const uint32_t mw = mrow[cq];
-#pragma unroll
-    for (int cc = 0; cc < 4; cc++) {
-      const uint32_t m = (mw >> (8 * cc)) & 0xffu;
-      const uint4 t = tab[2 * m];
-      const uint32_t t2 = tab[2 * m + 1].x;
-      const uint32_t xv = x[4 * cq + cc][d];
-      acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
-    }
-  }
-  return acc;
-}
-
-// The owned block brought up to date with the previous panel in one pass, one
-// wave, lane (t, d): F = M x S_{p-1} (M: the block rows' panel p - 1
-// columns, `mrow` = row t's 4 dwords), then blk ^= F x R_{p-1}[:, panel p]
-// (`rp` rows, dwords col0 .. col0 + 3).  Every operand load and both table
-// gathers are issued before the arithmetic that waits on them; F's row goes
-// to the quad by DPP, not through LDS.
-__device__ __forceinline__ uint32_t mc3_block_update(const uint4* tab, uint32_t blk, const uint32_t* mrow,
-                                                     const uint32_t (*sp)[4], const uint32_t (*rp)[64], int col0,
-                                                     int lane) {
-  const int d = lane & 3;
-  uint32_t mw[4], sv[16], rv[16];
-#pragma unroll
-  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    sv[c] = sp[c][d];
-    rv[c] = rp[c][col0 + d];
-  }
-  uint32_t F = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t m = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    const uint4 tt = tab[2 * m];
-    const uint32_t tt2 = tab[2 * m + 1].x;
-    F ^= gmul4(tt, tt2, sel0(sv[c]), sel1(sv[c]), sel2(sv[c]));
-  }
-  uint32_t fw[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
-  uint32_t acc = blk;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t m = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    const uint4 tt = tab[2 * m];
-    const uint32_t tt2 = tab[2 * m + 1].x;
-    acc ^= gmul4(tt, tt2, sel0(rv[c]), sel1(rv[c]), sel2(rv[c]));
-  }
-  return acc;
-}
-
-// mc2_panel_gj with the block in registers (lane (t, d) = dword d of block
-// row t, `P`) and the pivot's inverse tables gathered beside the row's own
-// tables, before the pivot is known: lane (t, 0..3) loads the tables of f
-// and inv(f) for its row's entry f in column c; the pivot lane's inverse
-// tables then come by v_readlane.  One dependent LDS round trip per step
-// (the gathers), no ds_bpermute.
-__device__ __forceinline__ bool mc3_panel_gj(const uint4* tab, const uint4* itab, uint32_t P, int lane,
-                                             uint32_t* s_val, int* s_row) {
-  const int t = lane >> 2, d = lane & 3;
-  uint32_t Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
-  uint32_t used = 0;
-  int mycol = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t f = (quad_bcast(P, c >> 2) >> (8 * (c & 3))) & 0xffu;
-    const uint4 tf = tab[2 * f];
-    const uint32_t tf2 = tab[2 * f + 1].x;
-    const uint4 ti = itab[2 * f];
-    const uint32_t ti2 = itab[2 * f + 1].x;
-    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
-    if (m == 0) return false;
-    const int pl = __builtin_ctzll(m), tp = pl >> 2;
-    const uint32_t Pp = row_bcast(P, tp, d), Tp = row_bcast(Tr, tp, d);
-    const uint4 si = make_uint4(__builtin_amdgcn_readlane(ti.x, pl), __builtin_amdgcn_readlane(ti.y, pl),
-                                __builtin_amdgcn_readlane(ti.z, pl), __builtin_amdgcn_readlane(ti.w, pl));
-    const uint32_t si2 = __builtin_amdgcn_readlane(ti2, pl);
-    const uint32_t Pn = gmul4(si, si2, sel0(Pp), sel1(Pp), sel2(Pp));
-    const uint32_t Tn = gmul4(si, si2, sel0(Tp), sel1(Tp), sel2(Tp));
-    if (t == tp) {
-      P = Pn;
-      Tr = Tn;
-      mycol = c;
-    } else {
-      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
-      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
-    }
-    used |= 1u << tp;
-  }
-  *s_val = Tr;
-  *s_row = mycol;
-  return true;
-}
-
-// The block update's second product with the selectors of its data operand
-// (R_{p-1}[:, panel p], known before S_{p-1}) computed ahead: r0/r1/r2[c] =
-// sel0/1/2 of R[c][col0 + d]
-__device__ __forceinline__ void mc3_pre_r(const uint32_t (*rp)[64], int col0, int lane, uint32_t* r0, uint32_t* r1,
-                                          uint32_t* r2) {
-  const int d = lane & 3;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t x = rp[c][col0 + d];
-    r0[c] = sel0(x);
-    r1[c] = sel1(x);
-    r2[c] = sel2(x);
-  }
-}
-__device__ __forceinline__ uint32_t mc3_block_update_pre(const uint4* tab, uint32_t blk, const uint32_t* mrow,
-                                                         const uint32_t (*sp)[4], const uint32_t* r0,
-                                                         const uint32_t* r1, const uint32_t* r2, int lane) {
-  const int d = lane & 3;
-  uint32_t mw[4], sv[16];
-#pragma unroll
-  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
-#pragma unroll
-  for (int c = 0; c < 16; c++) sv[c] = sp[c][d];
-  uint32_t F = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t m = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    const uint4 tt = tab[2 * m];
-    const uint32_t tt2 = tab[2 * m + 1].x;
-    F ^= gmul4(tt, tt2, sel0(sv[c]), sel1(sv[c]), sel2(sv[c]));
-  }
-  uint32_t fw[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
-  uint32_t acc = blk;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t m = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    const uint4 tt = tab[2 * m];
-    const uint32_t tt2 = tab[2 * m + 1].x;
-    acc ^= gmul4(tt, tt2, r0[c], r1[c], r2[c]);
-  }
-  return acc;
-}
-
-// The 16 x 16 block inversion in circular form: one 16-byte row per block
-// row (lane (t, d) = dword d), slot s holding the coefficient of column s
-// until column s is eliminated and then T's column pi(s) (pi(s): the row that
-// pivoted column s), as gf_elim_circ_kernel does for whole rows.  Step c:
-// the pivot row (lowest unpicked row with slot c non-zero, entry dp) is
-// normalized, Q = inv(dp) x row, whose slot c is then 1; a non-pivot row
-// takes row ^= f x Q' with Q' = Q but slot c = 1 ^ inv(dp), so that its slot
-// c becomes f x inv(dp) = T[t][pi(c)] (the pivot row's T column pi(c), its
-// own identity, was 1); the pivot row becomes Q with slot c = inv(dp).  An
-// unpicked row's own identity T[t][t] = 1 needs no slot: no pivot row has T
-// column t.  At the end, S row c = the slots of row pi(c) with output byte j
-// taken from slot pi^-1(j) (two v_perm per lane).  Half the row operations
-// of the [block | T] form (mc2_panel_gj).
-__device__ __forceinline__ bool mc3_gj_circ(const uint4* tab, const uint4* itab, uint32_t P, int lane,
-                                            uint32_t* s_val, int* s_row) {
-  const int t = lane >> 2, d = lane & 3;
-  uint32_t used = 0, selA = 0, selB = 0, mskA = 0;
-  int mycol = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const int cd = c >> 2, cb = 8 * (c & 3);
-    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
-    const uint4 tf = tab[2 * f];
-    const uint32_t tf2 = tab[2 * f + 1].x;
-    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
-    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
-    if (m == 0) return false;
-    const int pl = __builtin_ctzll(m), tp = pl >> 2;
-    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
-    const uint4 ti = itab[2 * dp];
-    const uint32_t ti2 = itab[2 * dp + 1].x;
-    const uint32_t Pp = bperm(P, tp * 4 + d);
-    const uint32_t inv = (ti.x >> 8) & 0xffu;  // T0 entry 1: inv(dp) x 1
-    uint32_t Q = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
-    if (d == cd) Q ^= inv << cb;
-    if (t == tp) {
-      P = d == cd ? Q ^ (1u << cb) : Q;
-      mycol = c;
-    } else {
-      P ^= gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
-    }
-    used |= 1u << tp;
-    if (d == (tp >> 2)) {  // output byte tp of every S row comes from slot c
-      const int ob = 8 * (tp & 3);
-      if (c < 8) {
-        selA |= (uint32_t)c << ob;
-        mskA |= 0xffu << ob;
-      } else {
-        selB |= (uint32_t)(c - 8) << ob;
-      }
-    }
-  }
-  const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
-  *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
-  *s_row = mycol;
-  return true;
-}
-
-// The circular-form inversion with one block row per lane (lanes 0-15, row t
-// = lane: slots in P[0..3]; lanes 16-63 carry zero rows that are never
-// candidates) and no branches, so that the step's one LDS round trip -- the
-// gather of the tables of f and of inv(f) for every row's entry f in column
-// c -- is issued before anything waits on it:
-//  * the candidates are a ballot of f != 0 under an SGPR mask of unpicked
-//    rows; the pivot row's four dwords and, once the gather is back, the
-//    tables of inv(dp) come by v_readlane from the pivot lane (uniform);
-//  * Q = inv(dp) x pivot row with slot c = 1 ^ inv(dp); a row takes row ^=
-//    f x Q, the pivot lane takes Q with slot c = inv(dp) (a select);
-//  * pi^-1 is kept as sixteen 4-bit slot numbers in an SGPR pair; at the end
-//    S row c = row pi(c)'s slots with output byte j from slot pi^-1(j)
-//    (v_perm with uniform selectors).
-// Returns false (S undefined) when a column has no candidate.  Lane t < 16
-// ends holding S row *s_row in s[0..3].
-__device__ __forceinline__ bool mc3_gj_rows(const uint4* tab, const uint4* itab, uint32_t* P, int lane, uint32_t* s,
-                                            int* s_row) {
-  uint64_t cand = 0xffffull;  // unpicked rows (lanes)
-  uint64_t pinv = 0;          // slot of output byte j at bits 4j .. 4j + 3
-  bool fail = false;
-  int mycol = 0;
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const int cq = c >> 2, cb = 8 * (c & 3);
-    const uint32_t f = (P[cq] >> cb) & 0xffu;
-    const uint4 tf = tab[2 * f];
-    const uint32_t tf2 = tab[2 * f + 1].x;
-    const uint4 ti = itab[2 * f];
-    const uint32_t ti2 = itab[2 * f + 1].x;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
-    fail |= m == 0;
-    const int pl = m ? __builtin_ctzll(m) : 0;
-    cand &= ~(1ull << pl);
-    pinv |= (uint64_t)c << (4 * pl);
-    uint32_t pr[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) pr[q] = __builtin_amdgcn_readlane(P[q], pl);
-    const uint4 si = make_uint4(__builtin_amdgcn_readlane(ti.x, pl), __builtin_amdgcn_readlane(ti.y, pl),
-                                __builtin_amdgcn_readlane(ti.z, pl), __builtin_amdgcn_readlane(ti.w, pl));
-    const uint32_t si2 = __builtin_amdgcn_readlane(ti2, pl);
-    const uint32_t inv = (si.x >> 8) & 0xffu;
-    const bool piv = lane == pl;
-    mycol = piv ? c : mycol;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      uint32_t Q = gmul4(si, si2, sel0(pr[q]), sel1(pr[q]), sel2(pr[q]));
-      if (q == cq) Q ^= inv << cb;
-      const uint32_t upd = P[q] ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
-      P[q] = piv ? (q == cq ? Q ^ (1u << cb) : Q) : upd;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    uint32_t sa = 0, sb = 0, ma = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t sl = (uint32_t)(pinv >> (4 * (4 * q + b))) & 15u;
-      if (sl < 8) {
-        sa |= sl << (8 * b);
-        ma |= 0xffu << (8 * b);
-      } else {
-        sb |= (sl - 8) << (8 * b);
-      }
-    }
-    s[q] = (__builtin_amdgcn_perm(P[1], P[0], sa) & ma) | (__builtin_amdgcn_perm(P[3], P[2], sb) & ~ma);
-  }
-  *s_row = mycol;
-  return !fail;
-}
-
-// acc ^ sum over 8 terms of (tables of the multiplier bytes m[0..7]) x data
-// with precomputed selectors: all 16 table reads are issued first (a
-// scheduling barrier keeps the compiler from sinking each read next to its
-// use, which serialises one LDS round trip per term)
-__device__ __forceinline__ uint32_t mc3_dot8(const uint4* tab, uint32_t acc, const uint32_t* m, const uint32_t* s0,
-                                             const uint32_t* s1, const uint32_t* s2) {
-  uint4 tt[8];
-  uint32_t t2[8];
-#pragma unroll
-  for (int c = 0; c < 8; c++) {
-    tt[c] = tab[2 * m[c]];
-    t2[c] = tab[2 * m[c] + 1].x;
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int c = 0; c < 8; c++) acc ^= gmul4(tt[c], t2[c], s0[c], s1[c], s2[c]);
-  return acc;
-}
-
-// mc3_block_update_pre with the table reads batched (mc3_dot8): F = M x S,
-// then blk ^= F x R[:, panel p] (R's selectors r0/r1/r2 computed ahead)
-__device__ __forceinline__ uint32_t mc3_block_update_b(const uint4* tab, uint32_t blk, const uint32_t* mrow,
-                                                       const uint32_t (*sp)[4], const uint32_t* r0,
-                                                       const uint32_t* r1, const uint32_t* r2, int lane) {
-  const int d = lane & 3;
-  uint32_t mw[4], m[16], s0[16], s1[16], s2[16];
-#pragma unroll
-  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
-#pragma unroll
-  for (int c = 0; c < 16; c++) {
-    const uint32_t x = sp[c][d];
-    m[c] = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-    s0[c] = sel0(x);
-    s1[c] = sel1(x);
-    s2[c] = sel2(x);
-  }
-  uint32_t F = mc3_dot8(tab, 0u, m, s0, s1, s2);
-  F = mc3_dot8(tab, F, m + 8, s0 + 8, s1 + 8, s2 + 8);
-  uint32_t fw[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
-#pragma unroll
-  for (int c = 0; c < 16; c++) m[c] = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-  uint32_t acc = mc3_dot8(tab, blk, m, r0, r1, r2);
-  return mc3_dot8(tab, acc, m + 8, r0 + 8, r1 + 8, r2 + 8);
 }
 
 // acc ^ sum over 8 terms of (tables of m[c]) x x[c], both the tables and the
@@ -1609,7 +938,6 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   if (tid == 0) {
     lds.rows_done = 0;
     lds.chain_cnt = 0;
-    lds.chain_sync = 0;
     lds.fail = 0;
   }
   __syncthreads();
@@ -1676,41 +1004,27 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         uint32_t gw[4];  // dword cq of each row's G (wave-uniform)
 #pragma unroll
         for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
-        if (args.variant & 16) {
-          // the 16 (uniform) table reads and 4 data reads of these columns
-          // first, then the arithmetic: one LDS round trip per 4 columns
-          uint4 tt[4][4];
-          uint32_t t2[4][4], xs[4];
-#pragma unroll
-          for (int cc = 0; cc < 4; cc++) {
-            xs[cc] = lds.rp[slot][4 * cq + cc][lane];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-              const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
-              tt[cc][i] = lds.tab[2 * f];
-              t2[cc][i] = lds.tab[2 * f + 1].x;
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int cc = 0; cc < 4; cc++) {
-            const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
-#pragma unroll
-            for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
-          }
-          continue;
-        }
+        // the 16 (uniform) table reads and 4 data reads of these columns
+        // first, then the arithmetic: one LDS round trip per 4 columns
+        // (sinking each read next to its use cost one round trip per term)
+        uint4 tt[4][4];
+        uint32_t t2[4][4], xs[4];
 #pragma unroll
         for (int cc = 0; cc < 4; cc++) {
-          const uint32_t x = lds.rp[slot][4 * cq + cc][lane];
-          const uint32_t s0 = sel0(x), s1 = sel1(x), s2 = sel2(x);
+          xs[cc] = lds.rp[slot][4 * cq + cc][lane];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
-            const uint4 t = lds.tab[2 * f];
-            const uint32_t t2 = lds.tab[2 * f + 1].x;
-            acc[i] ^= mc_mul(t, t2, s0, s1, s2);
+            tt[cc][i] = lds.tab[2 * f];
+            t2[cc][i] = lds.tab[2 * f + 1].x;
           }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int cc = 0; cc < 4; cc++) {
+          const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+#pragma unroll
+          for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
         }
       }
       const int u = lane - db;  // the panel columns take G
@@ -1768,9 +1082,8 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   } else {
     // ================= chain waves =================
     const int cw = w - 8;
-    if (cw == 0 || ((args.variant & 32) && cw < 4)) __builtin_amdgcn_s_setprio(3);
+    if (cw == 0) __builtin_amdgcn_s_setprio(3);
     int unpublished = 2 * q;  // the first owned panel whose S_p is not out yet
-    int nsync = 0;            // chain_sync rounds so far (split variant)
     for (int p = 0; p < NP; p++) {
       const int slot = p % kMc2Slots;
       gu64* base = pub + (size_t)p * kMc2PanelGran;
@@ -1781,137 +1094,20 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       if ((p >> 1) == q) {
         if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
         if (cw == 0) MC2_STAMP(4 * p + 1);
-        const bool split = (args.variant & 1) && p >= 1;
-        const bool split4 = (args.variant & 32) && p >= 1;
-        if (split4 && cw < 4) {
-          // the block update over chain waves 0-3 (on four SIMDs), four
-          // terms of each product per wave, partials folded through LDS
-          // behind tight-spin counters (no s_sleep): F's four partials go to
-          // every wave, the second product's to wave 0
-          const int t = lane >> 2, d = lane & 3, ps = (p - 1) % kMc2Slots;
-          uint32_t m[4];
-          const uint32_t mw4 = lds.mb[slot][t][cw];
-#pragma unroll
-          for (int cc = 0; cc < 4; cc++) m[cc] = (mw4 >> (8 * cc)) & 0xffu;
-          uint32_t acc = 0;
-          {
-            uint4 tt[4];
-            uint32_t t2[4], xv[4];
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) {
-              tt[cc] = lds.tab[2 * m[cc]];
-              t2[cc] = lds.tab[2 * m[cc] + 1].x;
-              xv[cc] = lds.sp[ps][4 * cw + cc][d];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) acc ^= gmul4(tt[cc], t2[cc], sel0(xv[cc]), sel1(xv[cc]), sel2(xv[cc]));
-          }
-          lds.part[cw][t][d] = acc;
-          mc2_signal(&lds.chain_sync, lane);
-          nsync += 2;
-          if (!mc3_spin(lds, &lds.chain_sync, 4 * (nsync - 1))) break;
-          const uint32_t F = lds.part[0][t][d] ^ lds.part[1][t][d] ^ lds.part[2][t][d] ^ lds.part[3][t][d];
-          const uint32_t fw = quad_bcast(F, cw);  // F[t][4 cw .. 4 cw + 3]
-          uint32_t acc2 = 0;
-          {
-            uint4 tt[4];
-            uint32_t t2[4], xv[4];
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) {
-              const uint32_t f = (fw >> (8 * cc)) & 0xffu;
-              tt[cc] = lds.tab[2 * f];
-              t2[cc] = lds.tab[2 * f + 1].x;
-              xv[cc] = lds.rp[ps][4 * cw + cc][4 * p + d];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int cc = 0; cc < 4; cc++) acc2 ^= gmul4(tt[cc], t2[cc], sel0(xv[cc]), sel1(xv[cc]), sel2(xv[cc]));
-          }
-          lds.part[4 + cw][t][d] = acc2;
-          mc2_signal(&lds.chain_sync, lane);
-          if (cw == 0 && !mc3_spin(lds, &lds.chain_sync, 4 * nsync)) break;
-        }
-        if (split) {
-          // the block's two small products with their 16 terms split over the
-          // 8 chain waves (2 each), partials folded through LDS
-          const int t = lane >> 2, d = lane & 3, ps = (p - 1) % kMc2Slots;
-          const int c0 = 2 * cw;
-          uint32_t acc = 0;
-#pragma unroll
-          for (int cc = 0; cc < 2; cc++) {  // F = M x S_{p-1}
-            const uint32_t m = (lds.mb[slot][t][c0 >> 2] >> (8 * ((c0 + cc) & 3))) & 0xffu;
-            const uint4 tt = lds.tab[2 * m];
-            const uint32_t tt2 = lds.tab[2 * m + 1].x;
-            const uint32_t xv = lds.sp[ps][c0 + cc][d];
-            acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
-          }
-          lds.part[cw][t][d] = acc;
-          mc2_signal(&lds.chain_sync, lane);
-          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
-          uint32_t fdw = 0;  // dword c0 / 4 of F's row t: the bytes of this wave's two terms
-#pragma unroll
-          for (int j = 0; j < 8; j++) fdw ^= lds.part[j][t][c0 >> 2];
-          uint32_t acc2 = 0;
-#pragma unroll
-          for (int cc = 0; cc < 2; cc++) {  // block ^= F x R_{p-1}[:, panel p]
-            const uint32_t m = (fdw >> (8 * ((c0 + cc) & 3))) & 0xffu;
-            const uint4 tt = lds.tab[2 * m];
-            const uint32_t tt2 = lds.tab[2 * m + 1].x;
-            const uint32_t xv = lds.rp[ps][c0 + cc][4 * p + d];
-            acc2 ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
-          }
-          // every wave has read part[] (its F dword) before anyone overwrites it
-          mc2_signal(&lds.chain_sync, lane);
-          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
-          lds.part[cw][t][d] = acc2;
-          mc2_signal(&lds.chain_sync, lane);
-          if (!mc2_wait(lds, &lds.chain_sync, 8 * ++nsync)) break;
-        }
         if (cw == 0) {
+          // the block brought up to date with panel p - 1 (two 16-term
+          // products, operand reads batched), then inverted in registers
           const int t = lane >> 2, d = lane & 3;
           uint32_t blk = lds.mb[slot][t][4 + d];
-          if (split4) {
-            blk ^= lds.part[4][t][d] ^ lds.part[5][t][d] ^ lds.part[6][t][d] ^ lds.part[7][t][d];
-          } else if (split) {
-#pragma unroll
-            for (int j = 0; j < 8; j++) blk ^= lds.part[j][t][d];
-          } else if (p >= 1 && (args.variant & 8)) {  // batched operand reads
+          if (p >= 1) {
             const int ps = (p - 1) % kMc2Slots;
             blk = mc3_block_update_c(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], lds.rp[ps], 4 * p, lane);
-          } else if (p >= 1) {
-            const int ps = (p - 1) % kMc2Slots;
-            lds.ft[t][d] = mc2_small(lds.tab, 0u, lds.mb[slot][t], lds.sp[ps], d);  // F = M x S_{p-1}
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            // block ^= F x R_{p-1}[:, panel p]
-            uint32_t acc = blk;
-            for (int cq = 0; cq < 4; cq++) {
-              const uint32_t fw = lds.ft[t][cq];
-#pragma unroll
-              for (int cc = 0; cc < 4; cc++) {
-                const uint32_t m = (fw >> (8 * cc)) & 0xffu;
-                const uint4 tt = lds.tab[2 * m];
-                const uint32_t tt2 = lds.tab[2 * m + 1].x;
-                const uint32_t xv = lds.rp[ps][4 * cq + cc][4 * p + d];
-                acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
-              }
-            }
-            blk = acc;
           }
-          lds.pan[t][d] = blk;
-          __builtin_amdgcn_s_waitcnt(0xc07f);
           MC2_STAMP(4 * p + 2);
           uint32_t sval = 0;
           int srow = 0;
-          bool inv_ok;
-          if (args.variant & 4) {  // circular-form, branch-free inversion of the block in registers
-            inv_ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
-            if (inv_ok) lds.sp[slot][srow][d] = sval;
-          } else if (args.variant & 2) {
-            inv_ok = mc2_panel_gj<true>(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow);
-          } else {
-            inv_ok = mc2_panel_gj<false>(lds.tab, lds.itab, lds.pan, lds.sp[slot], lane, &sval, &srow);
-          }
+          const bool inv_ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
+          if (inv_ok) lds.sp[slot][srow][d] = sval;
           if (!inv_ok) {
             __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           } else {
@@ -2469,12 +1665,15 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   return full;
 }
 
-// KODR_ELIM_MC: 0 one workgroup per decoder, 1 the first multi-workgroup
-// kernel, 2 mc2, 4 mc4, 3 (default) mc4 when the launch's decoders fit it
+// KODR_ELIM_MC: 0 one workgroup per decoder, 2 mc2, 4 mc4, 3 (default) mc4
+// when the launch's decoders fit it
 // (G * groups <= kElimMcMaxBlocks: one decoder at k = 256 takes 33
 // workgroups) else mc2 (measured: profiles/r04/elim_modes/)
 static int elim_mc_mode() {
-  static const int mc = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 3;
+  static const int mc = [] {
+    const int m = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 3;
+    return m == 0 || m == 2 || m == 4 ? m : 3;
+  }();
   return mc;
 }
 
@@ -2527,8 +1726,6 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
         hipLaunchKernelGGL(gf_elim_mc4_kernel<4>, grid, dim3(kMc4Threads), 0, stream, args);
       else
         hipLaunchKernelGGL(gf_elim_mc4_kernel<2>, grid, dim3(kMc4Threads), 0, stream, args);
-    } else if (m == 1) {
-      hipLaunchKernelGGL(gf_elim_mc_kernel, grid, dim3(64 * kMcWaves), 0, stream, args);
     } else {
       hipLaunchKernelGGL(gf_elim_mc2_kernel, grid, dim3(1024), 0, stream, args);
     }

@@ -115,11 +115,6 @@ struct ElimArgs {
   // mc2 / mc4 only (optional): the T rows of a finished decoder also to
   // device memory, out_dev + g * k * k + row * k (GetPieces reads them there)
   uint8_t* out_dev;
-  int variant;  // gf_elim_mc2 tuning bits (KODR_MC2_VARIANT, default 28): 1 split the
-                // block's small products over the 8 chain waves, 2 pivot-row broadcast
-                // by v_readlane, 4 circular-form branch-free block inversion
-                // (mc3_gj_v5), 8 batched block update, 16 batched row updates, 32 the
-                // block update over 4 chain waves
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;

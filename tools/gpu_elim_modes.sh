@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-modes}; mkdir -p $OUT
 for rep in 1 2; do
   for M in ${MODES:-0 2 4}; do
-    KODR_ELIM_MC=$M KODR_MC2_VARIANT=60 timeout -k 10 200 python -u tools/elim_time.py ${KS:-160,192,224,256} ${GS:-1,8,16} > $OUT/e_${M}_r$rep.log 2>&1 || { tail -20 $OUT/e_${M}_r$rep.log; exit 1; }
+    KODR_ELIM_MC=$M timeout -k 10 200 python -u tools/elim_time.py ${KS:-160,192,224,256} ${GS:-1,8,16} > $OUT/e_${M}_r$rep.log 2>&1 || { tail -20 $OUT/e_${M}_r$rep.log; exit 1; }
     echo "mc=$M rep $rep: $(python3 -c "import json,sys; print(' '.join(f\"k{d['k']}G{d['G']} {d['gpu_us']}/{d['host_us']}\" for d in map(json.loads, open(sys.argv[1]))))" $OUT/e_${M}_r$rep.log)"
   done
 done

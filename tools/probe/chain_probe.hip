@@ -19,6 +19,396 @@
 namespace kodr_amd {
 namespace {
 
+// The library's mc2 LDS plus the probe's scratch (the panel block and the
+// split variants' partial products live here, not in the kernel).
+struct ProbeLds {
+  uint4 tab[256 * 2];
+  uint4 itab[256 * 2];
+  uint32_t rp[kMc2Slots][16][64];
+  uint32_t sp[kMc2Slots][16][4];
+  uint32_t mb[kMc2Slots][16][8];
+  uint32_t pan[16][4];
+  uint32_t ft[16][4];
+  int chain_cnt;
+  int fail;
+};
+
+// ---- chain variants measured here and not kept in the library ----
+// mc_panel_gj's algorithm on an LDS block, S to `s_out` ([16][4]), its rows
+// also kept in registers for publishing (returns false if singular)
+// lane (t, d) gets dword d of block row tp: four v_readlane and a select,
+// instead of a ds_bpermute round trip
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int tp, int d) {
+  const uint32_t a0 = __builtin_amdgcn_readlane(v, 4 * tp), a1 = __builtin_amdgcn_readlane(v, 4 * tp + 1);
+  const uint32_t a2 = __builtin_amdgcn_readlane(v, 4 * tp + 2), a3 = __builtin_amdgcn_readlane(v, 4 * tp + 3);
+  return d == 0 ? a0 : d == 1 ? a1 : d == 2 ? a2 : a3;
+}
+
+template <bool RL>
+__device__ __forceinline__ bool mc2_panel_gj(const uint4* tab, const uint4* itab, const uint32_t (*pan)[4],
+                                             uint32_t (*s_out)[4], int lane, uint32_t* s_val, int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t P = pan[t][d], Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
+  uint32_t used = 0;
+  int mycol = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) return false;
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
+    const uint4 ti = itab[2 * dp];
+    const uint32_t ti2 = itab[2 * dp + 1].x;
+    const uint32_t Pp = RL ? row_bcast(P, tp, d) : bperm(P, tp * 4 + d);
+    const uint32_t Tp = RL ? row_bcast(Tr, tp, d) : bperm(Tr, tp * 4 + d);
+    const uint32_t Pn = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
+    const uint32_t Tn = gmul4(ti, ti2, sel0(Tp), sel1(Tp), sel2(Tp));
+    if (t == tp) {
+      P = Pn;
+      Tr = Tn;
+      mycol = c;
+    } else {
+      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
+      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
+    }
+    used |= 1u << tp;
+  }
+  s_out[mycol][d] = Tr;
+  *s_val = Tr;
+  *s_row = mycol;
+  return true;
+}
+
+// out[t][d] = base ^ sum_c M[t][c] x X[c][d], one wave, lane (t, d): the M
+// row (4 dwords, 16 bytes) and X rows (4 dwords) in LDS
+__device__ __forceinline__ uint32_t mc2_small(const uint4* tab, uint32_t base, const uint32_t* mrow,
+                                              const uint32_t (*x)[4], int d) {
+  uint32_t acc = base;
+  for (int cq = 0; cq < 4; cq++) {
+    const uint32_t mw = mrow[cq];
+#pragma unroll
+    for (int cc = 0; cc < 4; cc++) {
+      const uint32_t m = (mw >> (8 * cc)) & 0xffu;
+      const uint4 t = tab[2 * m];
+      const uint32_t t2 = tab[2 * m + 1].x;
+      const uint32_t xv = x[4 * cq + cc][d];
+      acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+    }
+  }
+  return acc;
+}
+
+// The owned block brought up to date with the previous panel in one pass, one
+// wave, lane (t, d): F = M x S_{p-1} (M: the block rows' panel p - 1
+// columns, `mrow` = row t's 4 dwords), then blk ^= F x R_{p-1}[:, panel p]
+// (`rp` rows, dwords col0 .. col0 + 3).  Every operand load and both table
+// gathers are issued before the arithmetic that waits on them; F's row goes
+// to the quad by DPP, not through LDS.
+__device__ __forceinline__ uint32_t mc3_block_update(const uint4* tab, uint32_t blk, const uint32_t* mrow,
+                                                     const uint32_t (*sp)[4], const uint32_t (*rp)[64], int col0,
+                                                     int lane) {
+  const int d = lane & 3;
+  uint32_t mw[4], sv[16], rv[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    sv[c] = sp[c][d];
+    rv[c] = rp[c][col0 + d];
+  }
+  uint32_t F = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t m = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    const uint4 tt = tab[2 * m];
+    const uint32_t tt2 = tab[2 * m + 1].x;
+    F ^= gmul4(tt, tt2, sel0(sv[c]), sel1(sv[c]), sel2(sv[c]));
+  }
+  uint32_t fw[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
+  uint32_t acc = blk;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t m = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    const uint4 tt = tab[2 * m];
+    const uint32_t tt2 = tab[2 * m + 1].x;
+    acc ^= gmul4(tt, tt2, sel0(rv[c]), sel1(rv[c]), sel2(rv[c]));
+  }
+  return acc;
+}
+
+// mc2_panel_gj with the block in registers (lane (t, d) = dword d of block
+// row t, `P`) and the pivot's inverse tables gathered beside the row's own
+// tables, before the pivot is known: lane (t, 0..3) loads the tables of f
+// and inv(f) for its row's entry f in column c; the pivot lane's inverse
+// tables then come by v_readlane.  One dependent LDS round trip per step
+// (the gathers), no ds_bpermute.
+__device__ __forceinline__ bool mc3_panel_gj(const uint4* tab, const uint4* itab, uint32_t P, int lane,
+                                             uint32_t* s_val, int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t Tr = (t >> 2) == d ? 1u << (8 * (t & 3)) : 0u;
+  uint32_t used = 0;
+  int mycol = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t f = (quad_bcast(P, c >> 2) >> (8 * (c & 3))) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const uint4 ti = itab[2 * f];
+    const uint32_t ti2 = itab[2 * f + 1].x;
+    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) return false;
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t Pp = row_bcast(P, tp, d), Tp = row_bcast(Tr, tp, d);
+    const uint4 si = make_uint4(__builtin_amdgcn_readlane(ti.x, pl), __builtin_amdgcn_readlane(ti.y, pl),
+                                __builtin_amdgcn_readlane(ti.z, pl), __builtin_amdgcn_readlane(ti.w, pl));
+    const uint32_t si2 = __builtin_amdgcn_readlane(ti2, pl);
+    const uint32_t Pn = gmul4(si, si2, sel0(Pp), sel1(Pp), sel2(Pp));
+    const uint32_t Tn = gmul4(si, si2, sel0(Tp), sel1(Tp), sel2(Tp));
+    if (t == tp) {
+      P = Pn;
+      Tr = Tn;
+      mycol = c;
+    } else {
+      P ^= gmul4(tf, tf2, sel0(Pn), sel1(Pn), sel2(Pn));
+      Tr ^= gmul4(tf, tf2, sel0(Tn), sel1(Tn), sel2(Tn));
+    }
+    used |= 1u << tp;
+  }
+  *s_val = Tr;
+  *s_row = mycol;
+  return true;
+}
+
+// The block update's second product with the selectors of its data operand
+// (R_{p-1}[:, panel p], known before S_{p-1}) computed ahead: r0/r1/r2[c] =
+// sel0/1/2 of R[c][col0 + d]
+__device__ __forceinline__ void mc3_pre_r(const uint32_t (*rp)[64], int col0, int lane, uint32_t* r0, uint32_t* r1,
+                                          uint32_t* r2) {
+  const int d = lane & 3;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t x = rp[c][col0 + d];
+    r0[c] = sel0(x);
+    r1[c] = sel1(x);
+    r2[c] = sel2(x);
+  }
+}
+__device__ __forceinline__ uint32_t mc3_block_update_pre(const uint4* tab, uint32_t blk, const uint32_t* mrow,
+                                                         const uint32_t (*sp)[4], const uint32_t* r0,
+                                                         const uint32_t* r1, const uint32_t* r2, int lane) {
+  const int d = lane & 3;
+  uint32_t mw[4], sv[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
+#pragma unroll
+  for (int c = 0; c < 16; c++) sv[c] = sp[c][d];
+  uint32_t F = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t m = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    const uint4 tt = tab[2 * m];
+    const uint32_t tt2 = tab[2 * m + 1].x;
+    F ^= gmul4(tt, tt2, sel0(sv[c]), sel1(sv[c]), sel2(sv[c]));
+  }
+  uint32_t fw[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
+  uint32_t acc = blk;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t m = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    const uint4 tt = tab[2 * m];
+    const uint32_t tt2 = tab[2 * m + 1].x;
+    acc ^= gmul4(tt, tt2, r0[c], r1[c], r2[c]);
+  }
+  return acc;
+}
+
+// The 16 x 16 block inversion in circular form: one 16-byte row per block
+// row (lane (t, d) = dword d), slot s holding the coefficient of column s
+// until column s is eliminated and then T's column pi(s) (pi(s): the row that
+// pivoted column s), as gf_elim_circ_kernel does for whole rows.  Step c:
+// the pivot row (lowest unpicked row with slot c non-zero, entry dp) is
+// normalized, Q = inv(dp) x row, whose slot c is then 1; a non-pivot row
+// takes row ^= f x Q' with Q' = Q but slot c = 1 ^ inv(dp), so that its slot
+// c becomes f x inv(dp) = T[t][pi(c)] (the pivot row's T column pi(c), its
+// own identity, was 1); the pivot row becomes Q with slot c = inv(dp).  An
+// unpicked row's own identity T[t][t] = 1 needs no slot: no pivot row has T
+// column t.  At the end, S row c = the slots of row pi(c) with output byte j
+// taken from slot pi^-1(j) (two v_perm per lane).  Half the row operations
+// of the [block | T] form (mc2_panel_gj).
+__device__ __forceinline__ bool mc3_gj_circ(const uint4* tab, const uint4* itab, uint32_t P, int lane,
+                                            uint32_t* s_val, int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint32_t used = 0, selA = 0, selB = 0, mskA = 0;
+  int mycol = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const bool nz = d == 0 && f != 0u && !((used >> t) & 1u);
+    const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+    if (m == 0) return false;
+    const int pl = __builtin_ctzll(m), tp = pl >> 2;
+    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
+    const uint4 ti = itab[2 * dp];
+    const uint32_t ti2 = itab[2 * dp + 1].x;
+    const uint32_t Pp = bperm(P, tp * 4 + d);
+    const uint32_t inv = (ti.x >> 8) & 0xffu;  // T0 entry 1: inv(dp) x 1
+    uint32_t Q = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp));
+    if (d == cd) Q ^= inv << cb;
+    if (t == tp) {
+      P = d == cd ? Q ^ (1u << cb) : Q;
+      mycol = c;
+    } else {
+      P ^= gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
+    }
+    used |= 1u << tp;
+    if (d == (tp >> 2)) {  // output byte tp of every S row comes from slot c
+      const int ob = 8 * (tp & 3);
+      if (c < 8) {
+        selA |= (uint32_t)c << ob;
+        mskA |= 0xffu << ob;
+      } else {
+        selB |= (uint32_t)(c - 8) << ob;
+      }
+    }
+  }
+  const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
+  *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
+  *s_row = mycol;
+  return true;
+}
+
+// The circular-form inversion with one block row per lane (lanes 0-15, row t
+// = lane: slots in P[0..3]; lanes 16-63 carry zero rows that are never
+// candidates) and no branches, so that the step's one LDS round trip -- the
+// gather of the tables of f and of inv(f) for every row's entry f in column
+// c -- is issued before anything waits on it:
+//  * the candidates are a ballot of f != 0 under an SGPR mask of unpicked
+//    rows; the pivot row's four dwords and, once the gather is back, the
+//    tables of inv(dp) come by v_readlane from the pivot lane (uniform);
+//  * Q = inv(dp) x pivot row with slot c = 1 ^ inv(dp); a row takes row ^=
+//    f x Q, the pivot lane takes Q with slot c = inv(dp) (a select);
+//  * pi^-1 is kept as sixteen 4-bit slot numbers in an SGPR pair; at the end
+//    S row c = row pi(c)'s slots with output byte j from slot pi^-1(j)
+//    (v_perm with uniform selectors).
+// Returns false (S undefined) when a column has no candidate.  Lane t < 16
+// ends holding S row *s_row in s[0..3].
+__device__ __forceinline__ bool mc3_gj_rows(const uint4* tab, const uint4* itab, uint32_t* P, int lane, uint32_t* s,
+                                            int* s_row) {
+  uint64_t cand = 0xffffull;  // unpicked rows (lanes)
+  uint64_t pinv = 0;          // slot of output byte j at bits 4j .. 4j + 3
+  bool fail = false;
+  int mycol = 0;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cq = c >> 2, cb = 8 * (c & 3);
+    const uint32_t f = (P[cq] >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const uint4 ti = itab[2 * f];
+    const uint32_t ti2 = itab[2 * f + 1].x;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
+    fail |= m == 0;
+    const int pl = m ? __builtin_ctzll(m) : 0;
+    cand &= ~(1ull << pl);
+    pinv |= (uint64_t)c << (4 * pl);
+    uint32_t pr[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) pr[q] = __builtin_amdgcn_readlane(P[q], pl);
+    const uint4 si = make_uint4(__builtin_amdgcn_readlane(ti.x, pl), __builtin_amdgcn_readlane(ti.y, pl),
+                                __builtin_amdgcn_readlane(ti.z, pl), __builtin_amdgcn_readlane(ti.w, pl));
+    const uint32_t si2 = __builtin_amdgcn_readlane(ti2, pl);
+    const uint32_t inv = (si.x >> 8) & 0xffu;
+    const bool piv = lane == pl;
+    mycol = piv ? c : mycol;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      uint32_t Q = gmul4(si, si2, sel0(pr[q]), sel1(pr[q]), sel2(pr[q]));
+      if (q == cq) Q ^= inv << cb;
+      const uint32_t upd = P[q] ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
+      P[q] = piv ? (q == cq ? Q ^ (1u << cb) : Q) : upd;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t sa = 0, sb = 0, ma = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t sl = (uint32_t)(pinv >> (4 * (4 * q + b))) & 15u;
+      if (sl < 8) {
+        sa |= sl << (8 * b);
+        ma |= 0xffu << (8 * b);
+      } else {
+        sb |= (sl - 8) << (8 * b);
+      }
+    }
+    s[q] = (__builtin_amdgcn_perm(P[1], P[0], sa) & ma) | (__builtin_amdgcn_perm(P[3], P[2], sb) & ~ma);
+  }
+  *s_row = mycol;
+  return !fail;
+}
+
+// acc ^ sum over 8 terms of (tables of the multiplier bytes m[0..7]) x data
+// with precomputed selectors: all 16 table reads are issued first (a
+// scheduling barrier keeps the compiler from sinking each read next to its
+// use, which serialises one LDS round trip per term)
+__device__ __forceinline__ uint32_t mc3_dot8(const uint4* tab, uint32_t acc, const uint32_t* m, const uint32_t* s0,
+                                             const uint32_t* s1, const uint32_t* s2) {
+  uint4 tt[8];
+  uint32_t t2[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    tt[c] = tab[2 * m[c]];
+    t2[c] = tab[2 * m[c] + 1].x;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < 8; c++) acc ^= gmul4(tt[c], t2[c], s0[c], s1[c], s2[c]);
+  return acc;
+}
+
+// mc3_block_update_pre with the table reads batched (mc3_dot8): F = M x S,
+// then blk ^= F x R[:, panel p] (R's selectors r0/r1/r2 computed ahead)
+__device__ __forceinline__ uint32_t mc3_block_update_b(const uint4* tab, uint32_t blk, const uint32_t* mrow,
+                                                       const uint32_t (*sp)[4], const uint32_t* r0,
+                                                       const uint32_t* r1, const uint32_t* r2, int lane) {
+  const int d = lane & 3;
+  uint32_t mw[4], m[16], s0[16], s1[16], s2[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) mw[q] = mrow[q];
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const uint32_t x = sp[c][d];
+    m[c] = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    s0[c] = sel0(x);
+    s1[c] = sel1(x);
+    s2[c] = sel2(x);
+  }
+  uint32_t F = mc3_dot8(tab, 0u, m, s0, s1, s2);
+  F = mc3_dot8(tab, F, m + 8, s0 + 8, s1 + 8, s2 + 8);
+  uint32_t fw[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
+#pragma unroll
+  for (int c = 0; c < 16; c++) m[c] = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+  uint32_t acc = mc3_dot8(tab, blk, m, r0, r1, r2);
+  return mc3_dot8(tab, acc, m + 8, r0 + 8, r1 + 8, r2 + 8);
+}
+
+
+
 struct ProbeIn {  // one iteration's data (dwords)
   uint32_t mb[16][8];  // block rows: panel p - 1 columns (0-3), panel p columns (4-7)
   uint32_t sp[16][4];  // S_{p-1}
@@ -28,7 +418,7 @@ struct ProbeIn {  // one iteration's data (dwords)
 template <int SMV, int GJV>
 __global__ __launch_bounds__(1024) void chain_probe(const uint32_t* tables, const ProbeIn* in, int iters, int mode,
                                                     unsigned long long* stats, uint32_t* s_out) {
-  __shared__ ElimMc2Lds lds;
+  __shared__ ProbeLds lds;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   for (int i = tid; i < 256 * 2; i += 1024) {
