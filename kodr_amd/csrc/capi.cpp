@@ -254,7 +254,9 @@ size_t gemm_chunk_rows(size_t ldx) { return ldx ? (kMaxDescBytes - 1) / ldx : 0;
 size_t bs_chunk_rows(size_t M, size_t K, size_t ldx, size_t ncols) {
   if (!ldx || ldx > 0x7fffffff) return 0;
   size_t kc = std::min<size_t>(K, (((size_t)1 << 32) - 1) / ldx);
-  if (kc > 8) kc = kc / 8 * 8;
+  // K in one launch when it fits (the kernel reads rows >= K as zero); split
+  // launches take whole 8-row program chunks
+  if (kc < K && kc > 8) kc = kc / 8 * 8;
   while (kc && !kodr_amd::plan_gemm_bs(M, kc, ncols).ok) kc = kc > 8 ? kc / 2 / 8 * 8 : 0;
   return kc;
 }
@@ -2197,11 +2199,16 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
           // the vectors of a batch the GPU left (a singular panel block): read
           // on a stream that does not wait for the rows' copies beside it
           hipStream_t vs = ctx->stream;
+          const double tf0 = timing ? tnow() : 0;
           if (side) TRY(ctx_aux_after_rows(ctx, &vs));
           HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, vs));
+          const double tf1 = timing ? tnow() : 0;
           size_t m = 0;
           st = d->core.add_many(d->hvecs.data(), k, rest, &m);
           n += m;
+          if (timing)
+            fprintf(stderr, "add_pieces_gpu: decoder %zu on the host from row %zu: vectors %.1f us, solve %.1f\n", g,
+                    c, tf1 - tf0, tnow() - tf1);
         }
       }
       int pst = dec_batch_post(d, rows[g], pitch, true, bcs[g], n);

@@ -135,36 +135,60 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
 // lanes per 32-byte block: lane pair (2j, 2j + 1) reads and writes its
 // block's halves (16 bytes per lane, contiguous over the wave: one 1 KiB
 // request per instruction instead of two half-used ones), swaps them by DPP,
-// bit-slices the whole block in both lanes and stores its half of the planes
-__global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
-                                                                   int nblk) {
-  const int y = blockIdx.y;
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // half-block index
-  const size_t hb = (size_t)nblk * 2;
-  const int r = (int)(i / hb), hi = (int)(i % hb), h = hi & 1;
-  const bool live = r < g.rows[y];
-  // every lane takes part in the swap (a disabled DPP source reads 0)
-  uint4 a = make_uint4(0u, 0u, 0u, 0u);
-  const size_t off = (size_t)r * dpitch + (size_t)hi * 16;
-  if (live) {
-    a = *reinterpret_cast<const uint4*>(g.src[y] + (size_t)r * spitch + (size_t)hi * 16);
-    *reinterpret_cast<uint4*>(g.dst[y] + off) = a;
-  }
-  // the partner lane's half (quad_perm [1, 0, 3, 2])
+// bit-slices the whole block in both lanes and stores its half of the planes.
+// Grid-stride over a capped grid (copy_bitslice_rows_grouped): the copies run
+// beside the elimination kernel, whose workgroups must find free wave slots
+// even when the copies reach the CUs first (a grid of one lane per half-block
+// filled every CU, and the elimination's workgroups waited behind it).
+__device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r, size_t hi, size_t spitch,
+                                             size_t dpitch, const uint4& a) {
   const uint32_t ox = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false);
   const uint32_t oy = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.y, 0xb1, 0xf, 0xf, false);
   const uint32_t oz = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false);
   const uint32_t ow = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false);
-  if (!live) return;
+  const size_t off = r * dpitch + hi * 16;
+  *reinterpret_cast<uint4*>(g.dst[y] + off) = a;
   uint32_t d[8];
-  if (h == 0) {
+  if ((hi & 1) == 0) {
     d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = ox; d[5] = oy; d[6] = oz; d[7] = ow;
   } else {
     d[0] = ox; d[1] = oy; d[2] = oz; d[3] = ow; d[4] = a.x; d[5] = a.y; d[6] = a.z; d[7] = a.w;
   }
   bitslice32(d);
   *reinterpret_cast<uint4*>(g.dbs[y] + off) =
-      h == 0 ? make_uint4(d[0], d[1], d[2], d[3]) : make_uint4(d[4], d[5], d[6], d[7]);
+      (hi & 1) == 0 ? make_uint4(d[0], d[1], d[2], d[3]) : make_uint4(d[4], d[5], d[6], d[7]);
+}
+
+__global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
+                                                                   int nblk) {
+  const int y = blockIdx.y;
+  const size_t hb = (size_t)nblk * 2;
+  const size_t total = (size_t)g.rows[y] * hb;  // even: a lane pair is live or done together
+  const size_t stride = (size_t)gridDim.x * 256;
+  const bool narrow = total <= 0xffffffffu;  // 32-bit index arithmetic (uniform)
+  const auto split = [&](size_t x, size_t* r, size_t* h) {
+    if (narrow) {
+      const uint32_t q = (uint32_t)x / (uint32_t)hb;
+      *r = q;
+      *h = (uint32_t)x - q * (uint32_t)hb;
+    } else {
+      *r = x / hb;
+      *h = x % hb;
+    }
+  };
+  // two half-blocks per lane per trip, both loads in flight before the stores
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += 2 * stride) {
+    const size_t j = i + stride;
+    const bool two = j < total;
+    size_t ri, hi, rj = 0, hj = 0;
+    split(i, &ri, &hi);
+    if (two) split(j, &rj, &hj);
+    const uint4 a = *reinterpret_cast<const uint4*>(g.src[y] + ri * spitch + hi * 16);
+    uint4 b = make_uint4(0u, 0u, 0u, 0u);
+    if (two) b = *reinterpret_cast<const uint4*>(g.src[y] + rj * spitch + hj * 16);
+    copy_bs_pair(g, y, ri, hi, spitch, dpitch, a);
+    if (two) copy_bs_pair(g, y, rj, hj, spitch, dpitch, b);
+  }
 }
 
 // The bodies' only home: this kernel exports the absolute address of body
@@ -839,6 +863,10 @@ bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, con
          spitch % 16 == 0 && (uintptr_t)dst % 16 == 0 && (uintptr_t)dst_bs % 16 == 0 && ncols / kBsBlock <= 0x7fffffff;
 }
 
+// copy workgroups resident per CU at most (16 of its 32 wave slots): room for
+// an elimination workgroup of 16 waves beside them
+constexpr int kCopyWgPerCu = 4;
+
 hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
                                       hipStream_t stream) {
   if (n <= 0) return hipSuccess;
@@ -851,8 +879,11 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   }
   const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
-  hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)((total + 255) / 256), (unsigned)n), dim3(256), 0,
-                     stream, g, spitch, dpitch, (int)nblk);
+  // at most kCopyWgPerCu workgroups (4 waves each) per CU over the launch
+  const size_t cap = std::max<size_t>(1, (size_t)kCopyWgPerCu * 256 / (size_t)n);
+  const size_t gx = std::min<size_t>((total + 255) / 256, cap);
+  hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream, g, spitch,
+                     dpitch, (int)nblk);
   return hipGetLastError();
 }
 
