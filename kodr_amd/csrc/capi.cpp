@@ -14,6 +14,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
+#include <future>
 #include <new>
 #include <string>
 #include <vector>
@@ -1904,15 +1906,35 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // release) instead of synchronising the stream and copying; cnt[i] = k when
 // every workgroup of decoder i is done, else 0 (kodr's route on the host).
 // A launch that never reports within 2 s is waited for on the stream once.
-int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt) {
+// on_fail(i): decoder i's workgroups have all reported and one failed (its
+// batch goes to the host whatever the others do), called once per such
+// decoder while the launch may still run
+int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt,
+                     const std::function<int(size_t)>& on_fail = nullptr) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
   const size_t nw = nc * (size_t)P;
   const auto t0 = std::chrono::steady_clock::now();
   bool synced = false;
+  std::vector<uint8_t> seen(on_fail ? nc : 0, 0);
   for (size_t i = 0;;) {
     while (i < nw && (st[i] & 0x7fffffffu) == a.epoch) i++;
     if (i == nw) break;
+    if (on_fail)  // any failed decoder reported in full?
+      for (size_t g = 0; g < nc; g++) {
+        if (seen[g]) continue;
+        bool all = true, fail = false;
+        for (int q = 0; q < P && all; q++) {
+          const uint32_t v = st[g * P + q];
+          all = (v & 0x7fffffffu) == a.epoch;
+          fail = fail || v != a.epoch;
+        }
+        if (all && fail) {
+          std::atomic_thread_fence(std::memory_order_acquire);
+          seen[g] = 1;
+          TRY(on_fail(g));
+        }
+      }
     if (!synced && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
       HIPC(hipStreamSynchronize(ctx->stream));
       synced = true;
@@ -2134,8 +2156,30 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
 #endif
     std::vector<int> cntv(nc);
     const uint8_t* tstates = hostp + hdr;  // T rows (tonly: k x k per decoder) or whole states
+    // a decoder whose launch failed (a singular panel block, or a singular C)
+    // takes kodr's route on the host from its state before the batch: started
+    // on its own thread as soon as it reports, beside the rest of the launch
+    std::vector<std::future<std::pair<int, size_t>>> early(nc);
+    auto early_host = [&](size_t i) -> int {
+      rlnc_decoder* d = ds[gpu[c0 + i]];
+      const size_t g = gpu[c0 + i];
+      if (d->core.is_decoded()) return RLNC_OK;
+      hipStream_t vs = ctx->stream;
+      TRY(ctx_aux_after_rows(ctx, &vs));
+      d->hvecs.resize(counts[g] * k);
+      HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g], pitch, k, counts[g], vs));
+      const size_t n = counts[g];
+      early[i] = std::async(std::launch::async, [d, k, n] {
+        size_t m = 0;
+        const int st = d->core.add_many(d->hvecs.data(), k, n, &m);
+        return std::make_pair(st, m);
+      });
+      return RLNC_OK;
+    };
+    // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      TRY(elim_direct_wait(ctx, a, nc, cntv.data()));
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(),
+                           side ? std::function<int(size_t)>(early_host) : std::function<int(size_t)>()));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
@@ -2190,7 +2234,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;
       size_t n = c;
-      if (c < counts[g]) {
+      if (early[i].valid()) {  // started on the host while the launch ran (got[i] = 0)
+        const auto res = early[i].get();
+        st = res.first;
+        n = res.second;
+      } else if (c < counts[g]) {
         if (d->core.is_decoded()) {
           st = RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;  // full/decoder.go:52-54
         } else {

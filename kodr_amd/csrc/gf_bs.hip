@@ -140,6 +140,8 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
 // beside the elimination kernel, whose workgroups must find free wave slots
 // even when the copies reach the CUs first (a grid of one lane per half-block
 // filled every CU, and the elimination's workgroups waited behind it).
+constexpr int kCopyUnroll = 4;
+
 __device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r, size_t hi, size_t spitch,
                                              size_t dpitch, const uint4& a) {
   const uint32_t ox = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false);
@@ -176,18 +178,26 @@ __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g,
       *h = x % hb;
     }
   };
-  // two half-blocks per lane per trip, both loads in flight before the stores
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += 2 * stride) {
-    const size_t j = i + stride;
-    const bool two = j < total;
-    size_t ri, hi, rj = 0, hj = 0;
-    split(i, &ri, &hi);
-    if (two) split(j, &rj, &hj);
-    const uint4 a = *reinterpret_cast<const uint4*>(g.src[y] + ri * spitch + hi * 16);
-    uint4 b = make_uint4(0u, 0u, 0u, 0u);
-    if (two) b = *reinterpret_cast<const uint4*>(g.src[y] + rj * spitch + hj * 16);
-    copy_bs_pair(g, y, ri, hi, spitch, dpitch, a);
-    if (two) copy_bs_pair(g, y, rj, hj, spitch, dpitch, b);
+  // kCopyUnroll half-blocks per lane per trip, every load in flight before
+  // the stores (the capped grid holds fewer loads in flight than one lane
+  // per half-block did)
+  constexpr int U = kCopyUnroll;
+  for (size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x; i0 < total; i0 += U * stride) {
+    size_t r[U], h[U];
+    uint4 a[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = i0 + u * stride;
+      r[u] = h[u] = 0;
+      a[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < total) {
+        split(i, &r[u], &h[u]);
+        a[u] = *reinterpret_cast<const uint4*>(g.src[y] + r[u] * spitch + h[u] * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (i0 + u * stride < total) copy_bs_pair(g, y, r[u], h[u], spitch, dpitch, a[u]);
   }
 }
 

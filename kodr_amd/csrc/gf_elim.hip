@@ -943,6 +943,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   __syncthreads();
 
   bool ok = true;
+  uint32_t R_out[4] = {0u, 0u, 0u, 0u};  // the finished T rows, for the device copy at the end
   if (w < 8) {
     // ================= row waves: rows 4w .. 4w + 3 =================
     const int half = w >> 2;  // 0: panel 2q's rows, 1: panel 2q + 1's
@@ -1000,6 +1001,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       uint32_t acc[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
+#pragma unroll 1  // one batch of operands live at a time (unrolled: 513 VGPRs spilled)
       for (int cq = 0; cq < 4; cq++) {
         uint32_t gw[4];  // dword cq of each row's G (wave-uniform)
 #pragma unroll
@@ -1076,7 +1078,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         const int gr = 32 * q + 4 * w + i;
         if (gr >= k) continue;
         mc_store_row(out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k), R[i], lane, k);
-        if (args.out_dev) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
+        R_out[i] = R[i];
       }
     }
   } else {
@@ -1188,6 +1190,13 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       args.counts[g * P + q] = lds.fail == 0 ? 1 : 0;
     }
   }
+  // the device copy of T after the system-scope release (as in mc4)
+  if (w < 8 && args.out_dev && lds.fail == 0)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int gr = 32 * q + 4 * w + i;
+      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R_out[i], lane, k);
+    }
 }
 
 // ---- mc4: a chain workgroup beside one row workgroup per 16-row panel ------
@@ -1599,7 +1608,6 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
       const int gr = row0 + RPW * w + i;
       if (gr >= k) continue;
       mc_store_row(out + (size_t)gr * args.out_pitch, R[i], lane, k);
-      if (args.out_dev) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
     }
   }
   __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
@@ -1609,6 +1617,15 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
     __hip_atomic_store(&args.counts[g * (NRW + 1) + x], (int)(ok ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // the device copy of T after the system-scope releases: written before
+  // them, its dirty lines made every wave's release write back L2 (mc2 with
+  // 16 decoders 280 -> 890 us); later kernels see it at the launch boundary
+  if (ok && x < NRW && args.out_dev)
+#pragma unroll
+    for (int i = 0; i < RPW; i++) {
+      const int gr = row0 + RPW * w + i;
+      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
+    }
 #undef MC4_STAMP
 }
 
