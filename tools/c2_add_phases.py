@@ -1,7 +1,9 @@
 """C2 single-decoder decode as bench.time_decode runs it (one batched
 rlnc_decoder_add_pieces call over k + 2 device wire rows, then
 rlnc_decoder_get_pieces_device), per repetition, with the AddPiece call's own
-phases when KODR_ADD_TIMING=1.  usage: python tools/c2_add_phases.py [reps]"""
+phases when KODR_ADD_TIMING=1.  usage: python tools/c2_add_phases.py [reps]
+[seed] (seed: rlnc_encoder_seed before the wire rows, as bench.py's c2_decode
+uses 7)"""
 import ctypes
 import os
 import sys
@@ -24,6 +26,8 @@ dP = ctx.alloc(k * L)
 ctx.h2d(dP, P)
 errors.check(L_.rlnc_encoder_create_device(ctx.handle, 0, dP, k, L, L, ctypes.byref(e)))
 dWire, dDec = ctx.alloc(n * W), ctx.alloc(k * L)
+if len(sys.argv) > 2:
+    L_.rlnc_encoder_seed(e, int(sys.argv[2]))
 errors.check(L_.rlnc_encoder_coded_wire_device(e, n, dWire, W))
 ctx.synchronize()
 for rep in range(int(sys.argv[1]) if len(sys.argv) > 1 else 8):

@@ -38,7 +38,7 @@ def main():
     n = k + 2
     groups = {}
     for r in csv.DictReader(open(a.trace)):
-        key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Workgroup_Size_X"]))
+        key = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Workgroup_Size_X"]))
         groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {"generations_per_step": G, "steps": ed["steps"], "warmup_steps_run": ed["warmup_steps_run"],
            "kernels": []}
