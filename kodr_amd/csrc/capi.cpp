@@ -67,8 +67,8 @@ struct DevBuf {
     HIPC(kodr_amd::DevicePool::get(dev).alloc(bytes, st, &p, &cap));
     return RLNC_OK;
   }
-  void release() {
-    if (p) kodr_amd::DevicePool::get(dev).free(p, cap, st);
+  void release(bool idle = false) {  // idle: nothing pending uses p (DevicePool::free)
+    if (p) kodr_amd::DevicePool::get(dev).free(p, cap, st, idle);
     p = nullptr;
     cap = 0;
   }
@@ -1313,14 +1313,17 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
     // waits for the stream (a query first: an idle stream costs no round trip)
     if (hipStreamQuery(d->ctx->stream) != hipSuccess) (void)hipStreamSynchronize(d->ctx->stream);
   }
-  d->recv.release();
-  d->tmat.release();
-  d->decoded.release();
-  d->rowbuf.release();
-  d->scratch.release();
-  d->recv_bs.release();
-  d->prog.release();
-  d->ptab.release();
+  // the context stream is idle here (and the side stream's copies were joined
+  // into it): the blocks go back without an event each
+  const bool idle = d->ctx != nullptr;
+  d->recv.release(idle);
+  d->tmat.release(idle);
+  d->decoded.release(idle);
+  d->rowbuf.release(idle);
+  d->scratch.release(idle);
+  d->recv_bs.release(idle);
+  d->prog.release(idle);
+  d->ptab.release(idle);
   delete d;
   return RLNC_OK;
 }

@@ -890,7 +890,8 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
   // at most kCopyWgPerCu workgroups (4 waves each) per CU over the launch
-  const size_t cap = std::max<size_t>(1, (size_t)kCopyWgPerCu * 256 / (size_t)n);
+  static const int wg_per_cu = getenv("KODR_COPY_WG_PER_CU") ? atoi(getenv("KODR_COPY_WG_PER_CU")) : kCopyWgPerCu;
+  const size_t cap = std::max<size_t>(1, (size_t)std::max(wg_per_cu, 1) * 256 / (size_t)n);
   const size_t gx = std::min<size_t>((total + 255) / 256, cap);
   hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream, g, spitch,
                      dpitch, (int)nblk);

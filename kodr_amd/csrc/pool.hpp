@@ -40,8 +40,8 @@ class DevicePool {
         free_.erase(best);
         cached_ -= b.size;
         hipError_t e = hipSuccess;
-        if (b.stream != stream) e = hipStreamWaitEvent(stream, b.ev, 0);
-        events_.push_back(b.ev);
+        if (b.ev && b.stream != stream) e = hipStreamWaitEvent(stream, b.ev, 0);
+        if (b.ev) events_.push_back(b.ev);
         if (e != hipSuccess) return e;
         *out = b.p;
         *cap = b.size;
@@ -58,10 +58,18 @@ class DevicePool {
     return e;
   }
 
-  // p (cap bytes, from alloc) is no longer needed once `stream` reaches here
-  void free(uint8_t* p, size_t cap, hipStream_t stream) {
+  // p (cap bytes, from alloc) is no longer needed once `stream` reaches here;
+  // idle: no work that uses p is pending on any stream (reusable at once, no
+  // event: a decoder's destroy frees several blocks after one stream query)
+  void free(uint8_t* p, size_t cap, hipStream_t stream, bool idle = false) {
     if (!p) return;
     std::lock_guard<std::mutex> lk(mu_);
+    if (idle) {
+      free_.push_front(Block{p, cap, stream, nullptr});
+      cached_ += cap;
+      while (cached_ > limit() && !free_.empty()) release_oldest();
+      return;
+    }
     hipEvent_t ev = nullptr;
     if (!events_.empty()) {
       ev = events_.back();
@@ -114,9 +122,9 @@ class DevicePool {
     Block b = free_.back();
     free_.pop_back();
     cached_ -= b.size;
-    (void)hipEventSynchronize(b.ev);
+    if (b.ev) (void)hipEventSynchronize(b.ev);
     (void)hipFree(b.p);
-    events_.push_back(b.ev);
+    if (b.ev) events_.push_back(b.ev);
   }
 
   std::mutex mu_;
