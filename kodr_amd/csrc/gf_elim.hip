@@ -778,6 +778,7 @@ __device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane,
 // the launch epoch, FAIL bit; bounded spins); three LDS slots per panel
 // buffer so a slot is rewritten only after both roles are two panels on.
 constexpr int kMc2Slots = 3;
+constexpr int kMc2ApplyCols = 4;  // columns per operand batch in the row apply
 constexpr int kMc2PanelGran = 16 * 64 + 64;  // granules per panel: R_p rows, then S_p
 
 struct ElimMc2Lds {
@@ -813,14 +814,16 @@ __device__ __forceinline__ void mc2_signal(int* ctr, int lane) {
 // acc ^ sum over 8 terms of (tables of m[c]) x x[c], both the tables and the
 // data read from LDS first (x: 8 dwords at stride `xs` from `xp`), then the
 // arithmetic (selectors computed after the reads)
-__device__ __forceinline__ uint32_t mc3_dot8x(const uint4* tab, uint32_t acc, const uint32_t* m, const uint32_t* xp,
+// (m: the 8 multipliers packed 4 per dword, mw[0..1])
+__device__ __forceinline__ uint32_t mc3_dot8x(const uint4* tab, uint32_t acc, const uint32_t* mw, const uint32_t* xp,
                                               int xs) {
   uint4 tt[8];
   uint32_t t2[8], x[8];
 #pragma unroll
   for (int c = 0; c < 8; c++) {
-    tt[c] = tab[2 * m[c]];
-    t2[c] = tab[2 * m[c] + 1].x;
+    const uint32_t m = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
+    tt[c] = tab[2 * m];
+    t2[c] = tab[2 * m + 1].x;
     x[c] = xp[c * xs];
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -835,20 +838,16 @@ __device__ __forceinline__ uint32_t mc3_block_update_c(const uint4* tab, uint32_
                                                        const uint32_t (*sp)[4], const uint32_t (*rp)[64], int col0,
                                                        int lane) {
   const int d = lane & 3;
-  uint32_t mw[4], m[16];
+  uint32_t mw[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) mw[q] = mrow[q];
-#pragma unroll
-  for (int c = 0; c < 16; c++) m[c] = (mw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-  uint32_t F = mc3_dot8x(tab, 0u, m, &sp[0][d], 4);
-  F = mc3_dot8x(tab, F, m + 8, &sp[8][d], 4);
+  uint32_t F = mc3_dot8x(tab, 0u, mw, &sp[0][d], 4);
+  F = mc3_dot8x(tab, F, mw + 2, &sp[8][d], 4);
   uint32_t fw[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) fw[q] = quad_bcast(F, q);
-#pragma unroll
-  for (int c = 0; c < 16; c++) m[c] = (fw[c >> 2] >> (8 * (c & 3))) & 0xffu;
-  const uint32_t acc = mc3_dot8x(tab, blk, m, &rp[0][col0 + d], 64);
-  return mc3_dot8x(tab, acc, m + 8, &rp[8][col0 + d], 64);
+  const uint32_t acc = mc3_dot8x(tab, blk, fw, &rp[0][col0 + d], 64);
+  return mc3_dot8x(tab, acc, fw + 2, &rp[8][col0 + d], 64);
 }
 
 // The circular-form inversion ((t, d) layout as mc3_gj_circ), branch-free:
@@ -1001,19 +1000,25 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       uint32_t acc[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
-#pragma unroll 1  // one batch of operands live at a time (unrolled: 513 VGPRs spilled)
-      for (int cq = 0; cq < 4; cq++) {
-        uint32_t gw[4];  // dword cq of each row's G (wave-uniform)
+      // kMc2ApplyCols columns per batch, one batch live at a time (the whole
+      // loop unrolled spilled 513 VGPRs).  The kernel holds ~113 VGPRs, all of
+      // a SIMD's file at 4 waves, so the row copies launched beside it cannot
+      // share its CUs; capped at 96 (waves_per_eu 5, a few bytes spilled) with
+      // the copies at 2 loads per lane, the round trip measured slower (238-241
+      // against 230-235 us per generation, profiles/r04/var_ab/)
+#pragma unroll 1
+      for (int cb = 0; cb < 16; cb += kMc2ApplyCols) {
+        uint32_t gw[4];  // the bytes of columns cb .. of each row's G (wave-uniform)
 #pragma unroll
-        for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
-        // the 16 (uniform) table reads and 4 data reads of these columns
-        // first, then the arithmetic: one LDS round trip per 4 columns
-        // (sinking each read next to its use cost one round trip per term)
-        uint4 tt[4][4];
-        uint32_t t2[4][4], xs[4];
+        for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cb >> 2]) >> (8 * (cb & 3));
+        // the (uniform) table reads and the data reads of these columns
+        // first, then the arithmetic: one LDS round trip per batch (sinking
+        // each read next to its use cost one round trip per term)
+        uint4 tt[kMc2ApplyCols][4];
+        uint32_t t2[kMc2ApplyCols][4], xs[kMc2ApplyCols];
 #pragma unroll
-        for (int cc = 0; cc < 4; cc++) {
-          xs[cc] = lds.rp[slot][4 * cq + cc][lane];
+        for (int cc = 0; cc < kMc2ApplyCols; cc++) {
+          xs[cc] = lds.rp[slot][cb + cc][lane];
 #pragma unroll
           for (int i = 0; i < 4; i++) {
             const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
@@ -1023,7 +1028,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int cc = 0; cc < 4; cc++) {
+        for (int cc = 0; cc < kMc2ApplyCols; cc++) {
           const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
 #pragma unroll
           for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
