@@ -1004,8 +1004,9 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
       // loop unrolled spilled 513 VGPRs).  The kernel holds ~113 VGPRs, all of
       // a SIMD's file at 4 waves, so the row copies launched beside it cannot
       // share its CUs; capped at 96 (waves_per_eu 5, a few bytes spilled) with
-      // the copies at 2 loads per lane, the round trip measured slower (238-241
-      // against 230-235 us per generation, profiles/r04/var_ab/)
+      // the copies at 2 or 4 loads per lane, the round trip measured slower
+      // (238-241 against 230-235, 235-236 against 228-230 us per generation,
+      // profiles/r04/var_ab/)
 #pragma unroll 1
       for (int cb = 0; cb < 16; cb += kMc2ApplyCols) {
         uint32_t gw[4];  // the bytes of columns cb .. of each row's G (wave-uniform)
