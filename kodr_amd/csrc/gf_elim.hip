@@ -1132,27 +1132,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         const gu64* src = base + (size_t)(2 * cw) * 64 + lane;
         uint64_t a = 0, b = 0, s = 0;
         bool seen_fail = false, timeout = false;
-        // one lane watches one granule (S's first, or its first R row's) and
-        // the wave reads everything once that is tagged: a whole-wave poll of
-        // every granule put ~1 TB/s of agent-scope loads on the fabric with 16
-        // decoders and slowed the row copies beside the launch
-        const gu64* const watch = cw == 0 ? base + 16 * 64 : base + (size_t)(2 * cw) * 64;
         for (int spins = 0;; spins++) {
-          uint64_t wv = 0;
-          if (lane == 0) wv = __hip_atomic_load(watch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t wtag = __builtin_amdgcn_readfirstlane((uint32_t)(wv >> 32));
-          if ((wtag & ~kMcFail) != epoch) {
-            if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-              seen_fail = true;
-              break;
-            }
-            if (spins > kMcSpinMax) {
-              timeout = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-          }
           a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (cw == 0) s = __hip_atomic_load(base + 16 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
