@@ -2535,6 +2535,25 @@ int rlnc_decoder_get_pieces_device(rlnc_decoder* d, uint8_t* d_out, size_t out_p
   const size_t rows = d->core.rank(), recv = d->core.received();
   d->hT.resize(std::max<size_t>(rows * recv, 1));
   d->core.copy_transform(d->hT.data(), recv);
+  // T where the GPU elimination left it (k x k on the device, this decoder's
+  // batch the last one through the context's buffer): no upload, whose DMA
+  // latency (15-20 us) sits in the stream ahead of the product.  Only without
+  // unit rows, which the host route copies instead of multiplying.
+  if (d->tdev && d->tdev_seq == d->ctx->tdev_seq && rows == recv && recv == d->core.piece_count()) {
+    bool unit = false;
+    for (size_t r = 0; r < rows && !unit; r++) {
+      const uint8_t* t = d->hT.data() + r * recv;
+      size_t nz = 0, last = 0;
+      for (size_t j = 0; j < recv && nz < 2; j++)
+        if (t[j]) nz++, last = j;
+      unit = nz == 1 && t[last] == 1;
+    }
+    if (!unit) {
+      d->last_gf_rows = rows;
+      d->last_copy_rows = 0;
+      return dec_gemm(d, d->tdev, rows, d_out, out_pitch);
+    }
+  }
   return dec_apply(d, rows, d->hT.data(), d_out, out_pitch);  // T is staged; no host buffer outlives the call
 }
 
