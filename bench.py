@@ -38,17 +38,17 @@ class host_elimination:
     """The comparisons' host legs run kodr's elimination on the host:
     rlnc_decoder_add_pieces and the lazy AddPiece flush would otherwise take
     the GPU elimination themselves for large full batches (capi.cpp
-    dec_route_gpu, KODR_ROUTE_MIN_K read per call)."""
+    dec_route_gpu, the context's rlnc_ctx_set_route_min_k)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
 
     def __enter__(self):
-        self.prev = os.environ.get("KODR_ROUTE_MIN_K")
-        os.environ["KODR_ROUTE_MIN_K"] = "100000"
+        self.prev = self.ctx.route_min_k
+        self.ctx.set_route_min_k(100000)
 
     def __exit__(self, *exc):
-        if self.prev is None:
-            os.environ.pop("KODR_ROUTE_MIN_K", None)
-        else:
-            os.environ["KODR_ROUTE_MIN_K"] = self.prev
+        self.ctx.set_route_min_k(self.prev)
 
 
 def setbytes(k, L, padding=0):
@@ -438,7 +438,7 @@ def roundtrip_kernels(rt, k, L):
                             "hbm_bytes": G * 2 * k * L},
         "issue_peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
         "note": "issue_frac against the one bit-sliced VALU floor (ISSUE_PER_S x MACS_PER_INST_BS); kernel durations "
-                "of the same command under rocprofv3 in profiles/r04/roundtrip/"}
+                "of the same command under rocprofv3 in profiles/r05/"}
 
 
 def main():
@@ -506,6 +506,30 @@ def main():
             dist.barrier()
         ctx.synchronize()
 
+    extras = {"construct_ms_per_generation": round(construct_ms, 3)}
+    # ---- value: the metric's encode + decode round trip (configs[1] encode +
+    # configs[2] decode) over the G resident generations: W warmup + K timed
+    # steps between barriers, max over ranks
+    # (--no-encode-decode: the encode leg alone, for the PMC passes of tools/)
+    ed = None
+    if not args.no_encode_decode:
+        elim0 = ctx.elim_stats()
+        rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng)
+        t_rt, n_warm_rt = run_timed(rt.step, args.steps, args.warmup, barrier, WARM_S)
+        elim1 = ctx.elim_stats()
+        ed = roundtrip_block(t_rt, args.steps, args.warmup, n_warm_rt, rt.units(), world, kdist, device="cuda")
+        ed["us_per_generation"] = round(ed["ms_per_step"] / G * 1e3, 2)
+        ed["payload_MBps"] = round(world * args.steps * G * k * L / (ed["ms_per_step"] * args.steps / 1e3) / 1e6, 1)
+        ed["wall_s"] = round(t_rt, 4)
+        legs = roundtrip_kernels(rt, k, L)
+        rt_ok = rt.decoded_ok()
+        rt_n = rt.n
+        # the elimination routes of every decoder of the warmup and timed steps
+        # (rlnc_ctx_elim_stats): host_after_gpu counts the launches that left a
+        # batch to kodr's algorithm on the host
+        elim_routes = {key: elim1[key] - elim0[key] for key in elim0}
+        rt.close()
+
     # W warmup steps, but never fewer than one pass over the G generations (no
     # generation is first touched inside the timed region) and never less than
     # WARM_S of back-to-back work: after a load step the MI355X's clocks dip
@@ -549,29 +573,7 @@ def main():
     macs = per_step * B * k * L
     bs = plan["kernel"] == 2
 
-    extras = {"construct_ms_per_generation": round(construct_ms, 3)}
-    ed = None
-    if not args.no_encode_decode:
-        # the metric's encode+decode round trip under the same protocol: every
-        # rank, W warmup + K timed steps, barriers, max over ranks
-        try:
-            rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng)
-            t_rt, n_warm_rt = run_timed(rt.step, args.steps, args.warmup, barrier, WARM_S)
-            ed = roundtrip_block(t_rt, args.steps, args.warmup, n_warm_rt, rt.units(), world, kdist, device="cuda")
-            ed["workload"] = (f"a step = {G} resident 32 MiB/256 generations x (k + 2 = {k + 2} coded pieces in one "
-                              "grouped encode launch, a fresh decoder each fed them in one batched AddPiece call "
-                              "(GPU elimination), one grouped GetPieces), device-resident; value in kodr units: "
-                              "(k + 2) x SetBytes + DecodableLen per generation")
-            ed["generations_per_step"] = G
-            ed["us_per_generation"] = round(ed["ms_per_step"] / G * 1e3, 2)
-            ed["payload_MBps"] = round(world * args.steps * G * k * L / (ed["ms_per_step"] * args.steps / 1e3) / 1e6, 1)
-            ed["legs"] = roundtrip_kernels(rt, k, L)
-            ed["roundtrip_ok"] = rt.decoded_ok()
-            if cpu is not None and cpu_dec is not None:
-                ed["cpu_baseline"] = cpu_baseline_roundtrip(cpu, cpu_dec)
-            rt.close()
-        except Exception as e:  # secondary block: never lose the headline line
-            ed = {"error": repr(e)[:300]}
+
     if not args.no_extras and rank == 0:
         extras.update(run_extras(ctx, L_, errors, encs, dV, dOut, B, k, L, rng))
     if world > 1 and not args.no_extras:
@@ -584,56 +586,89 @@ def main():
 
     hs.close()
 
-    if rank == 0:
+    if rank == 0 and ed is None:  # tools/ PMC passes: the encode leg alone
+        print(json.dumps({"metric": "encode leg only (--no-encode-decode)", "value": round(value, 1),
+                          "ms_per_step": round(t_max / args.steps * 1e3, 5), "plan": plan,
+                          "avg_launch_us": round(t_launch * 1e6, 3)}), flush=True)
+    elif rank == 0:
+        enc_macs = G * rt_n * k * L
+        te = legs["encode_launch"]["avg_us"] / 1e6
         line = {
             "metric": "coded MB/s device-resident, Full-RLNC encode+decode, 32M/256 pieces @1/2/4/8 GPU",
-            "value": round(value, 1),
+            "value": ed["value"],
             "unit": "MB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(t_max / args.steps * 1e3, 5),
+            "ms_per_step": ed["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded uniform random bytes and coding vectors)",
-            "config": {"workload": "Full RLNC ENCODE leg of the metric, 32 MiB generation / 256 pieces (BASELINE "
-                                   "configs[1]); "
-                                   + (f"a step = {B} coded pieces of each of the {G} resident generations in one "
-                                      "grouped launch" if grouped else
-                                      f"a step = {B} coded pieces of one generation (rotating over {G})")
-                                   + "; value counts encode only (configs[1]). The metric's encode+decode round "
-                                     "trip (configs[1] + configs[2]) is the top-level encode_decode block, timed "
-                                     "under the same protocol (steps, warmup, barriers, max over ranks)",
-                       "value_covers": "encode", "encode_decode_in": "encode_decode",
-                       "piece_count": k, "piece_size": L, "coded_pieces_per_generation_per_step": B,
-                       "generations_per_step": per_step, "coded_pieces_per_step": per_step * B,
-                       "resident_generations": G, "parallelism": f"generation-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(B, k, L, per_step),
-                         "kernel": kernel_name(plan),
-                         "plan": plan,
-                         "traffic_source": pmc_traffic_file(B, k, L, per_step),
-                         "hbm_bytes_per_launch": compulsory,
-                         "avg_launch_us": round(t_launch * 1e6, 3),
-                         "warmup_launches": n_warm, "generations_per_launch": per_step,
-                         "issue": {"achieved_gf_macs_per_s": float(f"{macs / t_launch:.4g}"),
-                                   "peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
-                                   "frac": round(macs / t_launch / VALU_FLOOR_MACS_PER_S, 4) if bs else None,
-                                   "gf_macs_per_launch": macs},
-                         "kodr_setbytes_per_launch": algo_bytes,
-                         "note": "achieved/frac: the launch's compulsory HBM bytes (per generation: the generation "
-                                 "once + B vectors + B pieces) / launch time / 8 TB/s; traffic: PMC-measured HBM "
-                                 "bytes per launch "
-                                 "(profiles/, FETCH_SIZE x2 + WRITE_SIZE); issue: GF MACs/s against the "
-                                 "bit-sliced method's VALU floor (8 XOR3 + 26/8 table instructions per "
-                                 "coefficient per 2 KiB at 2.3 cycles per wave instruction on 1024 SIMDs), "
-                                 "the bound that binds at B >= 9 (DESIGN.md Roofline)"},
-            "cpu_baseline": cpu,
-            "encode_decode": ed,
-            "wall_s": round(wall, 4),
+            "config": {"workload": (f"Full RLNC encode+decode round trip, 32 MiB generations / 256 pieces (BASELINE "
+                                    f"configs[1] encode + configs[2] decode), device-resident: a step = {G} resident "
+                                    f"generations x (k + 2 = {k + 2} coded pieces in one grouped encode launch, a "
+                                    "fresh decoder each fed them in one batched AddPiece call (GPU elimination), one "
+                                    "grouped GetPieces); value in kodr units: (k + 2) x SetBytes (encoder bench) + "
+                                    "DecodableLen (decoder bench) per generation"),
+                       "value_covers": "encode+decode",
+                       "piece_count": k, "piece_size": L, "generations_per_step": G,
+                       "coded_pieces_per_generation_per_step": k + 2, "resident_generations": G,
+                       "parallelism": f"generation-sharded x{world}"},
+            "roofline": {"bound": "valu", "achieved": float(f"{enc_macs / te:.4g}"),
+                         "peak": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"), "unit": "GF-MAC/s",
+                         "frac": round(enc_macs / te / VALU_FLOOR_MACS_PER_S, 4),
+                         "traffic": pmc_traffic(k + 2, k, L, G),
+                         "traffic_source": pmc_traffic_file(k + 2, k, L, G),
+                         "kernel": "gf_bs_kernel",
+                         "legs": legs,
+                         "hbm": {"achieved_GBps": round(legs["encode_launch"]["hbm_bytes"] / te / 1e9, 1),
+                                 "peak_GBps": HBM_PEAK_GBS, "frac": legs["encode_launch"]["hbm_frac"]},
+                         "note": "the round trip's dominant kernel is gf_bs_kernel (the grouped encode launch, k + 2 "
+                                 "pieces of 16 generations, and the grouped GetPieces, together ~85 % of a step): "
+                                 "258 GF MACs per generation byte read, so neither HBM (hbm.frac) nor MFMA (a "
+                                 "byte-field product) bounds it; SURVEY 8(d) prices decode against the VALU ceiling. "
+                                 "achieved/frac: the encode leg's GF MACs per second (HIP events around the launch) "
+                                 "against the bit-sliced method's VALU issue floor; legs: each leg's own fractions"},
+            "cpu_baseline": (cpu_baseline_roundtrip(cpu, cpu_dec) if cpu is not None and cpu_dec is not None
+                             else None),
+            "roundtrip": {"us_per_generation": ed["us_per_generation"], "payload_MBps": ed["payload_MBps"],
+                          "warmup_steps_run": ed["warmup_steps_run"],
+                          "units_per_step_per_rank": ed["units_per_step_per_rank"],
+                          "roundtrip_ok": rt_ok, "elimination_routes": elim_routes},
+            "encode": {
+                "value": round(value, 1), "unit": "MB/s", "ms_per_step": round(t_max / args.steps * 1e3, 5),
+                "workload": ("Full RLNC encode (BASELINE configs[1]), 32 MiB generation / 256 pieces; "
+                             + (f"a step = {B} coded pieces of each of the {G} resident generations in one grouped "
+                                "launch" if grouped else
+                                f"a step = {B} coded pieces of one generation (rotating over {G})")
+                             + "; kodr units: SetBytes per coded piece; same protocol (steps, warmup, barriers, "
+                               "max over ranks)"),
+                "coded_pieces_per_generation_per_step": B, "generations_per_step": per_step,
+                "coded_pieces_per_step": per_step * B,
+                "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "traffic": pmc_traffic(B, k, L, per_step),
+                             "kernel": kernel_name(plan),
+                             "plan": plan,
+                             "traffic_source": pmc_traffic_file(B, k, L, per_step),
+                             "hbm_bytes_per_launch": compulsory,
+                             "avg_launch_us": round(t_launch * 1e6, 3),
+                             "warmup_launches": n_warm, "generations_per_launch": per_step,
+                             "issue": {"achieved_gf_macs_per_s": float(f"{macs / t_launch:.4g}"),
+                                       "peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
+                                       "frac": round(macs / t_launch / VALU_FLOOR_MACS_PER_S, 4) if bs else None,
+                                       "gf_macs_per_launch": macs},
+                             "kodr_setbytes_per_launch": algo_bytes,
+                             "note": "achieved/frac: the launch's compulsory HBM bytes (per generation: the "
+                                     "generation once + B vectors + B pieces) / launch time / 8 TB/s; traffic: "
+                                     "PMC-measured HBM bytes per launch (profiles/, FETCH_SIZE x2 + WRITE_SIZE); "
+                                     "issue: GF MACs/s against the bit-sliced method's VALU floor"},
+                "cpu_baseline": cpu,
+                "wall_s": round(wall, 4),
+            },
+            "wall_s": ed["wall_s"],
         }
         if extras:
             line["extras"] = extras
@@ -1205,7 +1240,7 @@ def batched_elim(ctx, L_, errors, rng, k=256, G=32, L=256, reps=3):
             ctx.synchronize()
             t0 = time.perf_counter()
             if mode == "host":
-                with host_elimination():
+                with host_elimination(ctx):
                     for g in range(G):
                         c = ctypes.c_size_t()
                         st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g], n, pitch, L, 1, ctypes.byref(c))
@@ -1271,7 +1306,7 @@ def piecewise_grouped(ctx, L_, errors, encs, k, L, reps=2):
             if mode == "gpu":
                 errors.check(L_.rlnc_decoders_flush_gpu(darr, G))
             else:
-                with host_elimination():
+                with host_elimination(ctx):
                     for h in decs:
                         L_.rlnc_decoder_is_decoded(h)
             t2 = time.perf_counter()
@@ -1343,7 +1378,7 @@ def batched_elim_rounds(ctx, L_, errors, rng, k=256, G=32, L=256, rounds=4, reps
                 t0 = time.perf_counter()
                 cnt = cuts[r + 1] - cuts[r]
                 if mode == "host":
-                    with host_elimination():
+                    with host_elimination(ctx):
                         for g in range(G):
                             c = ctypes.c_size_t()
                             st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g] + cuts[r] * pitch, cnt, pitch, L, 1,

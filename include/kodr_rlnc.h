@@ -69,6 +69,14 @@ int rlnc_ctx_create(int device, void* stream, rlnc_ctx** out);
 int rlnc_ctx_destroy(rlnc_ctx* ctx);
 int rlnc_ctx_synchronize(rlnc_ctx* ctx);
 void* rlnc_ctx_stream(rlnc_ctx* ctx);            /* the hipStream_t in use */
+/* A single decoder's full batch (rlnc_decoder_add_pieces, the lazy AddPiece
+ * flush) takes the GPU elimination from piece count min_k on (default 224,
+ * where it measured at least as fast as the host's); a larger value keeps
+ * every such batch on the host (kodr's algorithm, the same state). */
+int rlnc_ctx_set_route_min_k(rlnc_ctx* ctx, size_t min_k);
+/* rlnc_decoder_elim_stats summed over every decoder of the context so far */
+int rlnc_ctx_elim_stats(const rlnc_ctx* ctx, size_t* gpu, size_t* gpu_retried, size_t* host_after_gpu,
+                        size_t* host);
 int rlnc_random_bytes(uint8_t* out, size_t n);   /* getrandom(2): crypto/rand stand-in */
 
 /* The engine's own device buffers (generations, received rows, twins) come
@@ -357,6 +365,14 @@ int rlnc_decoder_apply_stats(const rlnc_decoder* dec, size_t* gf_rows, size_t* c
 /* 1 if the last materialization's GF product ran on the bit-sliced kernel
  * (gf_bs_kernel), 0 for the v_perm kernel or no GF rows (diagnostics) */
 int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* dec);
+/* which route eliminated the decoder's batches so far: gpu = states the GPU
+ * elimination produced (gpu_retried of them after a permuted re-attempt:
+ * a singular panel block, gf_elim.hip), host_after_gpu = GPU launches that
+ * failed (a singular C, a structured batch) and left the batch to kodr's
+ * algorithm on the host, host = host eliminations without a GPU launch.
+ * Any pointer may be NULL. */
+int rlnc_decoder_elim_stats(const rlnc_decoder* dec, size_t* gpu, size_t* gpu_retried, size_t* host_after_gpu,
+                            size_t* host);
 int rlnc_decoder_transform(const rlnc_decoder* dec, uint8_t* out);
 
 /* ---- progressive decode (an extension) ---------------------- */

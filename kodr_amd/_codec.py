@@ -256,6 +256,18 @@ class _Decoder:
         """Decoded pieces land at row j of the device buffer d_out (None unbinds)."""
         errors.check(lib().rlnc_decoder_bind_output(self._h, None if d_out is None else ctypes.c_void_p(d_out), pitch))
 
+    def elim_stats(self):
+        """Which route eliminated this decoder's batches (rlnc_decoder_elim_stats)."""
+        return elim_stats(self._h)
+
+
+def elim_stats(h):
+    """rlnc_decoder_elim_stats of a decoder handle as a dict: gpu, gpu_retried,
+    host_after_gpu, host."""
+    v = [ctypes.c_size_t() for _ in range(4)]
+    errors.check(lib().rlnc_decoder_elim_stats(h, *[ctypes.byref(x) for x in v]))
+    return dict(zip(("gpu", "gpu_retried", "host_after_gpu", "host"), (x.value for x in v)))
+
 
 def flush_decoders(decoders):
     """Extension (no kodr counterpart): the pending AddPiece calls of many

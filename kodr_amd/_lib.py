@@ -28,6 +28,8 @@ SIGNATURES = {
     "rlnc_ctx_destroy": (_int, [_vp]),
     "rlnc_ctx_synchronize": (_int, [_vp]),
     "rlnc_ctx_stream": (_vp, [_vp]),
+    "rlnc_ctx_set_route_min_k": (_int, [_vp, _sz]),
+    "rlnc_ctx_elim_stats": (_int, [_vp, _szp, _szp, _szp, _szp]),
     "rlnc_random_bytes": (_int, [_u8p, _sz]),
     "rlnc_device_pool_trim": (_int, [_int, _sz]),
     "rlnc_device_pool_cached": (_sz, [_int]),
@@ -102,6 +104,7 @@ SIGNATURES = {
     "rlnc_decoder_coefficients": (_int, [_vp, _u8p]),
     "rlnc_decoder_apply_stats": (_int, [_vp, _szp, _szp]),
     "rlnc_decoder_last_apply_bitsliced": (_int, [_vp]),
+    "rlnc_decoder_elim_stats": (_int, [_vp, _szp, _szp, _szp, _szp]),
     "rlnc_decoder_transform": (_int, [_vp, _u8p]),
     "rlnc_gf_matmul_device": (_int, [_vp, _vp, _sz, _sz, _sz, _vp, _sz, _vp, _sz, _sz]),
     "rlnc_bitslice_device": (_int, [_vp, _vp, _sz, _sz, _sz]),

@@ -7,6 +7,7 @@
 // is no CPU compute fallback: without a usable HIP device every data call
 // fails with RLNC_ERR_NO_DEVICE / RLNC_ERR_HIP.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/random.h>
@@ -18,6 +19,7 @@
 #include <future>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/kodr_rlnc.h"
@@ -27,6 +29,7 @@
 #include "gf_kernels.hpp"
 #include "pool.hpp"
 #include "staging.hpp"
+#include "tune.hpp"
 
 using kodr_amd::DecoderCore;
 using kodr_amd::HostPool;
@@ -109,7 +112,10 @@ struct rlnc_ctx {
   uint8_t* elim_pin_dev = nullptr;  // ... as the device sees it
   size_t elim_pin_cap = 0;
   DevBuf elim_pub;           // gf_elim_mc's hand-off granules (zeroed when allocated)
-  uint32_t elim_epoch = 0;   // gf_elim_mc's launch tag, one per launch
+  uint32_t elim_epoch = 0;   // gf_elim_mc's last tag used: a launch takes the next gf_elim_mc_attempts()
+  size_t route_min_k = 224;  // single decoders take the GPU elimination from this k (rlnc_ctx_set_route_min_k)
+  // rlnc_decoder_elim_stats summed over the context's decoders (rlnc_ctx_elim_stats)
+  std::atomic<size_t> n_elim_gpu{0}, n_elim_gpu_retried{0}, n_elim_host_after_gpu{0}, n_elim_host{0};
   DevBuf elim_tdev;          // fresh decoders' T rows (k x k each) as the last batched GPU AddPiece left them
   uint64_t tdev_seq = 0;     // ... one number per such call
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
@@ -194,6 +200,10 @@ struct rlnc_decoder {
   std::vector<const uint8_t*> pend_src;  // queued device pieces (borrowed), arrival order
   size_t pend_row0 = 0;                  // received index of pend_src[0]
   DevBuf ptab;                           // the gather's source-row table
+  // which route eliminated this decoder's batches (rlnc_decoder_elim_stats)
+  size_t elim_gpu = 0, elim_gpu_retried = 0, elim_host_after_gpu = 0, elim_host = 0;
+  bool gpu_rejected = false;  // the GPU elimination failed on the queue as it is: the host takes it
+  int sticky = RLNC_OK;       // a HIP failure inside a state accessor, reported by the next call that can
   explicit rlnc_decoder(size_t k) : core(k) {}
 };
 
@@ -525,6 +535,22 @@ int rlnc_ctx_synchronize(rlnc_ctx* ctx) {
 
 void* rlnc_ctx_stream(rlnc_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+int rlnc_ctx_elim_stats(const rlnc_ctx* ctx, size_t* gpu, size_t* gpu_retried, size_t* host_after_gpu,
+                        size_t* host) {
+  if (!ctx) return RLNC_ERR_INVALID_ARGUMENT;
+  if (gpu) *gpu = ctx->n_elim_gpu;
+  if (gpu_retried) *gpu_retried = ctx->n_elim_gpu_retried;
+  if (host_after_gpu) *host_after_gpu = ctx->n_elim_host_after_gpu;
+  if (host) *host = ctx->n_elim_host;
+  return RLNC_OK;
+}
+
+int rlnc_ctx_set_route_min_k(rlnc_ctx* ctx, size_t min_k) {
+  if (!ctx) return RLNC_ERR_INVALID_ARGUMENT;
+  ctx->route_min_k = min_k;
+  return RLNC_OK;
+}
+
 int rlnc_random_bytes(uint8_t* out, size_t n) {
   size_t got = 0;
   while (got < n) {
@@ -798,7 +824,7 @@ int rlnc_encoder_compact(rlnc_encoder* e) {
 // pieces per generation (see rlnc_encoder_group_coded_pieces_device)
 constexpr size_t kGroupBsMinRows = 5;
 static size_t group_bs_min() {
-  static const size_t v = getenv("KODR_GROUP_BS_MIN") ? (size_t)atol(getenv("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
+  static const size_t v = kodr_amd::tune_env("KODR_GROUP_BS_MIN") ? (size_t)atol(kodr_amd::tune_env("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
   return v;
 }
 
@@ -1028,7 +1054,7 @@ int rec_build_piece_twin(rlnc_recoder* r) {
 }
 
 bool rec_side_enabled() {
-  static const bool v = getenv("KODR_REC_SIDE") ? atoi(getenv("KODR_REC_SIDE")) != 0 : true;
+  static const bool v = kodr_amd::tune_env("KODR_REC_SIDE") ? atoi(kodr_amd::tune_env("KODR_REC_SIDE")) != 0 : true;
   return v;
 }
 
@@ -1299,7 +1325,7 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
   if (ctx)
     for (DevBuf* b : {&d->recv, &d->recv_bs, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch, &d->ptab})
       b->bind(ctx->device, ctx->stream);
-  static const bool lazy = !getenv("KODR_DEC_LAZY") || atoi(getenv("KODR_DEC_LAZY")) != 0;  // A/B knob
+  static const bool lazy = !kodr_amd::tune_env("KODR_DEC_LAZY") || atoi(kodr_amd::tune_env("KODR_DEC_LAZY")) != 0;  // A/B knob
   d->lazy = lazy;
   *out = d;
   return RLNC_OK;
@@ -1380,18 +1406,40 @@ template <class F>
 int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read);
 }
 
+// a batch's elimination route, on the decoder and its context
+enum ElimRoute { kElimGpu, kElimGpuRetried, kElimHostAfterGpu, kElimHost };
+void count_elim(rlnc_decoder* d, ElimRoute r) {
+  rlnc_ctx* c = d->ctx;
+  switch (r) {
+    case kElimGpuRetried:
+      d->elim_gpu_retried++;
+      if (c) c->n_elim_gpu_retried++;
+      [[fallthrough]];
+    case kElimGpu:
+      d->elim_gpu++;
+      if (c) c->n_elim_gpu++;
+      break;
+    case kElimHostAfterGpu:
+      d->elim_host_after_gpu++;
+      if (c) c->n_elim_host_after_gpu++;
+      break;
+    case kElimHost:
+      d->elim_host++;
+      if (c) c->n_elim_host++;
+      break;
+  }
+}
+
 // One decoder's elimination goes to the GPU (gf_elim_mc4: a chain workgroup
 // beside row workgroups) instead of the host when its n new rows complete the
 // rank of a state of kept rows (fresh or continued: the full-batch case) and
-// k is at least KODR_ROUTE_MIN_K (default kRouteMinK, from where the GPU
+// k is at least the context's route_min_k (default 224, from where the GPU
 // route measured at least as fast as the host's: 87 against 86 us at k = 224,
-// 92-96 against 104-107 us at k = 256, profiles/r04/elim_modes/).
-constexpr size_t kRouteMinK = 224;
+// 92-96 against 104-107 us at k = 256, profiles/r04/elim_modes/;
+// rlnc_ctx_set_route_min_k).
 bool dec_route_gpu(const rlnc_decoder* d, size_t n) {
-  const char* e = getenv("KODR_ROUTE_MIN_K");  // read per call: tests switch it to keep host references
-  const size_t min_k = e ? (size_t)atol(e) : kRouteMinK;
   const size_t k = d->core.piece_count(), r = d->core.received();
-  return d->ctx && k >= min_k && k <= 256 && n >= 2 && d->core.rank() == r && r + n >= k &&
+  return d->ctx && k >= d->ctx->route_min_k && k <= 256 && n >= 2 && d->core.rank() == r && r + n >= k &&
          kodr_amd::gf_elim_mc_enabled();
 }
 
@@ -1415,16 +1463,29 @@ bool queue_looks_systematic(const rlnc_decoder* d) {
   return false;
 }
 
+// (a queue the GPU already failed on -- a singular C -- goes straight to the
+// host; a HIP error on the way is kept for the decoder's next call that
+// returns a status, since the accessors that flush return none)
 void dec_flush_coef(rlnc_decoder* d) {
   if (!d->npend) return;
-  if (dec_route_gpu(d, d->npend) && !queue_looks_systematic(d)) {
+  if (!d->gpu_rejected && dec_route_gpu(d, d->npend) && !queue_looks_systematic(d)) {
     rlnc_decoder* one = d;
-    (void)dec_elim_queues_gpu(&one, 1, [] { return RLNC_OK; });
+    if (const int e = dec_elim_queues_gpu(&one, 1, [] { return RLNC_OK; }))
+      if (d->sticky == RLNC_OK) d->sticky = e;
     if (!d->npend) return;
   }
   size_t used = 0;
   (void)d->core.add_many(d->pend_v.data(), d->core.piece_count(), d->npend, &used);
+  count_elim(d, kElimHost);
   d->npend = 0;
+  d->gpu_rejected = false;
+}
+
+// the HIP failure an accessor's flush met, once
+int dec_take_sticky(rlnc_decoder* d) {
+  const int e = d->sticky;
+  d->sticky = RLNC_OK;
+  return e;
 }
 
 // the queued device pieces into their received rows: one gather launch
@@ -1445,6 +1506,7 @@ int dec_flush_data(rlnc_decoder* d) {
 // everything queued: the state and the received rows are kodr's
 int dec_flush(rlnc_decoder* d) {
   dec_flush_coef(d);
+  TRY(dec_take_sticky(d));
   if (d->ctx && !d->pend_src.empty()) {
     TRY(set_dev(d->ctx));
     TRY(dec_flush_data(d));
@@ -1461,6 +1523,7 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   const size_t k = d->core.piece_count();
   // the queue could complete the rank: observe the state (full/decoder.go:52-54)
   if (d->npend && d->core.useful() + d->npend >= k) dec_flush_coef(d);
+  TRY(dec_take_sticky(d));
   if (d->core.is_decoded()) return RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;
   if (!vec) return RLNC_ERR_INVALID_ARGUMENT;
   TRY(dec_check(d, vlen, piece, plen));
@@ -1470,6 +1533,7 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
     d->pend_v.resize((d->npend + 1) * k);
     memcpy(d->pend_v.data() + d->npend * k, vec, k);
     d->npend++;
+    d->gpu_rejected = false;  // a new queue
     if (!d->ctx) return RLNC_OK;
     if (dev && borrow && (uintptr_t)piece % 16 == 0) {  // borrowed until the next data flush
       if (d->pend_src.empty()) d->pend_row0 = row;
@@ -1482,6 +1546,7 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
   }
   TRY(dec_flush(d));
   TRY(d->core.add(vec));
+  count_elim(d, kElimHost);
   TRY(dec_store_pieces(d, d->core.received() - 1, piece, d->L, 1, dev));
   if (d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
   return RLNC_OK;
@@ -1511,7 +1576,7 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   const size_t twin_ok = d->recv_bs.cap >= d->recv_rows * d->pitch ? std::min(d->bs_rows, recv) : 0;
   size_t min_rows = (recv - twin_ok) * d->pitch <= kBsTwinBudget ? kBsMinRows : kBsMinRowsDecode;
 #ifdef KODR_TUNE_MODES
-  if (const char* env = getenv("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
+  if (const char* env = kodr_amd::tune_env("KODR_BS_MIN_ROWS_DEC")) min_rows = (size_t)atol(env);
 #endif
   d->last_bs = false;
   if (M < min_rows || few_narrow_rows(M, recv, d->L) || (d->pitch % 32) ||
@@ -1786,6 +1851,7 @@ int dec_add_pieces_host(rlnc_decoder* d, const uint8_t* rows, size_t count, size
   // coefficient side, exactly as repeated AddPiece calls
   size_t n = 0;
   const int st = d->core.add_many(vecs, vpitch, count, &n);
+  count_elim(d, kElimHost);
   TRY(dec_batch_post(d, rows, pitch, dev, bc, n));
   if (n && d->policy == RLNC_DECODE_EAGER) TRY(dec_progress(d, -1));
   *consumed = n;
@@ -1811,7 +1877,7 @@ namespace {
 // KODR_ADD_SIDE=0 keeps the batched AddPiece's row copies on the context
 // stream ahead of the elimination (A/B)
 bool add_side_stream() {
-  static const bool v = getenv("KODR_ADD_SIDE") ? atoi(getenv("KODR_ADD_SIDE")) != 0 : true;
+  static const bool v = kodr_amd::tune_env("KODR_ADD_SIDE") ? atoi(kodr_amd::tune_env("KODR_ADD_SIDE")) != 0 : true;
   return v;
 }
 
@@ -1845,21 +1911,32 @@ int ctx_elim_tables(rlnc_ctx* ctx) {
   return RLNC_OK;
 }
 
+constexpr size_t kElimHdr = 4 * kodr_amd::kElimMcMaxBlocks;  // counts / status words ahead of the states
+
 // the multi-workgroup elimination's hand-off buffer for nc decoders and this
-// launch's epoch (a new tag per launch; the buffer is zeroed when it is
-// allocated and when the tags wrap)
+// launch's tags: gf_elim_mc_attempts() consecutive ones, after every tag any
+// earlier launch of the context used.  Tags only grow, so neither the hand-off
+// granules nor the status words in pinned memory (elim_pin) can hold a tag of
+// this launch before it runs, whichever buffer was reallocated since; a new
+// hand-off buffer is zeroed (tag 0: never a launch's).  When the tags would
+// wrap, the stream is drained and both are zeroed before counting from 1.
 int ctx_elim_mc(rlnc_ctx* ctx, size_t k, size_t nc, kodr_amd::ElimArgs* a) {
   const size_t bytes = kodr_amd::gf_elim_mc_pub_bytes((int)k, (int)nc);
+  const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   ctx->elim_pub.bind(ctx->device, ctx->stream);
   const uint8_t* before = ctx->elim_pub.p;
   TRY(ctx->elim_pub.reserve(bytes));
-  const bool fresh = ctx->elim_pub.p != before || ctx->elim_epoch >= 0x7ffffff0u;
-  if (fresh) {
+  if (ctx->elim_epoch + na >= 0x7ffffff0u) {
+    HIPC(hipStreamSynchronize(ctx->stream));
+    if (ctx->elim_pin) memset(ctx->elim_pin, 0, std::min(ctx->elim_pin_cap, kElimHdr));
     HIPC(hipMemsetAsync(ctx->elim_pub.p, 0, ctx->elim_pub.cap, ctx->stream));
     ctx->elim_epoch = 0;
+  } else if (ctx->elim_pub.p != before) {
+    HIPC(hipMemsetAsync(ctx->elim_pub.p, 0, ctx->elim_pub.cap, ctx->stream));
   }
   a->pub = reinterpret_cast<uint64_t*>(ctx->elim_pub.p);
-  a->epoch = ++ctx->elim_epoch;
+  a->epoch = ctx->elim_epoch + 1;
+  ctx->elim_epoch += na;
   return RLNC_OK;
 }
 
@@ -1887,7 +1964,6 @@ void elim_counts(const kodr_amd::ElimArgs& a, size_t nc, bool mc, const uint8_t*
     cnt[i] = ok ? a.k : 0;
   }
 }
-constexpr size_t kElimHdr = 4 * kodr_amd::kElimMcMaxBlocks;  // counts / status words ahead of the states
 
 // the pinned, device-mapped buffer gf_elim_mc2 writes its status words and T
 // rows into ("direct"), grown as needed and zeroed when allocated
@@ -1906,50 +1982,60 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 
 // A direct launch's results: the host polls the status words in pinned
 // memory (each workgroup stores its word after its T rows, system-scope
-// release) instead of synchronising the stream and copying; cnt[i] = k when
-// every workgroup of decoder i is done, else 0 (kodr's route on the host).
-// A launch that never reports within 2 s is waited for on the stream once.
-// on_fail(i): decoder i's workgroups have all reported and one failed (its
-// batch goes to the host whatever the others do), called once per such
-// decoder while the launch may still run
-int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt,
+// release) instead of synchronising the stream and copying.  A word is
+// reported when it carries one of the launch's tags (tag0 + attempt, bit 31
+// set on failure).  Decoder i is resolved when every one of its workgroups
+// reported success (cnt[i] = k, att[i] = the attempt that succeeded) or any
+// reported failure (cnt[i] = 0: kodr's route on the host).  A failed
+// workgroup leaves the decoder's abort granule first, so its workgroups that
+// have not started yet read no input: the host may go on without them.
+// on_fail(i) runs as soon as decoder i fails, while the launch may still run.
+// A launch that resolves nothing within 2 s is waited for on the stream once.
+int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt, int* att,
                      const std::function<int(size_t)>& on_fail = nullptr) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
+  const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
-  const size_t nw = nc * (size_t)P;
   const auto t0 = std::chrono::steady_clock::now();
   bool synced = false;
-  std::vector<uint8_t> seen(on_fail ? nc : 0, 0);
-  for (size_t i = 0;;) {
-    while (i < nw && (st[i] & 0x7fffffffu) == a.epoch) i++;
-    if (i == nw) break;
-    if (on_fail)  // any failed decoder reported in full?
-      for (size_t g = 0; g < nc; g++) {
-        if (seen[g]) continue;
-        bool all = true, fail = false;
-        for (int q = 0; q < P && all; q++) {
-          const uint32_t v = st[g * P + q];
-          all = (v & 0x7fffffffu) == a.epoch;
-          fail = fail || v != a.epoch;
-        }
-        if (all && fail) {
-          std::atomic_thread_fence(std::memory_order_acquire);
-          seen[g] = 1;
-          TRY(on_fail(g));
-        }
+  std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed
+  size_t open = nc;
+  for (unsigned spins = 0; open;) {
+    for (size_t g = 0; g < nc; g++) {
+      if (res[g]) continue;
+      int done = 0;
+      bool fail = false;
+      for (int q = 0; q < P && !fail; q++) {
+        const uint32_t v = st[g * P + q];
+        const uint32_t t = (v & 0x7fffffffu) - a.epoch;
+        if (t >= na) continue;  // not reported yet
+        if (v & 0x80000000u)
+          fail = true;
+        else
+          done++;
       }
-    if (!synced && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-      HIPC(hipStreamSynchronize(ctx->stream));
-      synced = true;
-      continue;
+      if (!fail && done < P) continue;
+      std::atomic_thread_fence(std::memory_order_acquire);
+      res[g] = fail ? -1 : 1;
+      open--;
+      if (fail && on_fail) TRY(on_fail(g));
     }
+    if (!open) break;
     if (synced) break;  // finished without reporting: the host route
+    if (++spins < 4096) {
+      _mm_pause();
+    } else {
+      std::this_thread::yield();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        HIPC(hipStreamSynchronize(ctx->stream));
+        synced = true;
+      }
+    }
   }
   std::atomic_thread_fence(std::memory_order_acquire);
   for (size_t i = 0; i < nc; i++) {
-    bool ok = true;
-    for (int q = 0; q < P; q++) ok = ok && st[i * P + q] == a.epoch;
-    cnt[i] = ok ? a.k : 0;
+    cnt[i] = res[i] == 1 ? a.k : 0;
+    att[i] = res[i] == 1 ? (int)((st[i * P] & 0x7fffffffu) - a.epoch) : 0;
   }
   return RLNC_OK;
 }
@@ -2157,7 +2243,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
 #else
     const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
 #endif
-    std::vector<int> cntv(nc);
+    std::vector<int> cntv(nc), attv(nc, 0);
     const uint8_t* tstates = hostp + hdr;  // T rows (tonly: k x k per decoder) or whole states
     // a decoder whose launch failed (a singular panel block, or a singular C)
     // takes kodr's route on the host from its state before the batch: started
@@ -2181,7 +2267,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     };
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      TRY(elim_direct_wait(ctx, a, nc, cntv.data(),
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(),
                            side ? std::function<int(size_t)>(early_host) : std::function<int(size_t)>()));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
@@ -2192,7 +2278,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
                           hdr + nc * ostride, 1, ctx->stream));
     }
 #ifdef KODR_ELIM_TIMING
-    if (const char* dump = getenv("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
+    if (const char* dump = kodr_amd::tune_env("KODR_ELIM_DUMP")) {  // tuning build: the kernel's stamps
       if (FILE* fp = fopen(dump, "wb")) {
         if (direct)
           fwrite(ctx->elim_pin, 1, hdr + nc * k * k, fp);
@@ -2224,6 +2310,10 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
         ok = tonly ? c == k && d->core.load_inverse(tstates + i * k * k, k)
                    : d->core.load_rref(tstates + i * ostride, opitch, c);
       got[i] = ok ? c - r : 0;
+      if (ok && c == k)
+        count_elim(d, attv[i] ? kElimGpuRetried : kElimGpu);
+      else
+        count_elim(d, kElimHostAfterGpu);
       const bool on_dev = ok && c == k && !cont && a.out_dev;
       d->tdev = on_dev ? a.out_dev + i * k * k : nullptr;
       d->tdev_seq = on_dev ? ctx->tdev_seq : 0;
@@ -2355,10 +2445,10 @@ int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read) {
       HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
       TRY(join());
       const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
-      std::vector<int> cntv(nc);
+      std::vector<int> cntv(nc), attv(nc, 0);
       const uint8_t* tstates = hostp + hdr;
       if (direct) {
-        TRY(elim_direct_wait(ctx, a, nc, cntv.data()));
+        TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data()));
         tstates = ctx->elim_pin + hdr;
       } else {
         HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
@@ -2372,13 +2462,20 @@ int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read) {
       const int* cnt = cntv.data();
       HostPool::get().run(nc, [&](size_t i) {
         rlnc_decoder* d = ds[el[c0 + i]];
-        if (cnt[i] != (int)k) return;  // M singular: the host flush below
-        const uint8_t* st = tonly ? tstates + i * k * k : tstates + i * ostride;
-        const size_t sp = tonly ? k : opitch;
-        const bool ok = d->core.received() == 0
-                            ? (tonly ? d->core.load_inverse(st, sp) : d->core.load_rref(st, sp, k))
-                            : d->core.load_continued(st, sp, tonly);
-        if (ok) d->npend = 0;
+        bool ok = false;
+        if (cnt[i] == (int)k) {
+          const uint8_t* st = tonly ? tstates + i * k * k : tstates + i * ostride;
+          const size_t sp = tonly ? k : opitch;
+          ok = d->core.received() == 0 ? (tonly ? d->core.load_inverse(st, sp) : d->core.load_rref(st, sp, k))
+                                       : d->core.load_continued(st, sp, tonly);
+        }
+        if (ok) {
+          d->npend = 0;
+          count_elim(d, attv[i] ? kElimGpuRetried : kElimGpu);
+        } else {  // M singular: the host flush takes the queue, without a second launch
+          d->gpu_rejected = true;
+          count_elim(d, kElimHostAfterGpu);
+        }
       });
     }
   }
@@ -2697,6 +2794,16 @@ int rlnc_decoder_apply_stats(const rlnc_decoder* d, size_t* gf_rows, size_t* cop
 }
 
 int rlnc_decoder_last_apply_bitsliced(const rlnc_decoder* d) { return d && d->last_bs ? 1 : 0; }
+
+int rlnc_decoder_elim_stats(const rlnc_decoder* d, size_t* gpu, size_t* gpu_retried, size_t* host_after_gpu,
+                            size_t* host) {
+  if (!d) return RLNC_ERR_INVALID_ARGUMENT;
+  if (gpu) *gpu = d->elim_gpu;
+  if (gpu_retried) *gpu_retried = d->elim_gpu_retried;
+  if (host_after_gpu) *host_after_gpu = d->elim_host_after_gpu;
+  if (host) *host = d->elim_host;
+  return RLNC_OK;
+}
 
 int rlnc_decoder_coefficients(const rlnc_decoder* d, uint8_t* out) {
   if (!d || !out) return RLNC_ERR_INVALID_ARGUMENT;

@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "host_gf.hpp"
+#include "tune.hpp"
 
 namespace kodr_amd {
 
@@ -392,8 +393,8 @@ struct FullSolve {
 
 bool DecoderCore::solve_full_batch(const uint8_t* vecs, size_t pitch) {
   const size_t k = k_;
-  static const bool enabled = !getenv("KODR_FULL_SOLVE") || atoi(getenv("KODR_FULL_SOLVE")) != 0;
-  static const size_t min_k = getenv("KODR_FULL_MIN_K") ? (size_t)atol(getenv("KODR_FULL_MIN_K")) : kFullMinK;
+  static const bool enabled = !kodr_amd::tune_env("KODR_FULL_SOLVE") || atoi(kodr_amd::tune_env("KODR_FULL_SOLVE")) != 0;
+  static const size_t min_k = kodr_amd::tune_env("KODR_FULL_MIN_K") ? (size_t)atol(kodr_amd::tune_env("KODR_FULL_MIN_K")) : kFullMinK;
   if (!enabled || received_ != 0 || k < min_k || !hostgf::have_gfni512()) return false;
   ensure_tcap(k);
   FullSolve F;
@@ -409,7 +410,7 @@ bool DecoderCore::solve_full_batch(const uint8_t* vecs, size_t pitch) {
   F.cur.assign(k, -1);
   F.used.assign(k, 0);
   F.pivrow.assign(k, -1);
-  static const bool timing = getenv("KODR_FULL_SOLVE") && atoi(getenv("KODR_FULL_SOLVE")) == 2;
+  static const bool timing = kodr_amd::tune_env("KODR_FULL_SOLVE") && atoi(kodr_amd::tune_env("KODR_FULL_SOLVE")) == 2;
   double ta = 0, tb = 0;
   for (size_t jb = 0; jb < k; jb += kFullNB) {
     const double t0 = timing ? now_us() : 0;

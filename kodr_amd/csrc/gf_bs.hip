@@ -41,6 +41,7 @@
 #include "gf_kernels.hpp"
 // generated: bodies, row loop, register map (gen_bs_bodies.py)
 #include "gf_bs_bodies.inc"
+#include "tune.hpp"
 
 namespace kodr_amd {
 
@@ -890,7 +891,7 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
   // at most kCopyWgPerCu workgroups (4 waves each) per CU over the launch
-  static const int wg_per_cu = getenv("KODR_COPY_WG_PER_CU") ? atoi(getenv("KODR_COPY_WG_PER_CU")) : kCopyWgPerCu;
+  static const int wg_per_cu = tune_env("KODR_COPY_WG_PER_CU") ? atoi(tune_env("KODR_COPY_WG_PER_CU")) : kCopyWgPerCu;
   const size_t cap = std::max<size_t>(1, (size_t)std::max(wg_per_cu, 1) * 256 / (size_t)n);
   const size_t gx = std::min<size_t>((total + 255) / 256, cap);
   hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream, g, spitch,
@@ -940,7 +941,7 @@ size_t bs_lds_bytes(int kw, int rpw, bool direct = false) {
 // fold): equal at B = 32-64, 2.4 % faster at B = 256 (profiles/r03/direct_ab/).
 // KODR_BS_DIRECT=0 keeps the folded plans (A/B measurements).
 bool bs_direct_allowed() {
-  static const bool v = getenv("KODR_BS_DIRECT") ? atoi(getenv("KODR_BS_DIRECT")) != 0 : true;
+  static const bool v = tune_env("KODR_BS_DIRECT") ? atoi(tune_env("KODR_BS_DIRECT")) != 0 : true;
   return v;
 }
 
@@ -1000,7 +1001,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   BsPlan p = plan_gemm_bs(M, K, ncols, group ? group->n : 1, group != nullptr);
   if (!p.ok) return hipErrorInvalidValue;
 #ifdef KODR_TUNE_MODES
-  if (const char* env = getenv("KODR_BS_KW")) {  // force the waves per workgroup
+  if (const char* env = tune_env("KODR_BS_KW")) {  // force the waves per workgroup
     const int kw = atoi(env);
     const long kpad = ((long)K + kBsChunk - 1) / kBsChunk * kBsChunk;
     p.kw = kw;
@@ -1019,7 +1020,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
   int mode = 0;
   (void)mode;
 #ifdef KODR_TUNE_MODES
-  if (const char* env = getenv("KODR_BS_MODE")) mode = atoi(env);
+  if (const char* env = tune_env("KODR_BS_MODE")) mode = atoi(env);
   if (mode == 14) {  // program scratch for the scalar-load variant, with look-ahead slack
     static uint32_t* scratch = nullptr;
     constexpr size_t kScratch = (size_t)64 << 20;

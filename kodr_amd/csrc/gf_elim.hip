@@ -50,6 +50,7 @@
 #include <algorithm>
 
 #include "gf_kernels.hpp"
+#include "tune.hpp"
 
 namespace kodr_amd {
 
@@ -725,9 +726,101 @@ __global__ __launch_bounds__(64 * kElimWaves) void gf_elim_circ_kernel(ElimArgs 
 // other with no overlap between groups, is superseded by these two: 200 vs
 // 153 (mc2) and 59 (mc4) us for one k = 256 decoder.)
 constexpr uint32_t kMcFail = 0x80000000u;
-constexpr int kMcSpinMax = 1 << 20;  // >= ~1 s of polling: only a lost workgroup gets there
+// A launch owns kMcAttempts consecutive tags, args.epoch .. args.epoch + 3, one
+// per attempt.  Attempt a inverts the rows rotated by mc_rot(a): when a panel's
+// 16 x 16 block is singular although C may not be (pivots stay inside the
+// panel's 16 rows, so a singular leading 16j x 16j block of C fails the
+// attempt: about 6 % of uniform k = 256 batches), every workgroup starts the
+// next attempt from the rows in another order.  FAIL granules carry the
+// reason in their data: 0 this attempt failed, kMcAbort the launch stops (a
+// singular last panel, which means C itself is singular; a panel block with
+// a zero column, which means a structured -- systematic -- batch no row order
+// fixes; a timeout; or the last attempt).  An abort is published with the
+// last tag, so that a consumer in any attempt sees it.
+constexpr int kMcAttempts = 4;
+constexpr uint32_t kMcAbort = 1u;
+// the longest a workgroup waits on one hand-off before it gives up (a
+// workgroup of the launch that is not resident, e.g. behind another kernel;
+// the host then takes kodr's route), in polls: a global poll (an agent-scope
+// round trip, >= ~0.3 us, and s_sleep) 8192 times is >= ~2 ms, an LDS counter
+// (>= ~50 cycles) 2^17 times >= ~3 ms.  Counted, not timed: a clock read in
+// the poll loops (s_memrealtime) slowed the chain by ~13 % (58 -> 66 us).
+constexpr int kMcPollSpins = 1 << 13;
+constexpr int kMcLdsSpins = 1 << 17;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// input row of row i < k in attempt att: (i + s) mod k, s = 0, k/2, k/4, 3k/4
+__device__ __forceinline__ int mc_rot(int att, int k) {
+  return att == 0 ? 0 : att == 1 ? k / 2 : att == 2 ? k / 4 : (3 * k) / 4;
+}
+__device__ __forceinline__ int mc_src_row(int gr, int k, int rot) {
+  const int r = gr + rot;
+  return r >= k ? r - k : r;
+}
+
+// a hand-off granule seen by attempt `tag` of a launch whose last tag is tlast:
+// 0 this attempt's value, 1 this attempt failed (its FAIL, or a later attempt's
+// value or FAIL: the producer has moved on), 2 abort, -1 not there yet
+// (branch-free: a branch per granule made the compiler wait for each poll
+// load before issuing the next, 4x the hand-off latency)
+__device__ __forceinline__ int mc_tag_state(uint64_t x, uint32_t tag, uint32_t tlast) {
+  const uint32_t tg = (uint32_t)(x >> 32), t = tg & ~kMcFail;
+  const int failed = (tg & kMcFail) && ((uint32_t)x & kMcAbort) ? 2 : 1;
+  const int later = t >= tag && t <= tlast ? failed : -1;
+  return tg == tag ? 0 : later;
+}
+
+
+// the workgroup's fail word: the largest reason any wave saw (1 this attempt, 2 abort)
+__device__ __forceinline__ void mc_set_fail(int* lfail, int why) {
+  __hip_atomic_fetch_max(lfail, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void mc_put(gu64* dst, uint32_t tag, uint32_t v) {
+  __hip_atomic_store(dst, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// FAIL for attempt `tag` (why 1) or an abort for every attempt (why 2)
+__device__ __forceinline__ void mc_put_fail(gu64* dst, uint32_t tag, uint32_t tlast, int why) {
+  const uint32_t t = why >= 2 ? tlast : tag;
+  __hip_atomic_store(dst, ((unsigned long long)(t | kMcFail) << 32) | (why >= 2 ? kMcAbort : 0u), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// why a singular panel block fails the launch: 2 (abort) when it is the last
+// panel with rows of C (every block before it was invertible, so C is
+// singular) or when a column of the block is zero in all 16 rows (a
+// structured batch: random rows make that a 256^-16 event), else 1 (retry)
+__device__ __forceinline__ int mc_singular_why(uint32_t blk, int lane, int p, int k) {
+  if (p == (k - 1) / 16) return 2;
+  uint32_t o = blk;  // OR over the 16 rows (t = lane / 4) of each dword d = lane % 4
+  o |= bperm(o, lane ^ 4);
+  o |= bperm(o, lane ^ 8);
+  o |= bperm(o, lane ^ 16);
+  o |= bperm(o, lane ^ 32);
+  const bool zero = lane < 4 && ((o - 0x01010101u) & ~o & 0x80808080u) != 0;
+  return __builtin_amdgcn_ballot_w64(zero) ? 2 : 1;
+}
+
+// byte j of a T row from the row attempt rotation s computed (T = T' Pi with
+// (Pi C)_i = C_{(i + s) mod k}, so T[j] = T'[(j - s) mod k]); scr: this
+// wave's 256 bytes of LDS
+__device__ __forceinline__ uint32_t mc_unrotate(uint32_t v, uint32_t* scr, int lane, int k, int s) {
+  scr[lane] = v;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's writes land before its reads
+  const volatile uint8_t* b = reinterpret_cast<const volatile uint8_t*>(scr);
+  uint32_t o = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int j = 4 * lane + q;
+    if (j < k) {
+      const int src = j - s < 0 ? j - s + k : j - s;
+      o |= (uint32_t)b[src] << (8 * q);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // ... and the reads before the next row's writes
+  return o;
+}
 
 __device__ __forceinline__ uint32_t mc_mul(const uint4& t, uint32_t t2, uint32_t s0, uint32_t s1, uint32_t s2) {
   return __builtin_amdgcn_perm(t.y, t.x, s0) ^ __builtin_amdgcn_perm(t.w, t.z, s1) ^
@@ -757,6 +850,40 @@ __device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane,
     if (4 * lane + b < k) row[4 * lane + b] = (uint8_t)(v >> (8 * b));
 }
 
+// row gr of the launch's matrix in attempt rotation rot, lane = dword (rows
+// past k: identity padding, the matrix stays [[C, 0], [0, I]])
+__device__ __forceinline__ uint32_t mc_load_row(const ElimArgs& args, int g, int gr, int rot, int lane) {
+  const int k = args.k;
+  if (gr >= k) return gr >> 2 == lane ? 1u << (8 * (gr & 3)) : 0u;
+  const uint8_t* src = args.vecs[g] + (size_t)mc_src_row(gr, k, rot) * args.vpitch;
+  uint32_t v = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++)
+    if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
+  return v;
+}
+
+// v, opaque to the compiler: an attempt's body takes its indices through
+// these, so that nothing computed from them is hoisted out of the attempt
+// loop (hoisted addresses stayed live through both roles and spilled)
+__device__ __forceinline__ int mc_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ int mc_opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ gu64* mc_opaque_s(gu64* v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+
+// A workgroup that starts after its decoder's launch was given up (an abort
+// in the decoder's abort granule, written before any failed status word)
+// reads no input at all: the host may already have handed the rows back to
+// their owner.  (The granule's read is issued beside the table loads.)
+
 // ---- mc2: the same inversion, pipelined inside each workgroup -------------
 // Panels of 16 columns (NP = 2P); workgroup q owns panels 2q ("A rows", its
 // local rows 0-15) and 2q + 1 ("B rows", 16-31).  In-place block
@@ -775,7 +902,7 @@ __device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane,
 //    apply of p - 1), inverts it (mc2_panel_gj) and publishes S_p; for any
 //    other panel the chain waves poll R_p and S_p into LDS.
 // Hand-offs between workgroups as described above (granules tagged with
-// the launch epoch, FAIL bit; bounded spins); three LDS slots per panel
+// the attempt's tag, FAIL bit; bounded waits); three LDS slots per panel
 // buffer so a slot is rewritten only after both roles are two panels on.
 constexpr int kMc2Slots = 3;
 constexpr int kMc2ApplyCols = 4;  // columns per operand batch in the row apply
@@ -791,15 +918,16 @@ struct ElimMc2Lds {
   uint32_t fw[8][4][4];            // row wave w: G of its rows
   int rows_done;                   // row-wave iterations finished (8 per panel, 8 for the start)
   int chain_cnt;                   // chain-wave iterations finished (8 per panel)
-  int fail;                        // 1 singular / FAIL seen, 2 timeout
+  int fail;                        // this attempt: 1 failed, 2 abort
+  int late;                        // the launch was aborted before this workgroup started
 };
 
 __device__ __forceinline__ bool mc2_wait(ElimMc2Lds& lds, int* ctr, int target) {
   for (int spins = 0;; spins++) {
     if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
     if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-    if (spins > kMcSpinMax) {
-      __hip_atomic_store(&lds.fail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (spins > kMcLdsSpins) {
+      mc_set_fail(&lds.fail, 2);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -906,8 +1034,9 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = args.k;
-  const uint32_t epoch = args.epoch;
-  gu64* pub = (gu64*)args.pub + (size_t)g * NP * kMc2PanelGran;
+  const uint32_t tag0 = args.epoch, tlast = tag0 + kMcAttempts - 1;
+  gu64* const pub = (gu64*)args.pub + (size_t)g * NP * kMc2PanelGran;
+  gu64* const pubA = (gu64*)args.pub + (size_t)gridDim.y * NP * kMc2PanelGran + g;  // the decoder's abort granule
 #ifdef KODR_ELIM_TIMING
   // tuning build: s_memrealtime (100 MHz) stamps by lane 0 of row wave 0 and
   // chain wave 0, into this workgroup's 1 KiB of the T region (no result):
@@ -928,280 +1057,287 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
 #endif
   if (w == 0) MC2_STAMP(80);
 
+  const uint64_t ab = tid == 0 ? __hip_atomic_load(pubA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   for (int i = tid; i < 256 * 2; i += 1024) {
     const uint32_t* a = args.tables + 4 * i;
     const uint32_t* b = args.tables + kElimInvTables + 4 * i;
     lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
     lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
   }
-  if (tid == 0) {
-    lds.rows_done = 0;
-    lds.chain_cnt = 0;
-    lds.fail = 0;
-  }
+  if (tid == 0) lds.late = mc_tag_state(ab, tag0, tlast) == 2;
   __syncthreads();
+  const bool late = __builtin_amdgcn_readfirstlane(lds.late) != 0;
 
-  bool ok = true;
-  uint32_t R_out[4] = {0u, 0u, 0u, 0u};  // the finished T rows, for the device copy at the end
-  if (w < 8) {
-    // ================= row waves: rows 4w .. 4w + 3 =================
-    const int half = w >> 2;  // 0: panel 2q's rows, 1: panel 2q + 1's
-    uint32_t R[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int gr = 32 * q + 4 * w + i;
-      uint32_t v = 0;
-      if (gr < k) {
-        const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-          if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
-      } else if (gr >> 2 == lane) {
-        v = 1u << (8 * (gr & 3));
-      }
-      R[i] = v;
+  // row waves: T rows 32 q + 4 w + i of the successful attempt (assigned only
+  // on the way out of the loop, so nothing is carried through the chain's path)
+  uint32_t Tout[4];
+  int fail = late ? 2 : 0, att = 0;
+  for (; !late; att++) {
+    const uint32_t tag = tag0 + att;
+    const int rot = mc_rot(att, k);
+    if (tid == 0) {  // (separate stores: a merged one kept a vector of zeros live through the kernel)
+      __hip_atomic_store(&lds.rows_done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&lds.chain_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&lds.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // workgroup 0's first panel: its block for the chain (no earlier panel)
-    if (q == 0 && half == 0 && lane < 4)
+    __syncthreads();
+    // the attempt, on opaque copies of the indices (mc_opaque)
+    auto attempt = [&](const int q, const int w, const int lane, gu64* const pub) {
+    int unpublished = 2 * q;  // chain wave 0: the first owned panel whose S_p is not out yet
+    uint32_t R[4] = {0u, 0u, 0u, 0u};  // row waves: rows 32 q + 4 w + i
+    if (w < 8) {
+      // ================= row waves: rows 4w .. 4w + 3 =================
+      const int half = w >> 2;  // 0: panel 2q's rows, 1: panel 2q + 1's
 #pragma unroll
-      for (int i = 0; i < 4; i++) lds.mb[0][4 * w + i][4 + lane] = R[i];
-    mc2_signal(&lds.rows_done, lane);
-    if (w == 0) MC2_STAMP(81);
+      for (int i = 0; i < 4; i++) R[i] = mc_load_row(args, g, 32 * q + 4 * w + i, rot, lane);
+      // workgroup 0's first panel: its block for the chain (no earlier panel)
+      if (q == 0 && half == 0 && lane < 4)
+#pragma unroll
+        for (int i = 0; i < 4; i++) lds.mb[0][4 * w + i][4 + lane] = R[i];
+      mc2_signal(&lds.rows_done, lane);
+      if (w == 0) MC2_STAMP(81);
 
-    auto apply = [&](int pa) {
-      const int slot = pa % kMc2Slots, db = 4 * pa;
-      const bool own = (pa >> 1) == q && (pa & 1) == half;
-      // G of the 4 rows: the panel's S rows (own) or F (in lds.fw)
-      const uint32_t(*Gp)[4] = own ? &lds.sp[slot][4 * (w & 3)] : lds.fw[w];
-      if (!own) {
-        // F of the 4 rows: lane (cg, i, u) sums c = 4 cg .. 4 cg + 3, then
-        // the four groups are folded (lanes 16 and 32 apart)
-        if (lane >= db && lane < db + 4)
+      auto apply = [&](int pa) {
+        const int slot = pa % kMc2Slots, db = 4 * pa;
+        const bool own = (pa >> 1) == q && (pa & 1) == half;
+        // G of the 4 rows: the panel's S rows (own) or F (in lds.fw)
+        const uint32_t(*Gp)[4] = own ? &lds.sp[slot][4 * (w & 3)] : lds.fw[w];
+        if (!own) {
+          // F of the 4 rows: lane (cg, i, u) sums c = 4 cg .. 4 cg + 3, then
+          // the four groups are folded (lanes 16 and 32 apart)
+          if (lane >= db && lane < db + 4)
 #pragma unroll
-          for (int i = 0; i < 4; i++) lds.mw[w][i][lane - db] = R[i];
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes land first
-        const int cg = lane >> 4, i = (lane >> 2) & 3, u = lane & 3;
-        const uint32_t mwd = lds.mw[w][i][cg];
-        uint32_t acc = 0;
+            for (int i = 0; i < 4; i++) lds.mw[w][i][lane - db] = R[i];
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's writes land first
+          const int cg = lane >> 4, i = (lane >> 2) & 3, u = lane & 3;
+          const uint32_t mwd = lds.mw[w][i][cg];
+          uint32_t acc = 0;
 #pragma unroll
-        for (int cc = 0; cc < 4; cc++) {
-          const uint32_t m = (mwd >> (8 * cc)) & 0xffu;
-          const uint4 t = lds.tab[2 * m];
-          const uint32_t t2 = lds.tab[2 * m + 1].x;
-          const uint32_t xv = lds.sp[slot][4 * cg + cc][u];
-          acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+          for (int cc = 0; cc < 4; cc++) {
+            const uint32_t m = (mwd >> (8 * cc)) & 0xffu;
+            const uint4 t = lds.tab[2 * m];
+            const uint32_t t2 = lds.tab[2 * m + 1].x;
+            const uint32_t xv = lds.sp[slot][4 * cg + cc][u];
+            acc ^= gmul4(t, t2, sel0(xv), sel1(xv), sel2(xv));
+          }
+          acc ^= bperm(acc, lane ^ 16);
+          acc ^= bperm(acc, lane ^ 32);
+          if (lane < 16) lds.fw[w][i][u] = acc;
+          __builtin_amdgcn_s_waitcnt(0xc07f);
         }
-        acc ^= bperm(acc, lane ^ 16);
-        acc ^= bperm(acc, lane ^ 32);
-        if (lane < 16) lds.fw[w][i][u] = acc;
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-      }
-      if (w == 0) MC2_STAMP(112 + pa);  // F of the rows known (pa <= 15: index <= 127)
-      uint32_t acc[4];
+        if (w == 0) MC2_STAMP(112 + pa);  // F of the rows known (pa <= 15: index <= 127)
+        uint32_t acc[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
-      // kMc2ApplyCols columns per batch, one batch live at a time (the whole
-      // loop unrolled spilled 513 VGPRs).  The kernel holds ~113 VGPRs, all of
-      // a SIMD's file at 4 waves, so the row copies launched beside it cannot
-      // share its CUs; capped at 96 (waves_per_eu 5, a few bytes spilled) with
-      // the copies at 2 or 4 loads per lane, the round trip measured slower
-      // (238-241 against 230-235, 235-236 against 228-230 us per generation,
-      // profiles/r04/var_ab/)
+        for (int i = 0; i < 4; i++) acc[i] = own ? 0u : R[i];
+        // kMc2ApplyCols columns per batch, one batch live at a time (the whole
+        // loop unrolled spilled 513 VGPRs).  The kernel holds ~113 VGPRs, all of
+        // a SIMD's file at 4 waves, so the row copies launched beside it cannot
+        // share its CUs; capped at 96 (waves_per_eu 5, a few bytes spilled) with
+        // the copies at 2 or 4 loads per lane, the round trip measured slower
+        // (238-241 against 230-235, 235-236 against 228-230 us per generation,
+        // profiles/r04/var_ab/)
 #pragma unroll 1
-      for (int cb = 0; cb < 16; cb += kMc2ApplyCols) {
-        uint32_t gw[4];  // the bytes of columns cb .. of each row's G (wave-uniform)
+        for (int cb = 0; cb < 16; cb += kMc2ApplyCols) {
+          uint32_t gw[4];  // the bytes of columns cb .. of each row's G (wave-uniform)
 #pragma unroll
-        for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cb >> 2]) >> (8 * (cb & 3));
-        // the (uniform) table reads and the data reads of these columns
-        // first, then the arithmetic: one LDS round trip per batch (sinking
-        // each read next to its use cost one round trip per term)
-        uint4 tt[kMc2ApplyCols][4];
-        uint32_t t2[kMc2ApplyCols][4], xs[kMc2ApplyCols];
+          for (int i = 0; i < 4; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cb >> 2]) >> (8 * (cb & 3));
+          // the (uniform) table reads and the data reads of these columns
+          // first, then the arithmetic: one LDS round trip per batch (sinking
+          // each read next to its use cost one round trip per term)
+          uint4 tt[kMc2ApplyCols][4];
+          uint32_t t2[kMc2ApplyCols][4], xs[kMc2ApplyCols];
 #pragma unroll
-        for (int cc = 0; cc < kMc2ApplyCols; cc++) {
-          xs[cc] = lds.rp[slot][cb + cc][lane];
+          for (int cc = 0; cc < kMc2ApplyCols; cc++) {
+            xs[cc] = lds.rp[slot][cb + cc][lane];
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
-            tt[cc][i] = lds.tab[2 * f];
-            t2[cc][i] = lds.tab[2 * f + 1].x;
+            for (int i = 0; i < 4; i++) {
+              const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
+              tt[cc][i] = lds.tab[2 * f];
+              t2[cc][i] = lds.tab[2 * f + 1].x;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cc = 0; cc < kMc2ApplyCols; cc++) {
+            const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
           }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        const int u = lane - db;  // the panel columns take G
 #pragma unroll
-        for (int cc = 0; cc < kMc2ApplyCols; cc++) {
-          const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
-#pragma unroll
-          for (int i = 0; i < 4; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
-        }
-      }
-      const int u = lane - db;  // the panel columns take G
-#pragma unroll
-      for (int i = 0; i < 4; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
-    };
+        for (int i = 0; i < 4; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
+      };
 
-    for (int p = 0; p < NP; p++) {
-      if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1)) || !mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
-      if (w == 0) MC2_STAMP(96 + p);
-      if (p >= 1) apply(p - 1);
-      if ((p >> 1) == q && (p & 1) == half) {  // my rows are panel p's: R_p out
+      for (int p = 0; p < NP; p++) {
+        if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1)) || !mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+        if (w == 0) MC2_STAMP(96 + p);
+        if (p >= 1) apply(p - 1);
+        if ((p >> 1) == q && (p & 1) == half) {  // my rows are panel p's: R_p out
+          const int slot = p % kMc2Slots;
+          gu64* dst = pub + (size_t)p * kMc2PanelGran;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int r = 4 * (w & 3) + i;
+            lds.rp[slot][r][lane] = R[i];
+            mc_put(dst + r * 64 + lane, tag, R[i]);
+          }
+        }
+        const int pn = p + 1;
+        if (pn < NP && (pn >> 1) == q && (pn & 1) == half) {  // next panel's block for the chain
+          const int slot = pn % kMc2Slots;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int r = 4 * (w & 3) + i;
+            if (lane >= 4 * p && lane < 4 * p + 4) lds.mb[slot][r][lane - 4 * p] = R[i];
+            if (lane >= 4 * pn && lane < 4 * pn + 4) lds.mb[slot][r][4 + lane - 4 * pn] = R[i];
+          }
+        }
+        mc2_signal(&lds.rows_done, lane);
+        if (w == 0) MC2_STAMP(64 + p);
+      }
+      if (mc2_wait(lds, &lds.chain_cnt, 8 * NP) && mc2_wait(lds, &lds.rows_done, 8 * (NP + 1))) {
+        apply(NP - 1);
+        if (w == 0) MC2_STAMP(82);
+      }
+    } else {
+      // ================= chain waves =================
+      const int cw = w - 8;
+      if (cw == 0) __builtin_amdgcn_s_setprio(3);
+      for (int p = 0; p < NP; p++) {
         const int slot = p % kMc2Slots;
-        gu64* dst = pub + (size_t)p * kMc2PanelGran;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int r = 4 * (w & 3) + i;
-          lds.rp[slot][r][lane] = R[i];
-          __hip_atomic_store(dst + r * 64 + lane, ((unsigned long long)epoch << 32) | R[i], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+        gu64* base = pub + (size_t)p * kMc2PanelGran;
+        // every chain wave finished panel p - 1 (no wave runs ahead: the count
+        // then means exactly that)
+        if (!mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
+        if (cw == 0) MC2_STAMP(4 * p);
+        if ((p >> 1) == q) {
+          if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
+          if (cw == 0) MC2_STAMP(4 * p + 1);
+          if (cw == 0) {
+            // the block brought up to date with panel p - 1 (two 16-term
+            // products, operand reads batched), then inverted in registers
+            const int t = lane >> 2, d = lane & 3;
+            uint32_t blk = lds.mb[slot][t][4 + d];
+            if (p >= 1) {
+              const int ps = (p - 1) % kMc2Slots;
+              blk = mc3_block_update_c(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], lds.rp[ps], 4 * p, lane);
+            }
+            MC2_STAMP(4 * p + 2);
+            uint32_t sval = 0;
+            int srow = 0;
+            const bool inv_ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
+            if (inv_ok) {
+              lds.sp[slot][srow][d] = sval;
+              mc_put(base + 16 * 64 + srow * 4 + d, tag, sval);
+              unpublished = p + 1;
+            } else {
+              mc_set_fail(&lds.fail, mc_singular_why(blk, lane, p, k));
+            }
+            MC2_STAMP(4 * p + 3);
+          }
+          if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+          mc2_signal(&lds.chain_cnt, lane);
+        } else {
+          // another workgroup's panel: R_p (rows 2cw, 2cw + 1) and S_p (wave 0) into LDS
+          const gu64* src = base + (size_t)(2 * cw) * 64 + lane;
+          uint64_t a = 0, b = 0, s = 0;
+          int why = 0;
+          for (int spins = 0;; spins++) {
+            a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cw == 0) s = __hip_atomic_load(base + 16 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int sa = mc_tag_state(a, tag, tlast), sb = mc_tag_state(b, tag, tlast);
+            const int ss = cw == 0 ? mc_tag_state(s, tag, tlast) : 0;
+            if (__builtin_amdgcn_ballot_w64(sa == 2 || sb == 2 || ss == 2)) {
+              why = 2;
+              break;
+            }
+            if (__builtin_amdgcn_ballot_w64(sa == 1 || sb == 1 || ss == 1)) {
+              why = 1;
+              break;
+            }
+            if (__builtin_amdgcn_ballot_w64(sa != 0 || sb != 0 || ss != 0) == 0) break;
+            if (const int lf = __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              why = lf;
+              break;
+            }
+            if (spins > kMcPollSpins) {
+              why = 2;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (why) {
+            mc_set_fail(&lds.fail, why);
+            break;
+          }
+          if (cw == 0) MC2_STAMP(4 * p + 1);
+          if (!mc2_wait(lds, &lds.rows_done, 8 * p)) break;  // the slot's last readers are done
+          if (cw == 0) MC2_STAMP(4 * p + 2);
+          lds.rp[slot][2 * cw][lane] = (uint32_t)a;
+          lds.rp[slot][2 * cw + 1][lane] = (uint32_t)b;
+          if (cw == 0) lds.sp[slot][lane >> 2][lane & 3] = (uint32_t)s;
+          mc2_signal(&lds.chain_cnt, lane);
+          if (cw == 0) MC2_STAMP(4 * p + 3);
         }
       }
-      const int pn = p + 1;
-      if (pn < NP && (pn >> 1) == q && (pn & 1) == half) {  // next panel's block for the chain
-        const int slot = pn % kMc2Slots;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int r = 4 * (w & 3) + i;
-          if (lane >= 4 * p && lane < 4 * p + 4) lds.mb[slot][r][lane - 4 * p] = R[i];
-          if (lane >= 4 * pn && lane < 4 * pn + 4) lds.mb[slot][r][4 + lane - 4 * pn] = R[i];
-        }
-      }
-      mc2_signal(&lds.rows_done, lane);
-      if (w == 0) MC2_STAMP(64 + p);
+      if (cw == 0) __builtin_amdgcn_s_setprio(0);
     }
-    ok = mc2_wait(lds, &lds.chain_cnt, 8 * NP) && mc2_wait(lds, &lds.rows_done, 8 * (NP + 1));
+    __syncthreads();
+    fail = lds.fail;
 #ifdef KODR_ELIM_TIMING
-    if (ok) {
-      apply(NP - 1);
-      if (w == 0) MC2_STAMP(82);
-    }
-    ok = false;
+    if (!fail) fail = 2;  // the stamps overwrite T: kodr's route on the host
 #endif
-    if (ok) {
-      apply(NP - 1);
+    if (fail && w == 8) {
+      // owned panels whose S_p is not out (an abort: every owned panel): FAIL
+      // on R_p and S_p, so that every later workgroup stops too
+      for (int p = fail >= 2 ? 2 * q : unpublished; p < 2 * q + 2 && p < NP; p++) {
+        gu64* base = pub + (size_t)p * kMc2PanelGran;
+        for (int r = 0; r < 17; r++) mc_put_fail(base + r * 64 + lane, tag, tlast, fail);
+      }
+      // the FAILs reach L2 before the row waves' stores of the next attempt
+      // to the same R_p slots (another wave: the barrier alone does not order them)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+    if (!fail && w < 8) {
+      // T = T' Pi: the rotation undone (through a slot no wave reads any more)
+      uint32_t* scr = &lds.rp[NP % kMc2Slots][0][0] + 64 * w;
       uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
+        Tout[i] = rot ? mc_unrotate(R[i], scr, lane, k, rot) : R[i];
         const int gr = 32 * q + 4 * w + i;
-        if (gr >= k) continue;
-        mc_store_row(out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k), R[i], lane, k);
-        R_out[i] = R[i];
+        if (gr < k) mc_store_row(out + (size_t)gr * args.out_pitch + (args.direct ? 0 : k), Tout[i], lane, k);
       }
     }
-  } else {
-    // ================= chain waves =================
-    const int cw = w - 8;
-    if (cw == 0) __builtin_amdgcn_s_setprio(3);
-    int unpublished = 2 * q;  // the first owned panel whose S_p is not out yet
-    for (int p = 0; p < NP; p++) {
-      const int slot = p % kMc2Slots;
-      gu64* base = pub + (size_t)p * kMc2PanelGran;
-      // every chain wave finished panel p - 1 (no wave runs ahead: the count
-      // then means exactly that)
-      if (!mc2_wait(lds, &lds.chain_cnt, 8 * p)) break;
-      if (cw == 0) MC2_STAMP(4 * p);
-      if ((p >> 1) == q) {
-        if (!mc2_wait(lds, &lds.rows_done, 8 * (p + 1))) break;
-        if (cw == 0) MC2_STAMP(4 * p + 1);
-        if (cw == 0) {
-          // the block brought up to date with panel p - 1 (two 16-term
-          // products, operand reads batched), then inverted in registers
-          const int t = lane >> 2, d = lane & 3;
-          uint32_t blk = lds.mb[slot][t][4 + d];
-          if (p >= 1) {
-            const int ps = (p - 1) % kMc2Slots;
-            blk = mc3_block_update_c(lds.tab, blk, lds.mb[slot][t], lds.sp[ps], lds.rp[ps], 4 * p, lane);
-          }
-          MC2_STAMP(4 * p + 2);
-          uint32_t sval = 0;
-          int srow = 0;
-          const bool inv_ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
-          if (inv_ok) lds.sp[slot][srow][d] = sval;
-          if (!inv_ok) {
-            __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            __hip_atomic_store(base + 16 * 64 + srow * 4 + d, ((unsigned long long)epoch << 32) | sval,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            unpublished = p + 1;
-          }
-          MC2_STAMP(4 * p + 3);
-        }
-        if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-        mc2_signal(&lds.chain_cnt, lane);
-      } else {
-        // another workgroup's panel: R_p (rows 2cw, 2cw + 1) and S_p (wave 0) into LDS
-        const gu64* src = base + (size_t)(2 * cw) * 64 + lane;
-        uint64_t a = 0, b = 0, s = 0;
-        bool seen_fail = false, timeout = false;
-        for (int spins = 0;; spins++) {
-          a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          b = __hip_atomic_load(src + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (cw == 0) s = __hip_atomic_load(base + 16 * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t ta = (uint32_t)(a >> 32), tb2 = (uint32_t)(b >> 32), ts = cw == 0 ? (uint32_t)(s >> 32) : epoch;
-          const bool okv = (ta & ~kMcFail) == epoch && (tb2 & ~kMcFail) == epoch && (ts & ~kMcFail) == epoch;
-          const bool anyfail = __builtin_amdgcn_ballot_w64(((ta == (epoch | kMcFail)) | (tb2 == (epoch | kMcFail)) |
-                                                            (ts == (epoch | kMcFail)))) != 0;
-          if (anyfail) {
-            seen_fail = true;
-            break;
-          }
-          if (__builtin_amdgcn_ballot_w64(!okv) == 0) break;
-          if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            seen_fail = true;
-            break;
-          }
-          if (spins > kMcSpinMax) {
-            timeout = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (seen_fail || timeout) {
-          __hip_atomic_store(&lds.fail, timeout ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          break;
-        }
-        if (cw == 0) MC2_STAMP(4 * p + 1);
-        if (!mc2_wait(lds, &lds.rows_done, 8 * p)) break;  // the slot's last readers are done
-        if (cw == 0) MC2_STAMP(4 * p + 2);
-        lds.rp[slot][2 * cw][lane] = (uint32_t)a;
-        lds.rp[slot][2 * cw + 1][lane] = (uint32_t)b;
-        if (cw == 0) lds.sp[slot][lane >> 2][lane & 3] = (uint32_t)s;
-        mc2_signal(&lds.chain_cnt, lane);
-        if (cw == 0) MC2_STAMP(4 * p + 3);
-      }
-    }
-    ok = __hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
-    if (!ok && cw == 0) {
-      // owned panels whose S_p is not out: FAIL on R_p and S_p, so that
-      // every later workgroup stops too
-      for (int p = unpublished; p < 2 * q + 2 && p < NP; p++) {
-        gu64* base = pub + (size_t)p * kMc2PanelGran;
-        for (int r = 0; r < 16; r++)
-          __hip_atomic_store(base + r * 64 + lane, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(base + 16 * 64 + lane, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    };
+    attempt(mc_opaque_s(q), mc_opaque_s(w), mc_opaque(lane), mc_opaque_s(pub));
+    __syncthreads();  // every wave read lds.fail before the next attempt resets it
+    if (fail != 1 || att + 1 == kMcAttempts) break;
   }
+  const bool ok = fail == 0;
   if (w == 0) MC2_STAMP(83);
 #undef MC2_STAMP
+  if (!ok && tid == 0) mc_put_fail(pubA, tag0, tlast, 2);  // late workgroups read no input
   if (args.direct) __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
   __syncthreads();
   if (tid == 0) {
+    const uint32_t tg = late ? tlast : tag0 + att;
     if (args.direct) {
       __atomic_thread_fence(__ATOMIC_RELEASE);
-      __hip_atomic_store(&args.counts[g * P + q], (int)(lds.fail == 0 ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
+      __hip_atomic_store(&args.counts[g * P + q], (int)(ok ? tg : tg | kMcFail), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
-      args.counts[g * P + q] = lds.fail == 0 ? 1 : 0;
+      args.counts[g * P + q] = ok ? 1 : 0;
     }
   }
   // the device copy of T after the system-scope release (as in mc4)
-  if (w < 8 && args.out_dev && lds.fail == 0)
+  if (w < 8 && args.out_dev && ok)
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       const int gr = 32 * q + 4 * w + i;
-      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R_out[i], lane, k);
+      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, Tout[i], lane, k);
     }
 }
 
@@ -1224,10 +1360,11 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
 // The row data the chain needs for panel p leaves the row workgroups one
 // panel earlier (after apply(p - 2)), so the chain waits on them only when a
 // row workgroup's hand-off and apply take longer than one chain step.
-// Hand-offs are 8-byte {data, epoch} granules (agent-scope relaxed stores,
-// polled with agent-scope loads), as in mc / mc2; a singular block publishes
+// Hand-offs are 8-byte {data, tag} granules (agent-scope relaxed stores,
+// polled with agent-scope loads), as in mc2; a singular block publishes
 // FAIL on every later S_p, and a workgroup that sees FAIL publishes FAIL on
-// its own slots and stops, so every workgroup ends; spins are bounded.
+// its own slots and starts the next attempt (or stops), so every workgroup
+// ends; waits are bounded.
 // Results are direct only: T rows into out (pinned host memory) and one
 // status word per workgroup, counts[g * (NP + 1) + x].
 constexpr int kMc4Threads = 256;
@@ -1244,7 +1381,7 @@ struct ElimMc4Lds {
   uint32_t crq[2][16][4];   // chain: R_{p-1}'s panel-p columns
   uint4 csel[2][16][4];     // chain: selectors (sel0, sel1, sel2) of S_p's dwords, slot p % 2
   uint4 crsel[2][16][4];    // chain: selectors of the staged R_{p-1} columns
-  int staged, consumed, fail;
+  int staged, consumed, fail, late;
 };
 
 __device__ __forceinline__ size_t mc4_pub_words(int NP) {
@@ -1252,33 +1389,34 @@ __device__ __forceinline__ size_t mc4_pub_words(int NP) {
 }
 
 // polls N granules per lane (at src[i * stride]) until every tag is this
-// launch's epoch: 0 (values in v), 1 a FAIL tag (or the workgroup's fail
-// word) seen, 2 timeout
+// attempt's: 0 (values in v), 1 this attempt failed (a FAIL or a later tag
+// seen, or the workgroup's fail word 1), 2 abort (an abort, a timeout, or
+// the fail word 2)
 template <int N>
-__device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t epoch, uint32_t* v, const int* lfail) {
+__device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t tag, uint32_t tlast, uint32_t* v,
+                                        const int* lfail) {
   for (int spins = 0;; spins++) {
-    bool okv = true, anyf = false;
+    bool okv = true, f1 = false, f2 = false;
+    uint64_t x[N];
+#pragma unroll
+    for (int i = 0; i < N; i++)  // every load in flight before the first wait
+      x[i] = __hip_atomic_load(src + (size_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (int i = 0; i < N; i++) {
-      const uint64_t x = __hip_atomic_load(src + (size_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t tg = (uint32_t)(x >> 32);
-      okv = okv && tg == epoch;
-      anyf = anyf || tg == (epoch | kMcFail);
-      v[i] = (uint32_t)x;
+      const int s = mc_tag_state(x[i], tag, tlast);
+      okv = okv && s == 0;
+      f1 = f1 || s == 1;
+      f2 = f2 || s == 2;
+      v[i] = (uint32_t)x[i];
     }
-    if (__builtin_amdgcn_ballot_w64(anyf)) return 1;
+    if (__builtin_amdgcn_ballot_w64(f2)) return 2;
+    if (__builtin_amdgcn_ballot_w64(f1)) return 1;
     if (__builtin_amdgcn_ballot_w64(!okv) == 0) return 0;
-    if (lfail && __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return 1;
-    if (spins > kMcSpinMax) return 2;
+    if (lfail)
+      if (const int lf = __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return lf;
+    if (spins > kMcPollSpins) return 2;
     __builtin_amdgcn_s_sleep(1);
   }
-}
-
-__device__ __forceinline__ void mc4_put(gu64* dst, uint32_t epoch, uint32_t v) {
-  __hip_atomic_store(dst, ((unsigned long long)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void mc4_put_fail(gu64* dst, uint32_t epoch) {
-  __hip_atomic_store(dst, (unsigned long long)(epoch | kMcFail) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // waits for an LDS counter of the mc4 chain workgroup (bounded; false on a
@@ -1287,8 +1425,8 @@ __device__ __forceinline__ bool mc4_wait(int* ctr, int target, int* lfail) {
   for (int spins = 0;; spins++) {
     if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
     if (__hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-    if (spins > 64 * kMcSpinMax) {
-      __hip_atomic_store(lfail, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (spins > kMcLdsSpins) {
+      mc_set_fail(lfail, 2);
       return false;
     }
   }
@@ -1345,11 +1483,9 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = args.k;
-  const uint32_t epoch = args.epoch;
-  gu64* const base = (gu64*)args.pub + (size_t)g * mc4_pub_words(NP);
-  gu64* const pubS = base;
-  gu64* const pubR = base + (size_t)NP * kMc4SGran;
-  gu64* const pubM = pubR + (size_t)NP * kMc4RGran;
+  const uint32_t tag0 = args.epoch, tlast = tag0 + kMcAttempts - 1;
+  gu64* const pubS = (gu64*)args.pub + (size_t)g * mc4_pub_words(NP);  // then R and M slots (attempt)
+  gu64* const pubA = (gu64*)args.pub + (size_t)gridDim.y * mc4_pub_words(NP) + g;  // the decoder's abort granule
   const bool chain = x == NRW;
 #ifdef KODR_ELIM_TIMING
   // tuning build: s_memrealtime stamps by lane 0 into workgroup x's 1 KiB of
@@ -1369,6 +1505,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
   } while (0)
 #endif
   if (w == 0) MC4_STAMP(96);
+  const uint64_t ab = tid == 0 ? __hip_atomic_load(pubA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   for (int i = tid; i < 256 * 2; i += kMc4Threads) {
     const uint32_t* a = args.tables + 4 * i;
     lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
@@ -1377,260 +1514,274 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
       lds.itab[i] = make_uint4(b[0], b[1], b[2], b[3]);
     }
   }
-  if (tid == 0) {
-    lds.staged = 0;
-    lds.consumed = 0;
-    lds.fail = 0;
-  }
+  if (tid == 0) lds.late = mc_tag_state(ab, tag0, tlast) == 2;
   __syncthreads();
+  const bool late = __builtin_amdgcn_readfirstlane(lds.late) != 0;
   if (w == 0) MC4_STAMP(97);
 
-  if (chain) {
-    const int t = lane >> 2, d = lane & 3;
-    if (w == 1) {
-      // ---- staging wave: MB_p and R_{p-1}'s panel-p columns into LDS ----
-      for (int p = 0; p < NP; p++) {
-        const int slot = p & 1;
-        if (p >= 2 && !mc4_wait(&lds.consumed, p - 1, &lds.fail)) break;  // the slot's last readers are done
-        uint32_t v[2];
-        int st = 0;
-        // dword dw of original row gr (rows past k: identity padding)
-        auto orig = [&](int gr, int dw) -> uint32_t {
-          if (gr >= k) return gr >> 2 == dw ? 1u << (8 * (gr & 3)) : 0u;
-          const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
-          uint32_t o = 0;
-#pragma unroll
-          for (int b = 0; b < 4; b++)
-            if (4 * dw + b < k) o |= (uint32_t)src[4 * dw + b] << (8 * b);
-          return o;
-        };
-        if (p == 0) {  // panels 0 and 1 start from the input rows ("as of -1"): no hand-off
-          lds.cmb[slot][t][4 + d] = orig(t, d);
-        } else if (p == 1) {
-          lds.cmb[slot][t][d] = orig(16 + t, d);
-          lds.cmb[slot][t][4 + d] = orig(16 + t, 4 + d);
-          const uint32_t rq = orig(t, 4 + d);
-          lds.crq[slot][t][d] = rq;
-          lds.crsel[slot][t][d] = mc4_sel(rq);
-        } else {
-          const gu64* mb = pubM + (size_t)p * kMc4MGran + t * 8 + d;
-          st = mc4_poll<2>(mb, 4, epoch, v, &lds.fail);
-          if (st == 0) {
-            lds.cmb[slot][t][d] = v[0];
-            lds.cmb[slot][t][4 + d] = v[1];
-            st = mc4_poll<1>(pubR + (size_t)(p - 1) * kMc4RGran + t * 64 + 4 * p + d, 0, epoch, v, &lds.fail);
-            if (st == 0) {
-              lds.crq[slot][t][d] = v[0];
-              lds.crsel[slot][t][d] = mc4_sel(v[0]);
-            }
-          }
-        }
-        if (st) {
-          __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          break;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&lds.staged, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        MC4_STAMP(48 + p);
-      }
-      return;
-    }
-    // ---- wave 0: update the block, invert it, publish S_p ----
-    if (w != 0) return;
-    __builtin_amdgcn_s_setprio(3);
-    int p = 0;
-    for (; p < NP; p++) {
-      const int slot = p & 1;
-      if (!mc4_wait(&lds.staged, p + 1, &lds.fail)) break;
-      MC4_STAMP(p);
-      uint32_t blk = lds.cmb[slot][t][4 + d];
-      if (p >= 1)
-        blk = mc4_block_update_s(lds.tab, blk, lds.cmb[slot][t], lds.csel[slot ^ 1], lds.crsel[slot], lane);
-      MC4_STAMP(16 + p);
-      uint32_t sval = 0;
-      int srow = 0;
-      if (!mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow)) {
-        __hip_atomic_store(&lds.fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        break;
-      }
-      mc4_put(pubS + (size_t)p * kMc4SGran + 4 * srow + d, epoch, sval);
-      lds.csel[slot][srow][d] = mc4_sel(sval);
-      MC4_STAMP(32 + p);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&lds.consumed, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-#ifdef KODR_ELIM_TIMING
-    const bool ok = false;
-#else
-    const bool ok = p == NP;
-#endif
-    for (int q = p; q < NP; q++) mc4_put_fail(pubS + (size_t)q * kMc4SGran + lane, epoch);  // every later S_p
-    if (lane == 0) {
-      __atomic_thread_fence(__ATOMIC_RELEASE);
-      __hip_atomic_store(&args.counts[g * (NRW + 1) + NRW], (int)(ok ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    return;
-  }
-
-  // ================= row workgroup x: rows RW x + RPW w + i =================
-  const int row0 = RW * x, pr = row0 / 16, lo = row0 - 16 * pr;  // its panel, offset in it
-  uint32_t R[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; i++) {
-    const int gr = row0 + RPW * w + i;
-    uint32_t v = 0;
-    if (gr < k) {
-      const uint8_t* src = args.vecs[g] + (size_t)gr * args.vpitch;
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if (4 * lane + b < k) v |= (uint32_t)src[4 * lane + b] << (8 * b);
-    } else if (gr >> 2 == lane) {
-      v = 1u << (8 * (gr & 3));  // padding rows: identity (the matrix stays [[C, 0], [0, I]])
-    }
-    R[i] = v;
-  }
-  // what the workgroup owes after apply(j) (j = -1: the loaded rows)
-  auto publish = [&](int j) {
-    const int lr = lo + RPW * w;  // local row (in the panel) of R[0]
-    if (pr == j + 1) {  // R_pr: the panel's rows as of pr - 1
-      gu64* dst = pubR + (size_t)pr * kMc4RGran + lr * 64 + lane;
-#pragma unroll
-      for (int i = 0; i < RPW; i++) mc4_put(dst + i * 64, epoch, R[i]);
-    }
-    if (pr == j + 2) {  // MB_pr: columns of panels pr - 1 and pr as of pr - 2
-      const int u = lane - 4 * (pr - 1);
-      if (u >= 0 && u < 8) {
-        gu64* dst = pubM + (size_t)pr * kMc4MGran + lr * 8 + u;
-#pragma unroll
-        for (int i = 0; i < RPW; i++) mc4_put(dst + i * 8, epoch, R[i]);
-      }
-    }
-  };
-  publish(-1);
-  int j = 0;
-  for (; j < NP; j++) {
-    // R_j (all 16 rows, from the hand-off slots, this workgroup's own
-    // included) and S_j into LDS: wave w polls rows 4 w .. 4 w + 3, wave 0 S_j
-    {
-      uint32_t v[4];
-      const int st = mc4_poll<4>(pubR + (size_t)j * kMc4RGran + (4 * w) * 64 + lane, 64, epoch, v, &lds.fail);
-      if (st) {
-        __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) lds.rp[4 * w + i][lane] = v[i];
-      }
-    }
-    if (w == 0) {
-      uint32_t v[1];
-      const int st = mc4_poll<1>(pubS + (size_t)j * kMc4SGran + lane, 0, epoch, v, &lds.fail);
-      if (st)
-        __hip_atomic_store(&lds.fail, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      else
-        lds.sp[lane >> 2][lane & 3] = v[0];
+  const int row0 = RW * x, pr = row0 / 16, lo = row0 - 16 * pr;  // row workgroup: its panel, offset in it
+  uint32_t Tout[RPW];  // row workgroup: T rows of the successful attempt (assigned on the way out)
+  int fail = late ? 2 : 0, att = 0;
+  for (; !late; att++) {
+    const uint32_t tag = tag0 + att;
+    const int rot = mc_rot(att, k);
+    if (tid == 0) {
+      __hip_atomic_store(&lds.staged, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&lds.consumed, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&lds.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
-    if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-    if (w == 0) MC4_STAMP(j);
-    // apply(j): the panel's own rows become S_j x R_j with S_j in the panel
-    // columns; the others take F = (panel-j bytes) x S_j, row ^= F x R_j,
-    // panel columns := F
-    const int db = 4 * j;
-    const bool own = pr == j;
-    const uint32_t(*Gp)[4] = own ? &lds.sp[lo + RPW * w] : lds.fw[w];
-    if (!own) {
-      // F of the RPW rows: lane (cg, i, u) sums terms c in group cg (16 / G
-      // of them), the G groups folded by ds_bpermute
-      constexpr int G = 16 / RPW, TPG = 16 / G;  // groups, terms per group
-      if (lane >= db && lane < db + 4)
+    // the attempt, on opaque copies of the indices (mc_opaque)
+    auto attempt = [&](const int g, const int w, const int lane, gu64* const pubS) {
+    gu64* const pubR = pubS + (size_t)NP * kMc4SGran;
+    gu64* const pubM = pubR + (size_t)NP * kMc4RGran;
+    int pfail = NP;  // chain wave 0: the first S_p not published
+    uint32_t R[RPW];
 #pragma unroll
-        for (int i = 0; i < RPW; i++) lds.mw[w][i][lane - db] = R[i];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      const int u = lane & 3, i = (lane >> 2) % RPW, cg = (lane >> 2) / RPW;
-      uint32_t acc = 0;
+    for (int i = 0; i < RPW; i++) R[i] = 0u;
+    if (chain) {
+      const int t = lane >> 2, d = lane & 3;
+      if (w == 1) {
+        // ---- staging wave: MB_p and R_{p-1}'s panel-p columns into LDS ----
+        for (int p = 0; p < NP; p++) {
+          const int slot = p & 1;
+          if (p >= 2 && !mc4_wait(&lds.consumed, p - 1, &lds.fail)) break;  // the slot's last readers are done
+          uint32_t v[2];
+          int st = 0;
+          // dword dw of row gr (rows past k: identity padding)
+          auto orig = [&](int gr, int dw) -> uint32_t {
+            if (gr >= k) return gr >> 2 == dw ? 1u << (8 * (gr & 3)) : 0u;
+            const uint8_t* src = args.vecs[g] + (size_t)mc_src_row(gr, k, rot) * args.vpitch;
+            uint32_t o = 0;
 #pragma unroll
-      for (int cc = 0; cc < TPG; cc++) {
-        const int c = TPG * cg + cc;
-        const uint32_t m = (lds.mw[w][i][c >> 2] >> (8 * (c & 3))) & 0xffu;
-        const uint4 tt = lds.tab[2 * m];
-        const uint32_t tt2 = lds.tab[2 * m + 1].x;
-        const uint32_t xv = lds.sp[c][u];
-        acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
-      }
-#pragma unroll
-      for (int sft = 4 * RPW; sft < 64; sft <<= 1) acc ^= bperm(acc, lane ^ sft);
-      if (lane < 4 * RPW) lds.fw[w][i][u] = acc;
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-    }
-    uint32_t acc[RPW];
-#pragma unroll
-    for (int i = 0; i < RPW; i++) acc[i] = own ? 0u : R[i];
-#pragma unroll
-    for (int cq = 0; cq < 4; cq++) {
-      uint32_t gw[RPW];
-#pragma unroll
-      for (int i = 0; i < RPW; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
-      uint4 tt[4][RPW];
-      uint32_t t2[4][RPW], xs[4];
-#pragma unroll
-      for (int cc = 0; cc < 4; cc++) {
-        xs[cc] = lds.rp[4 * cq + cc][lane];
-#pragma unroll
-        for (int i = 0; i < RPW; i++) {
-          const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
-          tt[cc][i] = lds.tab[2 * f];
-          t2[cc][i] = lds.tab[2 * f + 1].x;
+            for (int b = 0; b < 4; b++)
+              if (4 * dw + b < k) o |= (uint32_t)src[4 * dw + b] << (8 * b);
+            return o;
+          };
+          if (p == 0) {  // panels 0 and 1 start from the input rows ("as of -1"): no hand-off
+            lds.cmb[slot][t][4 + d] = orig(t, d);
+          } else if (p == 1) {
+            lds.cmb[slot][t][d] = orig(16 + t, d);
+            lds.cmb[slot][t][4 + d] = orig(16 + t, 4 + d);
+            const uint32_t rq = orig(t, 4 + d);
+            lds.crq[slot][t][d] = rq;
+            lds.crsel[slot][t][d] = mc4_sel(rq);
+          } else {
+            const gu64* mb = pubM + (size_t)p * kMc4MGran + t * 8 + d;
+            st = mc4_poll<2>(mb, 4, tag, tlast, v, &lds.fail);
+            if (st == 0) {
+              lds.cmb[slot][t][d] = v[0];
+              lds.cmb[slot][t][4 + d] = v[1];
+              st = mc4_poll<1>(pubR + (size_t)(p - 1) * kMc4RGran + t * 64 + 4 * p + d, 0, tag, tlast, v,
+                               &lds.fail);
+              if (st == 0) {
+                lds.crq[slot][t][d] = v[0];
+                lds.crsel[slot][t][d] = mc4_sel(v[0]);
+              }
+            }
+          }
+          if (st) {
+            mc_set_fail(&lds.fail, st);
+            break;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store(&lds.staged, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          MC4_STAMP(48 + p);
         }
+      } else if (w == 0) {
+        // ---- wave 0: update the block, invert it, publish S_p ----
+        __builtin_amdgcn_s_setprio(3);
+        int p = 0;
+        for (; p < NP; p++) {
+          const int slot = p & 1;
+          if (!mc4_wait(&lds.staged, p + 1, &lds.fail)) break;
+          MC4_STAMP(p);
+          uint32_t blk = lds.cmb[slot][t][4 + d];
+          if (p >= 1)
+            blk = mc4_block_update_s(lds.tab, blk, lds.cmb[slot][t], lds.csel[slot ^ 1], lds.crsel[slot], lane);
+          MC4_STAMP(16 + p);
+          uint32_t sval = 0;
+          int srow = 0;
+          if (!mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow)) {
+            mc_set_fail(&lds.fail, mc_singular_why(blk, lane, p, k));
+            break;
+          }
+          mc_put(pubS + (size_t)p * kMc4SGran + 4 * srow + d, tag, sval);
+          lds.csel[slot][srow][d] = mc4_sel(sval);
+          MC4_STAMP(32 + p);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store(&lds.consumed, p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        pfail = p;
+        __builtin_amdgcn_s_setprio(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      // ================= row workgroup x: rows RW x + RPW w + i =================
 #pragma unroll
-      for (int cc = 0; cc < 4; cc++) {
-        const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+      for (int i = 0; i < RPW; i++) R[i] = mc_load_row(args, g, row0 + RPW * w + i, rot, lane);
+      // what the workgroup owes after apply(j) (j = -1: the loaded rows)
+      auto publish = [&](int j) {
+        const int lr = lo + RPW * w;  // local row (in the panel) of R[0]
+        if (pr == j + 1) {  // R_pr: the panel's rows as of pr - 1
+          gu64* dst = pubR + (size_t)pr * kMc4RGran + lr * 64 + lane;
 #pragma unroll
-        for (int i = 0; i < RPW; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
+          for (int i = 0; i < RPW; i++) mc_put(dst + i * 64, tag, R[i]);
+        }
+        if (pr == j + 2) {  // MB_pr: columns of panels pr - 1 and pr as of pr - 2
+          const int u = lane - 4 * (pr - 1);
+          if (u >= 0 && u < 8) {
+            gu64* dst = pubM + (size_t)pr * kMc4MGran + lr * 8 + u;
+#pragma unroll
+            for (int i = 0; i < RPW; i++) mc_put(dst + i * 8, tag, R[i]);
+          }
+        }
+      };
+      publish(-1);
+      for (int j = 0; j < NP; j++) {
+        // R_j (all 16 rows, from the hand-off slots, this workgroup's own
+        // included) and S_j into LDS: wave w polls rows 4 w .. 4 w + 3, wave 0 S_j
+        {
+          uint32_t v[4];
+          const int st =
+              mc4_poll<4>(pubR + (size_t)j * kMc4RGran + (4 * w) * 64 + lane, 64, tag, tlast, v, &lds.fail);
+          if (st) {
+            mc_set_fail(&lds.fail, st);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds.rp[4 * w + i][lane] = v[i];
+          }
+        }
+        if (w == 0) {
+          uint32_t v[1];
+          const int st = mc4_poll<1>(pubS + (size_t)j * kMc4SGran + lane, 0, tag, tlast, v, &lds.fail);
+          if (st)
+            mc_set_fail(&lds.fail, st);
+          else
+            lds.sp[lane >> 2][lane & 3] = v[0];
+        }
+        __syncthreads();
+        if (__hip_atomic_load(&lds.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        if (w == 0) MC4_STAMP(j);
+        // apply(j): the panel's own rows become S_j x R_j with S_j in the panel
+        // columns; the others take F = (panel-j bytes) x S_j, row ^= F x R_j,
+        // panel columns := F
+        const int db = 4 * j;
+        const bool own = pr == j;
+        const uint32_t(*Gp)[4] = own ? &lds.sp[lo + RPW * w] : lds.fw[w];
+        if (!own) {
+          // F of the RPW rows: lane (cg, i, u) sums terms c in group cg (16 / G
+          // of them), the G groups folded by ds_bpermute
+          constexpr int G = 16 / RPW, TPG = 16 / G;  // groups, terms per group
+          if (lane >= db && lane < db + 4)
+#pragma unroll
+            for (int i = 0; i < RPW; i++) lds.mw[w][i][lane - db] = R[i];
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          const int u = lane & 3, i = (lane >> 2) % RPW, cg = (lane >> 2) / RPW;
+          uint32_t acc = 0;
+#pragma unroll
+          for (int cc = 0; cc < TPG; cc++) {
+            const int c = TPG * cg + cc;
+            const uint32_t m = (lds.mw[w][i][c >> 2] >> (8 * (c & 3))) & 0xffu;
+            const uint4 tt = lds.tab[2 * m];
+            const uint32_t tt2 = lds.tab[2 * m + 1].x;
+            const uint32_t xv = lds.sp[c][u];
+            acc ^= gmul4(tt, tt2, sel0(xv), sel1(xv), sel2(xv));
+          }
+#pragma unroll
+          for (int sft = 4 * RPW; sft < 64; sft <<= 1) acc ^= bperm(acc, lane ^ sft);
+          if (lane < 4 * RPW) lds.fw[w][i][u] = acc;
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+        }
+        uint32_t acc[RPW];
+#pragma unroll
+        for (int i = 0; i < RPW; i++) acc[i] = own ? 0u : R[i];
+#pragma unroll
+        for (int cq = 0; cq < 4; cq++) {
+          uint32_t gw[RPW];
+#pragma unroll
+          for (int i = 0; i < RPW; i++) gw[i] = __builtin_amdgcn_readfirstlane(Gp[i][cq]);
+          uint4 tt[4][RPW];
+          uint32_t t2[4][RPW], xs[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            xs[cc] = lds.rp[4 * cq + cc][lane];
+#pragma unroll
+            for (int i = 0; i < RPW; i++) {
+              const uint32_t f = (gw[i] >> (8 * cc)) & 0xffu;
+              tt[cc][i] = lds.tab[2 * f];
+              t2[cc][i] = lds.tab[2 * f + 1].x;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int cc = 0; cc < 4; cc++) {
+            const uint32_t s0 = sel0(xs[cc]), s1 = sel1(xs[cc]), s2 = sel2(xs[cc]);
+#pragma unroll
+            for (int i = 0; i < RPW; i++) acc[i] ^= mc_mul(tt[cc][i], t2[cc][i], s0, s1, s2);
+          }
+        }
+        const int u = lane - db;
+#pragma unroll
+        for (int i = 0; i < RPW; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
+        publish(j);
+        if (w == 0) MC4_STAMP(16 + j);
+        __syncthreads();  // rp / sp / mw / fw are rewritten next iteration
       }
     }
-    const int u = lane - db;
-#pragma unroll
-    for (int i = 0; i < RPW; i++) R[i] = (u >= 0 && u < 4) ? Gp[i][u & 3] : acc[i];
-    publish(j);
-    if (w == 0) MC4_STAMP(16 + j);
-    __syncthreads();  // rp / sp / mw / fw are rewritten next iteration
-  }
+    __syncthreads();
+    fail = lds.fail;
 #ifdef KODR_ELIM_TIMING
-  j = -1;  // the stamps overwrote T: report failure, kodr's route on the host
+    if (!fail) fail = 2;  // the stamps overwrote T: report failure, kodr's route on the host
 #endif
-  const bool ok = j == NP;
-  if (!ok) {  // every slot this workgroup still owes (or has put) gets FAIL, so its consumers stop
-    const int lr = lo + RPW * w;
-    for (int i = 0; i < RPW; i++) mc4_put_fail(pubR + (size_t)pr * kMc4RGran + (lr + i) * 64 + lane, epoch);
-    if (pr >= 1 && lane < 8)
-      for (int i = 0; i < RPW; i++) mc4_put_fail(pubM + (size_t)pr * kMc4MGran + (lr + i) * 8 + lane, epoch);
-  } else {
-    uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
-#pragma unroll
-    for (int i = 0; i < RPW; i++) {
-      const int gr = row0 + RPW * w + i;
-      if (gr >= k) continue;
-      mc_store_row(out + (size_t)gr * args.out_pitch, R[i], lane, k);
+    if (fail) {
+      if (chain) {
+        // every S_p not out yet (an abort: all of them), so that every row workgroup stops
+        if (w == 0)
+          for (int p = fail >= 2 ? 0 : pfail; p < NP; p++) mc_put_fail(pubS + (size_t)p * kMc4SGran + lane, tag, tlast, fail);
+      } else {
+        // every slot this workgroup owes (or has put) gets FAIL, so its consumers stop
+        const int lr = lo + RPW * w;
+        for (int i = 0; i < RPW; i++)
+          mc_put_fail(pubR + (size_t)pr * kMc4RGran + (lr + i) * 64 + lane, tag, tlast, fail);
+        if (pr >= 1 && lane < 8)
+          for (int i = 0; i < RPW; i++) mc_put_fail(pubM + (size_t)pr * kMc4MGran + (lr + i) * 8 + lane, tag, tlast, fail);
+      }
+      // the FAILs reach L2 before any store of the next attempt to the same slots
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
+    if (!fail && !chain) {
+      // T = T' Pi: the rotation undone (lds.rp is free after the last barrier)
+      uint8_t* out = args.out + (size_t)g * args.out_gen_stride;
+#pragma unroll
+      for (int i = 0; i < RPW; i++) {
+        Tout[i] = rot ? mc_unrotate(R[i], &lds.rp[w][0], lane, k, rot) : R[i];
+        const int gr = row0 + RPW * w + i;
+        if (gr < k) mc_store_row(out + (size_t)gr * args.out_pitch, Tout[i], lane, k);
+      }
+    }
+    };
+    attempt(mc_opaque_s(g), mc_opaque_s(w), mc_opaque(lane), mc_opaque_s(pubS));
+    __syncthreads();  // every wave read lds.fail before the next attempt resets it
+    if (fail != 1 || att + 1 == kMcAttempts) break;
   }
+  const bool ok = fail == 0;
+  if (!ok && tid == 0) mc_put_fail(pubA, tag0, tlast, 2);  // late workgroups read no input
   __atomic_thread_fence(__ATOMIC_RELEASE);  // this wave's T rows reach (host) memory first
   __syncthreads();
   if (tid == 0) {
+    const uint32_t tg = late ? tlast : tag0 + att;
     __atomic_thread_fence(__ATOMIC_RELEASE);
-    __hip_atomic_store(&args.counts[g * (NRW + 1) + x], (int)(ok ? epoch : epoch | kMcFail), __ATOMIC_RELAXED,
+    __hip_atomic_store(&args.counts[g * (NRW + 1) + x], (int)(ok ? tg : tg | kMcFail), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // the device copy of T after the system-scope releases: written before
   // them, its dirty lines made every wave's release write back L2 (mc2 with
   // 16 decoders 280 -> 890 us); later kernels see it at the launch boundary
-  if (ok && x < NRW && args.out_dev)
+  if (ok && !chain && args.out_dev)
 #pragma unroll
     for (int i = 0; i < RPW; i++) {
       const int gr = row0 + RPW * w + i;
-      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, R[i], lane, k);
+      if (gr < k) mc_store_row(args.out_dev + ((size_t)g * k + gr) * k, Tout[i], lane, k);
     }
 #undef MC4_STAMP
 }
@@ -1684,7 +1835,7 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
   // every batch full (n >= k) and k large enough for panels to pay
   bool full = args.k >= kElimBlockedMinK;
   for (int i = 0; i < G && full; i++) full = args.n[i] >= args.k;
-  if (const char* e = getenv("KODR_ELIM_BLOCKED")) full = full && atoi(e) != 0;  // A/B measurements
+  if (const char* e = tune_env("KODR_ELIM_BLOCKED")) full = full && atoi(e) != 0;  // A/B measurements
   return full;
 }
 
@@ -1694,7 +1845,7 @@ bool gf_elim_blocked(const ElimArgs& args, int G) {
 // workgroups) else mc2 (measured: profiles/r04/elim_modes/)
 static int elim_mc_mode() {
   static const int mc = [] {
-    const int m = getenv("KODR_ELIM_MC") ? atoi(getenv("KODR_ELIM_MC")) : 3;
+    const int m = tune_env("KODR_ELIM_MC") ? atoi(tune_env("KODR_ELIM_MC")) : 3;
     return m == 0 || m == 2 || m == 4 ? m : 3;
   }();
   return mc;
@@ -1703,7 +1854,7 @@ static int elim_mc_mode() {
 // mc4 rows per row wave (KODR_MC4_RPW: 4 = 16 rows per row workgroup, 2
 // (default) = 8)
 static int mc4_rows_per_wave() {
-  static const int rpw = getenv("KODR_MC4_RPW") && atoi(getenv("KODR_MC4_RPW")) == 4 ? 4 : 2;
+  static const int rpw = tune_env("KODR_MC4_RPW") && atoi(tune_env("KODR_MC4_RPW")) == 4 ? 4 : 2;
   return rpw;
 }
 static int mc4_groups(int k) { return (k + 15) / 16 * (16 / (4 * mc4_rows_per_wave())) + 1; }
@@ -1732,11 +1883,14 @@ bool gf_elim_mc_direct(const ElimArgs& args, int G) {
   return gf_elim_mc_taken(args, G) && (m == 2 || m == 4);
 }
 
+// the hand-off granules of G decoders, then one abort granule per decoder
 size_t gf_elim_mc_pub_bytes(int k, int G) {
-  if (mc_kernel_for(k, G) == 4) return (size_t)G * (size_t)((k + 15) / 16) * (kMc4SGran + kMc4RGran + kMc4MGran) * 8;
+  if (mc_kernel_for(k, G) == 4)
+    return ((size_t)G * (size_t)((k + 15) / 16) * (kMc4SGran + kMc4RGran + kMc4MGran) + (size_t)G) * 8;
   const size_t P = (size_t)mc2_groups(k);
-  return (size_t)G * std::max<size_t>(P * 32 * 64, 2 * P * kMc2PanelGran) * 8;
+  return ((size_t)G * 2 * P * kMc2PanelGran + (size_t)G) * 8;
 }
+int gf_elim_mc_attempts() { return kMcAttempts; }
 
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
@@ -1745,9 +1899,11 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
     const dim3 grid(gf_elim_mc_groups(args.k, G), G);
     if (m == 4) {
       if (!args.direct) return hipErrorInvalidValue;  // mc4 reports directly only
+#ifdef KODR_TUNE
       if (mc4_rows_per_wave() == 4)
         hipLaunchKernelGGL(gf_elim_mc4_kernel<4>, grid, dim3(kMc4Threads), 0, stream, args);
       else
+#endif
         hipLaunchKernelGGL(gf_elim_mc4_kernel<2>, grid, dim3(kMc4Threads), 0, stream, args);
     } else {
       hipLaunchKernelGGL(gf_elim_mc2_kernel, grid, dim3(1024), 0, stream, args);
@@ -1763,7 +1919,7 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   // (a row-per-lane layout of the same algorithm -- one LDS gather per
   // multiplier serving 64 rows, pivot rows as scalars -- measured slower too:
   // 536 vs 493 us at k = 256, profiles/r02/elim/elim_rows_ab.log)
-  static const int circ = getenv("KODR_ELIM_CIRC") ? atoi(getenv("KODR_ELIM_CIRC")) : 1;
+  static const int circ = tune_env("KODR_ELIM_CIRC") ? atoi(tune_env("KODR_ELIM_CIRC")) : 1;
   if (full && circ)
     hipLaunchKernelGGL(gf_elim_circ_kernel, dim3(G), dim3(64 * kElimWaves), 0, stream, args);
   else if (full && args.k <= 128)

@@ -29,6 +29,7 @@
 
 #include "gf_device.hpp"
 #include "gf_kernels.hpp"
+#include "tune.hpp"
 
 namespace kodr_amd {
 
@@ -767,7 +768,7 @@ GemmConfig choose_group_config(size_t M, size_t K, size_t ncols, size_t G) {
 
 // KODR_GEMM_CFG="mt,kw,s" forces a tile (tuning runs only; see tools/tune_gemm.py)
 static bool env_config(GemmConfig* g) {
-  const char* s = getenv("KODR_GEMM_CFG");
+  const char* s = tune_env("KODR_GEMM_CFG");
   if (!s || !*s) return false;
   g->p = 0;
   return sscanf(s, "%d,%d,%d,%d", &g->mt, &g->kw, &g->s, &g->p) >= 3;
@@ -781,7 +782,7 @@ static bool env_config(GemmConfig* g) {
 // flight per lane) measured 7.88 / 8.80.  KODR_GEMV=0 selects gf_gemm_kernel,
 // 1 the per-lane tables (A/B measurements).
 static int gemv_enabled() {
-  static const int v = getenv("KODR_GEMV") ? atoi(getenv("KODR_GEMV")) : 2;
+  static const int v = tune_env("KODR_GEMV") ? atoi(tune_env("KODR_GEMV")) : 2;
   return v;
 }
 
@@ -790,7 +791,7 @@ static int gemv_enabled() {
 // gf_gemm_kernel (20 ds_bpermute per step), so 3-8 rows stay there.
 // KODR_GEMV_MULTI=0 keeps gf_gemm_kernel for two rows too (A/B).
 static bool gemv_multi_enabled() {
-  static const bool v = getenv("KODR_GEMV_MULTI") ? atoi(getenv("KODR_GEMV_MULTI")) != 0 : true;
+  static const bool v = tune_env("KODR_GEMV_MULTI") ? atoi(tune_env("KODR_GEMV_MULTI")) != 0 : true;
   return v;
 }
 
@@ -831,7 +832,7 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   const int iM = (int)M, iK = (int)K, ild = (int)lda, inc = (int)ncols;
   int mode = 0;
 #ifdef KODR_TUNE_MODES
-  if (const char* e = getenv("KODR_GEMM_MODE")) mode = atoi(e);
+  if (const char* e = tune_env("KODR_GEMM_MODE")) mode = atoi(e);
   if (mode == 1 && g.mt == 8 && g.kw == 16 && g.s == 2)
     return launch<8, 16, 2, 16, 2, 1>(dA, ild, iM, iK, dX, ldx, dY, ldy, inc, stream);
   if (mode == 2 && g.mt == 8 && g.kw == 16 && g.s == 2)
@@ -852,7 +853,7 @@ hipError_t gf_gemm(const uint8_t* dA, size_t lda, size_t M, size_t K, const uint
   // (KODR_GROUP_AUX in tuning builds)
   int aux = grp ? kGroupAux : 0;
 #ifdef KODR_TUNE_MODES
-  if (const char* e = getenv("KODR_GROUP_AUX")) aux = atoi(e);
+  if (const char* e = tune_env("KODR_GROUP_AUX")) aux = atoi(e);
 #endif
 #define KODR_TRY(MT_, KW_, S_, RC_, P_)                                                         \
   if (g.mt == MT_ && g.kw == KW_ && g.s == S_ && (g.p == 0 || g.p == P_))                       \

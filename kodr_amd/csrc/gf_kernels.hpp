@@ -104,12 +104,14 @@ struct ElimArgs {
   int* counts;
   int k;
   // gf_elim_mc only: the hand-off buffer (gf_elim_mc_pub_bytes, zeroed once
-  // when allocated) and this launch's tag (1 .. 2^31 - 1, a new one per launch)
+  // when allocated) and this launch's first tag: the launch uses tags epoch ..
+  // epoch + gf_elim_mc_attempts() - 1 (one per attempt), all above every tag
+  // an earlier launch on the buffer used, below 2^31
   uint64_t* pub;
   uint32_t epoch;
-  // gf_elim_mc2 only ("direct"): T rows at out + row * out_pitch (no [I]
-  // part), and the status words counts[g * groups + q] = epoch (done) or
-  // epoch | 0x80000000 (failed), stored with system-scope release after the
+  // mc2 / mc4 ("direct"): T rows at out + row * out_pitch (no [I] part), and
+  // the status words counts[g * groups + q] = epoch + a (done in attempt a)
+  // or that | 0x80000000 (failed), stored with system-scope release after the
   // workgroup's T rows, so a host polling pinned memory can read them early
   int direct;
   // mc2 / mc4 only (optional): the T rows of a finished decoder also to
@@ -138,6 +140,9 @@ constexpr int kElimMcMaxBlocks = 256;
 int gf_elim_mc_groups(int k, int G);
 int gf_elim_mc_max_gens(int k);
 size_t gf_elim_mc_pub_bytes(int k, int G);
+// tags per launch: attempts with the rows in another order after a singular
+// panel block (gf_elim.hip, kMcAttempts)
+int gf_elim_mc_attempts();
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 // true when gf_elim_mc_taken and the launch honours args.direct (mc2)
 bool gf_elim_mc_direct(const ElimArgs& args, int G);

@@ -15,6 +15,7 @@ class Context:
         errors.check(lib().rlnc_ctx_create(device, ctypes.c_void_p(stream or 0), ctypes.byref(h)))
         self._h = h
         self.device = device
+        self.route_min_k = 224
 
     @property
     def handle(self):
@@ -26,6 +27,19 @@ class Context:
 
     def synchronize(self):
         errors.check(lib().rlnc_ctx_synchronize(self._h))
+
+    def elim_stats(self):
+        """rlnc_ctx_elim_stats: elimination routes summed over the context's
+        decoders (gpu, gpu_retried, host_after_gpu, host)."""
+        v = [ctypes.c_size_t() for _ in range(4)]
+        errors.check(lib().rlnc_ctx_elim_stats(self._h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("gpu", "gpu_retried", "host_after_gpu", "host"), (x.value for x in v)))
+
+    def set_route_min_k(self, min_k):
+        """Single decoders' full batches take the GPU elimination from piece
+        count min_k on (rlnc_ctx_set_route_min_k; default 224)."""
+        errors.check(lib().rlnc_ctx_set_route_min_k(self._h, int(min_k)))
+        self.route_min_k = int(min_k)
 
     def close(self):
         if self._h:

@@ -10,7 +10,9 @@ import numpy as np
 import pytest
 
 import oracle
+import panel_rule as pr
 from kodr_amd import _lib, errors
+from kodr_amd._codec import elim_stats
 
 pytestmark = pytest.mark.gpu
 U8P = _lib._u8p
@@ -87,11 +89,14 @@ def _rows(ctx, V, P, L):
 
 
 @pytest.fixture(autouse=True)
-def host_references(monkeypatch):
+def host_references(gpu_ctx):
     # the reference decoders here run kodr's elimination on the host:
     # rlnc_decoder_add_pieces and the lazy flush would otherwise route large
     # full batches to the GPU elimination themselves (capi.cpp dec_route_gpu)
-    monkeypatch.setenv("KODR_ROUTE_MIN_K", "100000")
+    prev = gpu_ctx.route_min_k
+    gpu_ctx.set_route_min_k(100000)
+    yield
+    gpu_ctx.set_route_min_k(prev)
 
 
 def _same(a, b):
@@ -115,6 +120,11 @@ def test_gpu_elimination_matches_host(gpu_ctx, kind, k):
     sg = _lib.lib().rlnc_decoder_add_pieces_gpu(gpu.h, ctypes.c_void_p(drows), n, pitch, L, ctypes.byref(cg))
     assert (sg, cg.value) == (sh, ch.value)
     _same(host, gpu)
+    if kind == "dense" and pr.gf_inverse(V[:k]) is not None:
+        # the state came from the GPU elimination, not a host fallback
+        s = elim_stats(gpu.h)
+        assert s["gpu"] == 1 and s["host_after_gpu"] == 0, s
+        assert elim_stats(host.h)["gpu"] == 0
     # and the oracle's literal decoder, step by step
     ref = oracle.Decoder(k)
     C = oracle.encode(P, V)
@@ -205,6 +215,10 @@ def test_gpu_elimination_c2_round_trip(gpu_ctx):
     assert (st, c.value) == (sh, ch.value)
     assert dec.state()[3]
     assert np.array_equal(dec.transform(), host.transform())
+    V = gpu_ctx.d2h(dW, n * W).reshape(n, W)[:k, :k]
+    s = elim_stats(dec.h)
+    assert s["gpu"] == 1 and s["host_after_gpu"] == 0, s
+    assert s["gpu_retried"] == (1 if pr.expected_attempt(V) else 0), s
     dDec = gpu_ctx.alloc(k * L)
     errors.check(_lib.lib().rlnc_decoder_get_pieces_device(dec.h, dDec, L))
     assert np.array_equal(gpu_ctx.d2h(dDec, k * L), data)
@@ -375,7 +389,7 @@ def test_routed_single_decoder_vs_oracle(gpu_ctx, monkeypatch, kind, k):
     (capi.cpp dec_route_gpu); singular blocks fall back to the host.  Both
     entry points against the oracle's literal decoder: return code, rows
     consumed, counters, coefficients and decoded pieces."""
-    monkeypatch.setenv("KODR_ROUTE_MIN_K", "128")
+    gpu_ctx.set_route_min_k(128)
     rng = np.random.default_rng(k * 7 + len(kind))
     L = 64
     P = rng.integers(0, 256, (k, L), dtype=np.uint8)
@@ -405,5 +419,8 @@ def test_routed_single_decoder_vs_oracle(gpu_ctx, monkeypatch, kind, k):
         if ref.is_decoded():
             s1, out = d.get_all()
             assert s1 == 0 and np.array_equal(out, P)
+        if kind == "dense" and pr.gf_inverse(V[:k]) is not None:
+            s = elim_stats(d.h)  # both entry points took the GPU elimination
+            assert s["gpu"] == 1 and s["host_after_gpu"] == 0, s
     gpu_ctx.synchronize()
     gpu_ctx.free(drows)

@@ -32,6 +32,6 @@ def test_elimination_kernels_do_not_spill(tmp_path):
         if m and name:
             kernels[name][m.group(1)] = int(m.group(2))
     mc = {n: v for n, v in kernels.items() if "gf_elim_mc" in n}
-    assert len(mc) >= 3, kernels.keys()   # mc2 and both mc4 instances
+    assert len(mc) >= 2, kernels.keys()   # mc2 and mc4<2> (mc4<4>: tuning builds only)
     for n, v in mc.items():
         assert v.get("VGPRs Spill") == 0 and v.get("ScratchSize [bytes/lane]") == 0, (n, v)
