@@ -165,6 +165,11 @@ struct rlnc_decoder {
   size_t recv_rows = 0;
   DevBuf recv_bs;            // bit-sliced twin of recv rows [0, bs_rows)
   size_t bs_rows = 0;
+  // compact rows: received rows [cmp_lo, cmp_hi) exist only in the twin (the
+  // batched device-row copies write the twin alone: T x R reads nothing else);
+  // a plain-row reader un-slices them first (dec_uncompact), a gather of
+  // systematic rows un-slices on the fly (gather_rows' twin rows)
+  size_t cmp_lo = 0, cmp_hi = 0;
   DevBuf tmat;               // transform upload
   DevBuf decoded;            // useful x pitch, valid when decoded_ready
   DevBuf rowbuf;             // one row for partial GetPiece
@@ -1356,9 +1361,20 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
 
 namespace {
 
+// the compact rows' plain bytes from their twin (bit-slicing is an involution)
+int dec_uncompact(rlnc_decoder* d) {
+  if (d->cmp_hi <= d->cmp_lo) return RLNC_OK;
+  const size_t lo = d->cmp_lo, n = d->cmp_hi - d->cmp_lo;
+  d->cmp_lo = d->cmp_hi = 0;
+  HIPC(kodr_amd::bitslice_rows(d->recv_bs.p + lo * d->pitch, d->recv.p + lo * d->pitch, d->pitch, n, d->L,
+                               d->ctx->stream));
+  return RLNC_OK;
+}
+
 // grow the received-piece buffer so rows [0, need) fit; keeps rows [0, have)
 int dec_reserve_rows(rlnc_decoder* d, size_t need, size_t have) {
   if (need <= d->recv_rows) return RLNC_OK;
+  TRY(dec_uncompact(d));  // the copy below and the twin's rebuild read plain rows
   size_t nrows = std::max<size_t>(d->recv_rows ? d->recv_rows * 2 : d->core.piece_count() + 8, need);
   DevBuf nb;
   nb.bind(d->ctx->device, d->ctx->stream);
@@ -1557,6 +1573,7 @@ int dec_add(rlnc_decoder* d, const uint8_t* vec, size_t vlen, const uint8_t* pie
 int dec_extend_twin(rlnc_decoder* d) {
   const size_t recv = d->core.received();
   if (d->recv_bs.cap < d->recv_rows * d->pitch) {
+    TRY(dec_uncompact(d));
     TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
     d->bs_rows = 0;
   }
@@ -1581,8 +1598,10 @@ int dec_gemm(rlnc_decoder* d, const uint8_t* dA, size_t M, uint8_t* dY, size_t l
   d->last_bs = false;
   if (M < min_rows || few_narrow_rows(M, recv, d->L) || (d->pitch % 32) ||
       !bs_chunk_rows(M, std::max<size_t>(recv, 1), d->pitch, d->L) ||
-      !kodr_amd::bs_ready(ctx->device))
+      !kodr_amd::bs_ready(ctx->device)) {
+    TRY(dec_uncompact(d));
     return gemm(ctx, dA, recv, M, recv, d->recv.p, d->pitch, dY, ldy, d->L);
+  }
   d->last_bs = true;
   TRY(dec_extend_twin(d));
   return gemm_bs(ctx, dA, recv, M, recv, d->recv_bs.p, d->pitch, dY, ldy, d->L);
@@ -1608,8 +1627,12 @@ int dec_apply(rlnc_decoder* d, size_t rows, const uint8_t* trows, uint8_t* dst, 
     while (j < recv && !t[j]) j++;
     bool unit = j < recv && t[j] == 1;
     for (size_t q = j + 1; unit && q < recv; q++) unit = !t[q];
-    if (unit) d->hsrc[i] = d->recv.p + j * d->pitch;
-    else m++;
+    if (unit && j >= d->cmp_lo && j < d->cmp_hi)  // a compact row: gathered from its twin, un-sliced
+      d->hsrc[i] = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(d->recv_bs.p + j * d->pitch) | 1);
+    else if (unit)
+      d->hsrc[i] = d->recv.p + j * d->pitch;
+    else
+      m++;
   }
   d->last_gf_rows = m;
   d->last_copy_rows = rows - m;
@@ -1770,20 +1793,28 @@ int dec_batch_pre(rlnc_decoder* d, const uint8_t* rows, size_t count, size_t pit
   if (twin) {
     d->bs_rows = std::min(d->bs_rows, row0);  // rows [row0, ..) are new
     if (d->recv_bs.cap < d->recv_rows * d->pitch) {  // as dec_extend_twin, through row0 + pre
+      TRY(dec_uncompact(d));
       TRY(d->recv_bs.reserve(d->recv_rows * d->pitch));
       d->bs_rows = 0;
     }
   }
-  // device rows whose twin starts here: copy and bit-slice in one pass
+  // device rows whose twin starts here: bit-sliced in one pass, into the twin
+  // only (compact rows [row0, row0 + pre), appended to a compact range that
+  // ends at row0) -- the plain copy's 1/3 of the pass's traffic is skipped
   uint8_t* dbs = twin ? d->recv_bs.p + row0 * d->pitch : nullptr;
   bool fused = false;
   if (twin && dev && d->bs_rows == row0 && d->L % 32 == 0) {
-    if (defer && kodr_amd::copy_bitslice_ok(rows + k, pitch, dst, dbs, d->pitch, d->L) && pre <= 0x7fffffff) {
-      defer->push_back({rows + k, dst, dbs, pre, d->pitch});
+    if (d->cmp_hi > d->cmp_lo && d->cmp_hi != row0) TRY(dec_uncompact(d));
+    if (defer && kodr_amd::copy_bitslice_ok(rows + k, pitch, nullptr, dbs, d->pitch, d->L) && pre <= 0x7fffffff) {
+      defer->push_back({rows + k, nullptr, dbs, pre, d->pitch});
       fused = true;
     } else {
-      fused = kodr_amd::copy_bitslice_rows(rows + k, pitch, dst, dbs, d->pitch, pre, d->L, d->ctx->stream) ==
+      fused = kodr_amd::copy_bitslice_rows(rows + k, pitch, nullptr, dbs, d->pitch, pre, d->L, d->ctx->stream) ==
               hipSuccess;
+    }
+    if (fused) {
+      if (d->cmp_hi <= d->cmp_lo) d->cmp_lo = row0;
+      d->cmp_hi = row0 + pre;
     }
   }
   if (!fused) {
@@ -1804,6 +1835,7 @@ int dec_batch_post(rlnc_decoder* d, const uint8_t* rows, size_t pitch, bool dev,
   const size_t k = d->core.piece_count();
   if (n) d->decoded_ready = false;
   if (bc.twin_end) d->bs_rows = bc.row0 + std::min(n, bc.pre);  // only accepted rows' twin counts
+  if (d->cmp_hi > bc.row0 + n) d->cmp_hi = std::max(d->cmp_lo, bc.row0 + n);  // nor compact rows past them
   // accepted rows not copied yet (dependent rows past the slack, or the
   // staged path) -> one 2D copy
   if (n > bc.pre) TRY(dec_store_pieces(d, bc.row0 + bc.pre, rows + bc.pre * pitch + k, pitch, n - bc.pre, dev));
@@ -1986,56 +2018,59 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // reported when it carries one of the launch's tags (tag0 + attempt, bit 31
 // set on failure).  Decoder i is resolved when every one of its workgroups
 // reported success (cnt[i] = k, att[i] = the attempt that succeeded) or any
-// reported failure (cnt[i] = 0: kodr's route on the host).  A failed
-// workgroup leaves the decoder's abort granule first, so its workgroups that
-// have not started yet read no input: the host may go on without them.
-// on_fail(i) runs as soon as decoder i fails, while the launch may still run.
-// A launch that resolves nothing within 2 s is waited for on the stream once.
+// reported failure (cnt[i] = 0: kodr's route on the host).  on_fail(i) runs
+// as soon as decoder i fails, while the launch may still run.
+// A decoder still unresolved kElimGiveUp after the launch was issued -- its
+// workgroups not resident, e.g. behind another kernel on the same GPU -- is
+// given up the same way: the launch finishes in the background on the
+// context stream, which every later use of its buffers and of the caller's
+// rows is ordered behind (device rows are read asynchronously on that
+// stream), and its late results are never read.
+constexpr auto kElimGiveUp = std::chrono::milliseconds(5);
 int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt, int* att,
                      const std::function<int(size_t)>& on_fail = nullptr) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
   const auto t0 = std::chrono::steady_clock::now();
-  bool synced = false;
-  std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed
+  std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed or given up
+  std::vector<int> satt(nc, 0);
   size_t open = nc;
   for (unsigned spins = 0; open;) {
-    for (size_t g = 0; g < nc; g++) {
-      if (res[g]) continue;
-      int done = 0;
-      bool fail = false;
-      for (int q = 0; q < P && !fail; q++) {
-        const uint32_t v = st[g * P + q];
-        const uint32_t t = (v & 0x7fffffffu) - a.epoch;
-        if (t >= na) continue;  // not reported yet
-        if (v & 0x80000000u)
-          fail = true;
-        else
-          done++;
-      }
-      if (!fail && done < P) continue;
-      std::atomic_thread_fence(std::memory_order_acquire);
-      res[g] = fail ? -1 : 1;
-      open--;
-      if (fail && on_fail) TRY(on_fail(g));
-    }
-    if (!open) break;
-    if (synced) break;  // finished without reporting: the host route
+    bool late = false;
     if (++spins < 4096) {
       _mm_pause();
     } else {
       std::this_thread::yield();
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-        HIPC(hipStreamSynchronize(ctx->stream));
-        synced = true;
+      late = std::chrono::steady_clock::now() - t0 > kElimGiveUp;
+    }
+    for (size_t g = 0; g < nc; g++) {
+      if (res[g]) continue;
+      int done = 0;
+      bool fail = false;
+      uint32_t first = 0;
+      for (int q = 0; q < P && !fail; q++) {
+        const uint32_t v = st[g * P + q];
+        const uint32_t t = (v & 0x7fffffffu) - a.epoch;
+        if (t >= na) continue;  // not reported yet
+        if (v & 0x80000000u) {
+          fail = true;
+        } else {
+          done++;
+          first = t;
+        }
       }
+      if (!fail && done < P && !late) continue;
+      std::atomic_thread_fence(std::memory_order_acquire);
+      res[g] = fail || done < P ? -1 : 1;
+      satt[g] = (int)first;
+      open--;
+      if (res[g] < 0 && on_fail) TRY(on_fail(g));
     }
   }
-  std::atomic_thread_fence(std::memory_order_acquire);
   for (size_t i = 0; i < nc; i++) {
     cnt[i] = res[i] == 1 ? a.k : 0;
-    att[i] = res[i] == 1 ? (int)((st[i * P] & 0x7fffffffu) - a.epoch) : 0;
+    att[i] = res[i] == 1 ? satt[i] : 0;
   }
   return RLNC_OK;
 }
@@ -2098,7 +2133,10 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   // elimination, launched after it so that its workgroups get their CUs
   // first; the context stream waits for them before anything later.
   const bool side = !defer.empty() && !gpu.empty() && add_side_stream();
-  if (side) TRY(ctx_side(ctx));
+  // (the side stream's events also order the host route's vector reads of a
+  // decoder whose launch failed or was given up: behind the rows' producers,
+  // not behind the elimination)
+  if (!gpu.empty()) TRY(ctx_side(ctx));
   auto launch_copies = [&]() -> int {
   for (size_t c0 = 0; c0 < defer.size(); c0 += kodr_amd::kCopyGroupMax) {
     const size_t nc = std::min<size_t>(kodr_amd::kCopyGroupMax, defer.size() - c0);
@@ -2115,9 +2153,9 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   }
   return RLNC_OK;
   };
+  if (!gpu.empty()) HIPC(hipEventRecord(ctx->rows_ready, ctx->stream));  // the rows' producer work
   if (side) {
-    HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the rows' producer work, ordered before the copies
-    HIPC(hipEventRecord(ctx->rows_ready, ctx->stream));
+    HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // ... ordered before the copies
     HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
   } else {
     TRY(launch_copies());
@@ -2268,7 +2306,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
       TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(),
-                           side ? std::function<int(size_t)>(early_host) : std::function<int(size_t)>()));
+                           std::function<int(size_t)>(early_host)));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
@@ -2341,7 +2379,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
           // on a stream that does not wait for the rows' copies beside it
           hipStream_t vs = ctx->stream;
           const double tf0 = timing ? tnow() : 0;
-          if (side) TRY(ctx_aux_after_rows(ctx, &vs));
+          TRY(ctx_aux_after_rows(ctx, &vs));
           HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, vs));
           const double tf1 = timing ? tnow() : 0;
           size_t m = 0;

@@ -552,6 +552,11 @@ def main():
     # tuning (MODE 30): the grouped two-row loop with every body inlined for
     # one coefficient (19: eight XOR3s) -- no jumps, wrong products
     out += emit("KODR_BS_MAIN_P2_INLINE", main_loop(True, inline=19))
+    # tuning (MODE 31 / 32): the grouped two-row loop without the row stream
+    # (the ring's stale rows; wrong products), with threaded / inlined bodies:
+    # what any load path (LDS staging, deeper prefetch) could save at most
+    out += emit("KODR_BS_MAIN_P2_NL", main_loop(True, False))
+    out += emit("KODR_BS_MAIN_P2_INLINE_NL", main_loop(True, False, inline=19))
     ops2 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
     out.append("#define KODR_BS_RING_OPERANDS_P2 " + ", ".join(ops2))
     clob2 = [f'"v{r}"' for r in list(range(ACC, RING)) + list(range(RING + 8 * P, VMAX))]

@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void bitslice_pitched_kernel(const uint8_t* __
 
 // dst row r = src row r (bytes [0, nblk * 32)), and dst_bs row r = its
 // bit-sliced form: one read of the source for both, for the decoder's
-// received rows (plain rows for the GetPiece paths, the twin for T x R).
+// received rows (plain rows for the GetPiece paths, the twin for T x R);
+// dst == nullptr writes the twin only (a compact decoder's rows).
 // src, spitch, dpitch: multiples of 16 (checked by the host).
 __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __restrict__ src, size_t spitch,
                                                            uint8_t* __restrict__ dst, uint8_t* __restrict__ dst_bs,
@@ -122,9 +123,11 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
   const uint4* q = reinterpret_cast<const uint4*>(src + (size_t)r * spitch + (size_t)b * kBsBlock);
   const size_t off = (size_t)r * dpitch + (size_t)b * kBsBlock;
   const uint4 a = q[0], c = q[1];
-  uint4* p = reinterpret_cast<uint4*>(dst + off);
-  p[0] = a;
-  p[1] = c;
+  if (dst) {
+    uint4* p = reinterpret_cast<uint4*>(dst + off);
+    p[0] = a;
+    p[1] = c;
+  }
   uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
   bitslice32(d);
   uint4* t = reinterpret_cast<uint4*>(dst_bs + off);
@@ -150,7 +153,7 @@ __device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r
   const uint32_t oz = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false);
   const uint32_t ow = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false);
   const size_t off = r * dpitch + hi * 16;
-  *reinterpret_cast<uint4*>(g.dst[y] + off) = a;
+  if (g.dst[y]) *reinterpret_cast<uint4*>(g.dst[y] + off) = a;  // (null: twin only)
   uint32_t d[8];
   if ((hi & 1) == 0) {
     d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = ox; d[5] = oy; d[6] = oz; d[7] = ow;
@@ -343,7 +346,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // rows of its task, so there is no cross-wave fold; its accumulators leave
   // the asm in registers and are transposed and stored straight from there
   // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
-  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30) && RP == 2;
+  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32) && RP == 2;
   uint32_t* red = lds;
   uint32_t* tgt_l = DIRECT ? lds : lds + 64 * 64;
   uint32_t* prog_l = tgt_l + 256;
@@ -625,6 +628,16 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
                    : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
                    : KODR_BS_ASM_INPUTS
                    : KODR_BS_CLOBBERS_P2_DIRECT);
+    } else if (nr > 0 && MODE == 31) {  // tuning: no row stream (stale rows, wrong products)
+      asm volatile(KODR_BS_MAIN_P2_NL "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
+                   : KODR_BS_ASM_INPUTS
+                   : KODR_BS_CLOBBERS_P2_DIRECT);
+    } else if (nr > 0 && MODE == 32) {  // tuning: neither jumps nor row stream
+      asm volatile(KODR_BS_MAIN_P2_INLINE_NL "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
+                   : KODR_BS_ASM_INPUTS
+                   : KODR_BS_CLOBBERS_P2_DIRECT);
     } else if (nr > 0) {
       asm volatile(KODR_BS_MAIN_P2 "s_waitcnt lgkmcnt(0)\n\t"
                    : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
@@ -661,7 +674,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   }
   if (nr > 0 && MODE != 5) {
     if constexpr (RP != KODR_BS_P) {
-      static_assert(RP == 2 && (MODE == 0 || MODE == 30), "the two-row ring variant has the plain main loop only");
+      static_assert(RP == 2 && (MODE == 0 || MODE >= 30), "the two-row ring variant has the plain main loop only");
       asm volatile(KODR_BS_MAIN_P2 KODR_BS_REDUCE "s_waitcnt lgkmcnt(0)\n\t"
                    : KODR_BS_RING_OPERANDS_P2
                    : KODR_BS_ASM_INPUTS
@@ -827,7 +840,7 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     g.y_stride = group->y_stride;
     // gridDim.x is a multiple of 8, so the XCD order of each generation's
     // blocks is the single-generation one; the two-row ring (plain loop only)
-    constexpr int rp = MODE == 0 || MODE == 30 ? 2 : KODR_BS_P;
+    constexpr int rp = MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
                        lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, BsSideK{});
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
@@ -858,7 +871,7 @@ hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, u
                               size_t rows, size_t ncols, hipStream_t stream) {
   if (!rows || !ncols) return hipSuccess;
   if (ncols % kBsBlock || dpitch % kBsBlock || dpitch < ncols || (uintptr_t)src % 16 || spitch % 16 ||
-      (uintptr_t)dst % 16 || (uintptr_t)dst_bs % 16)
+      (uintptr_t)dst % 16 || !dst_bs || (uintptr_t)dst_bs % 16)
     return hipErrorInvalidValue;
   const size_t nblk = ncols / kBsBlock;
   const size_t total = rows * nblk;
@@ -871,7 +884,8 @@ hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, u
 bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, const uint8_t* dst_bs, size_t dpitch,
                       size_t ncols) {
   return ncols && ncols % kBsBlock == 0 && dpitch % kBsBlock == 0 && dpitch >= ncols && (uintptr_t)src % 16 == 0 &&
-         spitch % 16 == 0 && (uintptr_t)dst % 16 == 0 && (uintptr_t)dst_bs % 16 == 0 && ncols / kBsBlock <= 0x7fffffff;
+         spitch % 16 == 0 && (uintptr_t)dst % 16 == 0 && dst_bs && (uintptr_t)dst_bs % 16 == 0 &&
+         ncols / kBsBlock <= 0x7fffffff;
 }
 
 // copy workgroups resident per CU at most (16 of its 32 wave slots): room for
@@ -1045,7 +1059,8 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 10 ? KODR_BS_CALL(KW_, 10) : mode == 11 ? KODR_BS_CALL(KW_, 11)                \
          : mode == 12 ? KODR_BS_CALL(KW_, 12) : mode == 13 ? KODR_BS_CALL(KW_, 13)                \
          : mode == 14 ? KODR_BS_CALL(KW_, 14) : mode == 20 ? KODR_BS_CALL(KW_, 20)           \
-         : mode == 30 ? KODR_BS_CALL(KW_, 30)                                                 \
+         : mode == 30 ? KODR_BS_CALL(KW_, 30) : mode == 31 ? KODR_BS_CALL(KW_, 31)           \
+         : mode == 32 ? KODR_BS_CALL(KW_, 32)                                                 \
                                                : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \

@@ -538,6 +538,34 @@ hipError_t launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, siz
 // caller's generation buffer), else dst + r * dpitch.  Used where a row of the
 // product is a plain copy: unit rows of the decode transform (systematic
 // pieces) and gathers of GEMM scratch rows.
+// 8x8 bit transpose inside each byte lane of 8 dwords (gf_bs.hip bitslice32:
+// the bit-sliced twin <-> plain bytes, an involution)
+__device__ __forceinline__ void unslice32(uint32_t (&d)[8]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t t = ((d[q] >> 4) ^ d[q + 4]) & 0x0F0F0F0Fu;
+    d[q + 4] ^= t;
+    d[q] ^= t << 4;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    if (q & 2) continue;
+    const uint32_t t = ((d[q] >> 2) ^ d[q + 2]) & 0x33333333u;
+    d[q + 2] ^= t;
+    d[q] ^= t << 2;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; q += 2) {
+    const uint32_t t = ((d[q] >> 1) ^ d[q + 1]) & 0x55555555u;
+    d[q + 1] ^= t;
+    d[q] ^= t << 1;
+  }
+}
+
+// A source pointer with bit 0 set names a row of a bit-sliced twin (a compact
+// decoder's received row, 32-byte blocks, ncols a multiple of 32): the lane
+// pair of each block swaps halves (DPP), un-slices the block and stores its
+// half of the plain bytes.  The tag is per row (blockIdx.y): uniform.
 __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* const* __restrict__ src,
                                                          uint8_t* const* __restrict__ dtab,
                                                          uint8_t* __restrict__ dst, size_t dpitch,
@@ -545,8 +573,26 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* const* 
   const int r = blockIdx.y;
   const int c = (blockIdx.x * 256 + threadIdx.x) * kLaneBytes;
   if (c >= ncols) return;
-  const uint8_t* s = src[r] + c;
+  const uintptr_t sp = reinterpret_cast<uintptr_t>(src[r]);
+  const uint8_t* s = reinterpret_cast<const uint8_t*>(sp & ~(uintptr_t)1) + c;
   uint8_t* d = (dtab ? dtab[r] : dst + (size_t)r * dpitch) + c;
+  if (sp & 1) {  // twin row: both lanes of a block are live (ncols % 32 == 0)
+    const uint4 a = *reinterpret_cast<const uint4*>(s);
+    const uint32_t ox = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false);
+    const uint32_t oy = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.y, 0xb1, 0xf, 0xf, false);
+    const uint32_t oz = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false);
+    const uint32_t ow = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false);
+    const bool lo = ((c / kLaneBytes) & 1) == 0;
+    uint32_t v[8];
+    if (lo) {
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = ox; v[5] = oy; v[6] = oz; v[7] = ow;
+    } else {
+      v[0] = ox; v[1] = oy; v[2] = oz; v[3] = ow; v[4] = a.x; v[5] = a.y; v[6] = a.z; v[7] = a.w;
+    }
+    unslice32(v);
+    *reinterpret_cast<uint4*>(d) = lo ? make_uint4(v[0], v[1], v[2], v[3]) : make_uint4(v[4], v[5], v[6], v[7]);
+    return;
+  }
   if (c + kLaneBytes <= ncols) {
     *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
   } else {

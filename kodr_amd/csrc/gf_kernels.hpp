@@ -70,7 +70,9 @@ hipError_t copy_rows(const uint8_t* src, size_t spitch, uint8_t* dst, size_t dpi
                      hipStream_t stream);
 
 // dst row r = device row d_src[r] (16-byte aligned); written at d_dst[r] when
-// d_dst (a device table) is given, else at dY + r * ldy.  rows <= 65535.
+// d_dst (a device table) is given, else at dY + r * ldy.  rows <= 65535.  A
+// source pointer with bit 0 set is a row of a bit-sliced twin (ncols a
+// multiple of 32): its plain bytes are gathered (un-sliced on the way).
 hipError_t gather_rows(const uint8_t* const* d_src, uint8_t* dY, size_t ldy, size_t rows, size_t ncols,
                        hipStream_t stream, uint8_t* const* d_dst = nullptr);
 
@@ -164,6 +166,7 @@ hipError_t bitslice_rows_pitched(const uint8_t* src, size_t spitch, uint8_t* dst
 // rows bit-sliced (as bitslice_rows), from one read of src.  ncols and dpitch
 // multiples of 32; src, spitch, dst, dst_bs 16-byte aligned (else
 // hipErrorInvalidValue: the caller copies and bit-slices in two passes).
+// (dst == nullptr: the twin only)
 hipError_t copy_bitslice_rows(const uint8_t* src, size_t spitch, uint8_t* dst, uint8_t* dst_bs, size_t dpitch,
                               size_t rows, size_t ncols, hipStream_t stream);
 // copy_bitslice_rows for up to kCopyGroupMax row sets of one shape (ncols,
