@@ -2125,14 +2125,26 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       continue;
     }
     if ((status[g] = dec_check(d, k, rows[g] + k, piece_len)) != RLNC_OK) continue;
-    if ((status[g] = dec_batch_pre(d, rows[g], counts[g], pitch, true, &bcs[g], &defer)) != RLNC_OK) continue;
     gpu.push_back(g);
   }
+  // the rows' reservations and deferred copies (dec_batch_pre), run after the
+  // first elimination launch so that its kernel starts ahead of them; a
+  // decoder whose preparation fails keeps its state (its launch result is
+  // not loaded) and reports the error
+  std::vector<uint8_t> pre_fail(G, 0);
+  bool prepped = false;
+  auto prep_rows = [&]() {
+    if (prepped) return;
+    prepped = true;
+    for (size_t g : gpu)
+      if ((status[g] = dec_batch_pre(ds[g], rows[g], counts[g], pitch, true, &bcs[g], &defer)) != RLNC_OK)
+        pre_fail[g] = 1;
+  };
   // the deferred row copies: one launch per kCopyGroupMax decoders (one piece
   // length, so one pitch).  With a side stream they run beside the
   // elimination, launched after it so that its workgroups get their CUs
   // first; the context stream waits for them before anything later.
-  const bool side = !defer.empty() && !gpu.empty() && add_side_stream();
+  const bool side = !gpu.empty() && add_side_stream();
   // (the side stream's events also order the host route's vector reads of a
   // decoder whose launch failed or was given up: behind the rows' producers,
   // not behind the elimination)
@@ -2158,6 +2170,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // ... ordered before the copies
     HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
   } else {
+    prep_rows();
     TRY(launch_copies());
   }
   bool copies_out = !side;
@@ -2165,6 +2178,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   // decoders' row bookkeeping assumes them) and joins the side stream
   auto copies_guard = on_scope_exit([&] {
     if (copies_out) return;
+    prep_rows();
     (void)launch_copies();
     (void)hipEventRecord(ctx->side_done, ctx->side);
     (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
@@ -2267,6 +2281,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     }
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
+      prep_rows();
       TRY(launch_copies());
       HIPC(hipEventRecord(ctx->side_done, ctx->side));
       HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
@@ -2290,7 +2305,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     auto early_host = [&](size_t i) -> int {
       rlnc_decoder* d = ds[gpu[c0 + i]];
       const size_t g = gpu[c0 + i];
-      if (d->core.is_decoded()) return RLNC_OK;
+      if (d->core.is_decoded() || pre_fail[g]) return RLNC_OK;
       hipStream_t vs = ctx->stream;
       TRY(ctx_aux_after_rows(ctx, &vs));
       d->hvecs.resize(counts[g] * k);
@@ -2339,6 +2354,10 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     HostPool::get().run(nc, [&](size_t i) {
       rlnc_decoder* d = ds[gpu[c0 + i]];
       const size_t r = base[gpu[c0 + i]];
+      if (pre_fail[gpu[c0 + i]]) {  // its rows were not prepared: the state stays as it was
+        got[i] = 0;
+        return;
+      }
       size_t c = (size_t)std::max(cnt[i], 0);
       bool ok = false;
       if (c == k && cont)
@@ -2361,6 +2380,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       const size_t g = gpu[c0 + i];
       rlnc_decoder* d = ds[g];
       const size_t c = got[i];
+      if (pre_fail[g]) continue;  // status[g] holds its error, consumed[g] = 0
       // the rest of the batch (past a row off its diagonal, or past k) through
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;
