@@ -314,6 +314,7 @@ class RoundTripStep:
         self.ev = [ctx.event() for _ in range(4)]
         self.t_enc, self.t_add, self.t_get, self.ok = [], [], [], True
         self.next_decs = None
+        self.plans = None
 
     def _decoders(self):
         import ctypes
@@ -337,6 +338,9 @@ class RoundTripStep:
         errors.check(L_.rlnc_encoder_group_coded_pieces_device(self.earr, G, self.dV[s_], self.n, self.dW[s_] + k,
                                                                self.W))
         ctx.record(e[1])
+        if self.plans is None:   # the launches' kernel instances (first warmup step: tools/prof_driver.py)
+            from kodr_amd._lib import last_launch_plan
+            self.plans = {"encode": last_launch_plan()}
         ta0 = time.perf_counter()
         cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
         errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[s_], self.counts, self.W, L, cons, sts))
@@ -344,6 +348,9 @@ class RoundTripStep:
         ctx.record(e[2])
         errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
         ctx.record(e[3])
+        if "get" not in self.plans:
+            from kodr_amd._lib import last_launch_plan
+            self.plans["get"] = last_launch_plan()
         self.ok = self.ok and all(st in (0, 3) for st in sts) and all(c == k for c in cons)
         self.next_decs = self._decoders()    # the next step's, on the host while GetPieces runs
         for x in decs:
@@ -424,18 +431,19 @@ def roundtrip_kernels(rt, k, L):
                           "gf_macs_per_s": float(f"{enc_macs / te:.4g}"),
                           "issue_frac": round(enc_macs / te / VALU_FLOOR_MACS_PER_S, 4),
                           "hbm_bytes": G * (k * L + n * k + n * L),
-                          "hbm_frac": round(G * (k * L + n * k + n * L) / te / 1e9 / HBM_PEAK_GBS, 4)},
+                          "hbm_frac": round(G * (k * L + n * k + n * L) / te / 1e9 / HBM_PEAK_GBS, 4),
+                          "plan": rt.plans["encode"]},
         "add_pieces_call": {"avg_us": round(ta * 1e6, 2), "us_per_generation": round(ta / G * 1e6, 2),
                             "elimination_gf_macs": elim_macs,
-                            "row_bytes": G * 3 * n * L,
-                            "note": "host wall time: vector gather + elimination (gf_elim_mc_kernel) + the rows' copy "
-                                    "and bit-sliced twin beside it (read n L, write 2 n L per generation) + T read "
-                                    "back and loaded"},
+                            "row_bytes": G * 2 * n * L,
+                            "note": "host wall time: vector gather + elimination (gf_elim_mc_kernel) + the rows' "
+                                    "bit-sliced twin written beside it (read n L, write n L per generation: compact "
+                                    "rows, no plain copy) + T read back and loaded"},
         "get_pieces_call": {"kernel": "gf_bs_kernel (grouped T x R)", "avg_us": round(tg * 1e6, 2),
                             "us_per_generation": round(tg / G * 1e6, 2),
                             "gf_macs_per_s": float(f"{get_macs / tg:.4g}"),
                             "issue_frac": round(get_macs / tg / VALU_FLOOR_MACS_PER_S, 4),
-                            "hbm_bytes": G * 2 * k * L},
+                            "hbm_bytes": G * 2 * k * L, "plan": rt.plans["get"]},
         "issue_peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
         "note": "issue_frac against the one bit-sliced VALU floor (ISSUE_PER_S x MACS_PER_INST_BS); kernel durations "
                 "of the same command under rocprofv3 in profiles/r05/"}

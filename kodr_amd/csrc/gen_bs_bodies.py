@@ -39,17 +39,19 @@ import os
 
 # Register map: 128 VGPRs in all (4 waves per SIMD), the compiler keeping its
 # own values in v[0..ACC).
-ACC = 12           # 8 rows x 8 planes: v[12..75]; copy r owns v[12+8r .. 19+8r]
-TL0 = 76           # TL table, 15 registers v[76..90] (singles first, as aligned pairs)
-PL = 91            # LDS address of the next program quad
-TH0 = 92           # TH table v[92..106]
+# (KODR_BS_ACC moves the whole map: A/B builds that give the compiler fewer
+# registers of its own to fit a deeper ring)
+ACC = int(os.environ.get("KODR_BS_ACC", "12"))  # 8 rows x 8 planes: v[12..75]; copy r owns v[12+8r .. 19+8r]
+TL0 = ACC + 64     # TL table, 15 registers v[76..90] (singles first, as aligned pairs)
+PL = TL0 + 15      # LDS address of the next program quad
+TH0 = PL + 1       # TH table v[92..106]
 # ring depth (rows in flight per wave): 1 measured 1.5-2.5 % faster than 2 at
 # B = 16-32 in single launches (profiles/r01/bs_ring.log), 2 about 1.7 %
 # faster in grouped launches, whose waves stream 64 rows
 # (profiles/r02/ring_ab/); the kernel carries both (KODR_BS_MAIN: P, the
 # default; KODR_BS_MAIN_P2: two rows).  3 drops to 3 waves per SIMD.
 P = int(os.environ.get("KODR_BS_P", "1"))
-RING = 108         # P row slots x 8 planes: v[108..123]
+RING = TH0 + 16    # P row slots x 8 planes: v[108..123]
 PG = RING + 8 * P  # program chunk: 8 rows x 8 targets, lane 8j + m (absolute lo words)
 PGN = PG + 1       # the next chunk, in flight from LDS
 VMAX = PGN + 1     # first VGPR not used by the asm
@@ -368,7 +370,7 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()
 # after I' with one ds_add_rtn_u32 from a single lane.
 D_EX = 46          # s[46:47] exec save
 D_SC, D_SN, D_SK, D_SKM1, D_TMP = 48, 49, 50, 51, 52
-D_VAT = 107        # the fetched row index (lane 0)
+D_VAT = RING - 1   # the fetched row index (lane 0)
 D_PG, D_PGN = RING + 8 * P, RING + 8 * P + 1   # targets of the current / next row (lanes 0..7)
 D_VADDR, D_VCNT, D_VONE = D_PG + 2, D_PG + 3, D_PG + 4
 D_VMAX = D_VONE + 1
@@ -571,6 +573,16 @@ def main():
     clob2d = [f'"v{r}"' for r in list(range(ACC + 64, RING)) + list(range(RING + 8 * P, VMAX))]
     clob2d += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
     out.append("#define KODR_BS_CLOBBERS_P2_DIRECT " + ", ".join(clob2d) + ', "scc", "memory"')
+    # the three-row ring (tuning, MODE 33: direct grouped launches), which fits
+    # 4 waves per SIMD only with the map moved down (KODR_BS_ACC=4)
+    set_ring(3)
+    out += emit("KODR_BS_MAIN_P3", main_loop(True))
+    ops3 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
+    out.append("#define KODR_BS_RING_OPERANDS_P3 " + ", ".join(ops3))
+    clob3d = [f'"v{r}"' for r in list(range(ACC + 64, RING)) + list(range(RING + 8 * P, VMAX))]
+    clob3d += [f'"s{r}"' for r in list(range(40, 46)) + [GPC, GPC + 1] + list(range(T0, CNT + 1))]
+    out.append("#define KODR_BS_CLOBBERS_P3_DIRECT " + ", ".join(clob3d) + ', "scc", "memory"')
+    out.append(f"#define KODR_BS_VMAX_P3 {VMAX}")
     set_ring(p0)
     out.append(f"// {n_inst} body instructions in {NCOPY} copies, {n_inst / 256 / NCOPY:.2f} per coefficient; "
                f"row prep {len(table_lines(0))} per row; {total} bytes of bodies")

@@ -1,18 +1,17 @@
 #!/usr/bin/env python3
-"""Per-kernel roofline of bench.py's encode_decode round trip from a
-rocprofv3 kernel trace of `bench.py --no-extras` (headline + round trip only).
+"""rocprofv3 kernel trace of the driver's exact bench command
+(`rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20
+--warmup 5`) against the bench line that same run printed.
 
   python tools/prof_roundtrip.py <run_kernel_trace.csv> <bench.json> [--out FILE]
 
-Groups the trace by (kernel, grid); the round trip's launches are
-  * the grouped encode: gf_bs_kernel<..., true, ...> with G x (k + 2) rows of
-    output per launch (told from the headline's B = 32 launch by its grid);
-  * the elimination: gf_elim_mc_kernel (one launch per AddPiece call);
-  * the rows' copy and bit-sliced twin: copy_bitslice_rows_grouped's kernel;
-  * GetPieces: the grouped gf_bs_kernel launch over the decoders' twins;
-and prints each group's count and median duration with its bound: GF MACs
-against the bit-sliced VALU floor (bench.VALU_FLOOR_MACS_PER_S) or bytes
-against the 8 TB/s HBM peak."""
+The launches are told apart by the kernel instance each leg recorded
+(bench.py: legs[*].plan, encode.roofline.plan -- workgroups x 64 x waves
+threads in grid x, generations in grid y) and by their order: bench.py runs
+the round trip's warmup + timed steps first, then the encode leg's warmup +
+timed launches, then the extras.  For each leg: the timed launches' rocprof
+average against the HIP-event average in the bench line, and the fraction of
+its bound recomputed from the rocprof duration."""
 import argparse
 import csv
 import json
@@ -24,6 +23,21 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 
 
+def launches(trace):
+    rows = []
+    for r in csv.DictReader(open(trace)):
+        rows.append((int(r["Start_Timestamp"]), r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]),
+                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rows.sort()
+    return rows
+
+
+def of_plan(rows, plan, after=0):
+    """The gf_bs_kernel launches of a recorded plan, in start order, that start after `after`."""
+    gx = plan["workgroups"] * 64 * plan["waves"]
+    return [r for r in rows if "gf_bs_kernel" in r[1] and r[2] == gx and r[3] == plan["generations"] and r[0] > after]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -31,43 +45,68 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     with open(a.bench) as f:
-        line = json.loads([l for l in f if l.startswith("{")][-1])
-    ed = line["encode_decode"]
-    G = ed["generations_per_step"]
-    k, L = bench.K_PIECES, bench.L_BYTES
+        line = json.loads([x for x in f if x.startswith("{")][-1])
+    rows = launches(a.trace)
+    rt = line["roundtrip"]
+    legs = line["roofline"]["legs"]
+    steps, n_warm = line["steps"], rt["warmup_steps_run"]
+    G = line["config"]["generations_per_step"]
+    k, L = line["config"]["piece_count"], line["config"]["piece_size"]
     n = k + 2
-    groups = {}
-    for r in csv.DictReader(open(a.trace)):
-        key = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]), int(r["Workgroup_Size_X"]))
-        groups.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    out = {"generations_per_step": G, "steps": ed["steps"], "warmup_steps_run": ed["warmup_steps_run"],
-           "kernels": []}
-    peak_mac = bench.VALU_FLOOR_MACS_PER_S
-    for (name, gx, gy, wg), d in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
-        med = statistics.median(d)
-        e = {"kernel": name[-90:], "grid": [gx, gy], "workgroup": wg, "launches": len(d),
-             "median_us": round(med, 2), "total_ms": round(sum(d) / 1e3, 3)}
-        if "gf_elim_mc" in name:
-            macs = gy * k ** 3
-            e.update(leg="elimination (AddPiece)", gf_macs=macs,
-                     gf_macs_per_s=float(f"{macs / med * 1e6:.4g}"), issue_frac=round(macs / med * 1e6 / peak_mac, 4))
-        elif "copy_bitslice" in name:
-            b = G * 3 * n * L
-            e.update(leg="rows' copy + twin (AddPiece)", hbm_bytes=b, hbm_frac=round(b / med / 1e3 / bench.HBM_PEAK_GBS, 4))
-        elif "gf_bs_kernel" in name and "true" in name:
-            # grouped launches: grid y = generations; the encode writes n rows per
-            # generation, GetPieces k (gf_bs plans 8-row tiles: rows = 8 x tiles)
-            e["leg"] = "grouped gf_bs_kernel"
-        out["kernels"].append(e)
-    # attribute the grouped bit-sliced groups by launch count: per timed+warm step
-    # one encode launch and one GetPieces launch per 16 decoders
-    steps = ed["steps"] + ed["warmup_steps_run"]
-    bs = [e for e in out["kernels"] if e.get("leg") == "grouped gf_bs_kernel"]
-    for e in bs:
-        if e["launches"] == steps and e["grid"][1] == G:
-            pass
+    peak = bench.VALU_FLOOR_MACS_PER_S
+    out = {"command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps %d --warmup %d"
+                      % (steps, line["warmup"]),
+           "bench_value": line["value"], "bench_ms_per_step": line["ms_per_step"], "legs": {}}
+
+    def leg(name, sel, events_us, macs=None, hbm=None):
+        if len(sel) < n_warm + steps:
+            out["legs"][name] = {"error": f"{len(sel)} launches, expected {n_warm + steps}"}
+            return None
+        timed = [r[4] for r in sel[n_warm:n_warm + steps]]
+        avg = statistics.mean(timed)
+        e = {"kernel": sel[0][1].replace("(anonymous namespace)::", "").split("(")[0][-100:],
+             "grid": [sel[0][2], sel[0][3]], "timed_launches": len(timed), "rocprof_avg_us": round(avg, 2),
+             "rocprof_min_us": round(min(timed), 2), "rocprof_max_us": round(max(timed), 2)}
+        if events_us is not None:
+            e["bench_events_avg_us"] = events_us
+            e["events_over_rocprof"] = round(events_us / avg, 4)
+        if macs is not None:
+            e["issue_frac_from_rocprof"] = round(macs / avg * 1e6 / peak, 4)
+        if hbm is not None:
+            e["hbm_frac_from_rocprof"] = round(hbm / avg / 1e3 / bench.HBM_PEAK_GBS, 4)
+        out["legs"][name] = e
+        return sel[n_warm + steps - 1][0]
+
+    leg("roundtrip_encode", of_plan(rows, legs["encode_launch"]["plan"]), legs["encode_launch"]["avg_us"],
+        macs=G * n * k * L)
+    leg("roundtrip_get_pieces", of_plan(rows, legs["get_pieces_call"]["plan"]), legs["get_pieces_call"]["avg_us"],
+        macs=G * k * k * L)
+    elim = [r for r in rows if "gf_elim_mc" in r[1] and r[3] == G]
+    leg("roundtrip_elimination", elim, None, macs=G * k ** 3)
+    twin = [r for r in rows if "copy_bitslice" in r[1]]
+    leg("roundtrip_rows_twin", twin, None, hbm=G * 2 * n * L)
+    # the encode leg (bench.py's second timed phase): its own warmup count
+    enc = line["encode"]["roofline"]
+    last_rt = max((r[0] for r in of_plan(rows, legs["encode_launch"]["plan"])[:n_warm + steps]), default=0)
+    sel = of_plan(rows, enc["plan"], after=last_rt)
+    w = enc["warmup_launches"]
+    if len(sel) >= w + steps:
+        timed = [r[4] for r in sel[w:w + steps]]
+        avg = statistics.mean(timed)
+        out["legs"]["encode_B32"] = {
+            "grid": [sel[0][2], sel[0][3]], "timed_launches": steps, "rocprof_avg_us": round(avg, 2),
+            "bench_events_avg_us": enc["avg_launch_us"], "events_over_rocprof": round(enc["avg_launch_us"] / avg, 4),
+            "hbm_frac_from_rocprof": round(enc["hbm_bytes_per_launch"] / avg / 1e3 / bench.HBM_PEAK_GBS, 4),
+            "issue_frac_from_rocprof": round(enc["issue"]["gf_macs_per_launch"] / avg * 1e6 / peak, 4)}
+    else:
+        out["legs"]["encode_B32"] = {"error": f"{len(sel)} launches, expected {w + steps}"}
+    out["roofline_frac_bench"] = line["roofline"]["frac"]
+    rte = out["legs"].get("roundtrip_encode", {})
+    if "rocprof_avg_us" in rte:
+        out["roofline_frac_from_rocprof"] = rte["issue_frac_from_rocprof"]
     with open(a.out, "w") if a.out else sys.stdout as f:
         json.dump(out, f, indent=1)
+        f.write("\n")
 
 
 if __name__ == "__main__":
