@@ -774,22 +774,35 @@ bool DecoderCore::load_rref(const uint8_t* state, size_t pitch, size_t c) {
 bool DecoderCore::load_inverse(const uint8_t* tinv, size_t pitch) {
   const size_t k = k_;
   if (received_ != 0 || k < 2) return false;
+  pinv_.resize(k * k);
+  if (pitch == k) {
+    memcpy(pinv_.data(), tinv, k * k);
+  } else {
+    for (size_t i = 0; i < k; i++) memcpy(pinv_.data() + i * k, tinv + i * pitch, k);
+  }
+  pinv_on_ = true;
+  received_ = k;
+  useful_ = k;
+  all_clean_ = true;
+  return true;
+}
+
+void DecoderCore::expand_inverse() {
+  const size_t k = k_;
+  pinv_on_ = false;
   ensure_tcap(k);
   for (size_t i = 0; i < k; i++) {
     uint8_t* row = free_.back();
     free_.pop_back();
     memset(row, 0, k);
     row[i] = 1;
-    memcpy(row + k, tinv + i * pitch, k);
+    memcpy(row + k, pinv_.data() + i * k, k);
     memset(row + 2 * k, 0, tcap_ - k);
     push_row(row, -1, 0);
     clean_[i] = 1;
     touched_[i] = 0;
   }
-  received_ = k;
-  useful_ = k;
-  all_clean_ = true;
-  return true;
+  std::vector<uint8_t>().swap(pinv_);
 }
 
 bool DecoderCore::load_continued(const uint8_t* state, size_t pitch, bool inverse) {
@@ -842,6 +855,10 @@ bool DecoderCore::load_continued(const uint8_t* state, size_t pitch, bool invers
 size_t DecoderCore::decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const {
   row_of->assign(k_, -1);
   scale->assign(k_, 0);
+  if (pinv_on_) {  // [I | C^-1]: row j is e_j
+    for (size_t j = 0; j < k_; j++) (*row_of)[j] = (int32_t)j, (*scale)[j] = 1;
+    return k_;
+  }
   size_t n = 0;
   for (size_t i = 0; i < rows_.size(); i++) {
     const int32_t p = up_[i] >= 0 ? up_[i] : unit_col(rows_[i], k_);
@@ -855,8 +872,8 @@ size_t DecoderCore::decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* 
 
 int DecoderCore::piece_available(size_t idx) const {
   if (idx >= k_) return 12;                         // :222-224 ErrPieceOutOfBound
-  if (idx >= rows_.size()) return 11;               // :225-227 ErrPieceNotDecodedYet
-  if (rows_.size() >= k_) return 0;                 // :229-231
+  if (idx >= rank()) return 11;                     // :225-227 ErrPieceNotDecodedYet
+  if (rank() >= k_) return 0;                       // :229-231
   const uint8_t* c = rows_[idx];                    // :233-252
   for (size_t i = 0; i < k_; i++) {
     if (i == idx) {
@@ -869,10 +886,19 @@ int DecoderCore::piece_available(size_t idx) const {
 }
 
 void DecoderCore::copy_transform(uint8_t* out, size_t ld) const {
+  if (pinv_on_) {
+    for (size_t i = 0; i < k_; i++) memcpy(out + i * ld, pinv_.data() + i * k_, k_);
+    return;
+  }
   for (size_t i = 0; i < rows_.size(); i++) memcpy(out + i * ld, rows_[i] + k_, received_);
 }
 
 void DecoderCore::copy_coefficients(uint8_t* out) const {
+  if (pinv_on_) {
+    memset(out, 0, k_ * k_);
+    for (size_t i = 0; i < k_; i++) out[i * k_ + i] = 1;
+    return;
+  }
   for (size_t i = 0; i < rows_.size(); i++) memcpy(out + i * k_, rows_[i], k_);
 }
 

@@ -44,6 +44,10 @@ class DecoderCore {
   // A fresh decoder takes the state kodr reaches after k pieces whose vectors
   // C are independent: [I | C^-1], given as C^-1 (k rows of k bytes at `pitch`,
   // columns in arrival order).  Returns false (and changes nothing) otherwise.
+  // The state is kept as that one k x k block until a row is read (coeff_row,
+  // t_row): the counters, rank, decoded(), piece_available() and the copies
+  // answer from the block, so a batched AddPiece followed by GetPieces never
+  // spreads it into k rows (a quarter of a C2 AddPiece call's host time).
   bool load_inverse(const uint8_t* tinv, size_t pitch);
   // A decoder holding r = received() >= 1 rows, all kept (rank() == r),
   // whose next k - r arrivals make its first k coding vectors C independent:
@@ -60,7 +64,7 @@ class DecoderCore {
   size_t useful() const { return useful_; }
   size_t received() const { return received_; }
   size_t piece_count() const { return k_; }
-  size_t rank() const { return rows_.size(); }        // decoder_state.go:187-189
+  size_t rank() const { return pinv_on_ ? k_ : rows_.size(); }  // decoder_state.go:187-189
 
   // decoder_state.go:221-261 availability rule for GetPiece(idx): 0 when row
   // idx of the coded matrix may be returned, else kodr's error code.
@@ -71,13 +75,24 @@ class DecoderCore {
   // returns the count
   size_t decoded(std::vector<int32_t>* row_of, std::vector<uint8_t>* scale) const;
 
-  const uint8_t* coeff_row(size_t i) const { return rows_[i]; }
-  const uint8_t* t_row(size_t i) const { return rows_[i] + k_; }
+  const uint8_t* coeff_row(size_t i) const {
+    expand();
+    return rows_[i];
+  }
+  const uint8_t* t_row(size_t i) const {
+    expand();
+    return rows_[i] + k_;
+  }
   // copy T (rank x received) densely into out (row stride = received)
   void copy_transform(uint8_t* out, size_t ld) const;
   void copy_coefficients(uint8_t* out) const;
 
  private:
+  // the block load_inverse kept -> k rows (before anything reads or changes them)
+  void expand() const {
+    if (pinv_on_) const_cast<DecoderCore*>(this)->expand_inverse();
+  }
+  void expand_inverse();
   void rref();
   void rref_clean();
   size_t add_panel(const uint8_t* vecs, size_t pitch, size_t np);
@@ -118,6 +133,8 @@ class DecoderCore {
   std::vector<uint32_t> ucnt_;         // per coefficient column: unit rows with that pivot
   size_t ndense_ = 0;                  // dense rows in rows_
   std::vector<size_t> dense_pos_;      // positions of dense rows (rebuilt per literal pass)
+  std::vector<uint8_t> pinv_;          // load_inverse's C^-1 (k x k) while pinv_on_
+  bool pinv_on_ = false;
 };
 
 }  // namespace kodr_amd

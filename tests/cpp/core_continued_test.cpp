@@ -1,4 +1,4 @@
-// DecoderCore::load_continued on the CPU (kodr_amd/csrc/decoder_core.cpp):
+// DecoderCore::load_continued (and load_inverse's lazy block) on the CPU (kodr_amd/csrc/decoder_core.cpp):
 // a decoder holding r rows takes the state of M = [its r coefficient rows ;
 // the next k - r vectors] inverted elsewhere, and must end exactly where
 // kodr's own route (decoder_state.go:15-182, here DecoderCore::add row by
@@ -107,7 +107,64 @@ static void run_case(size_t k, size_t r, int kind, bool inverse, std::mt19937& r
   CHECK(d.add(extra.data()) == 3, "k=%zu r=%zu: AddPiece after the load not refused", k, r);
 }
 
+// DecoderCore::load_inverse keeps [I | C^-1] as one block until a row is
+// read: every accessor before and after the rows are spread must answer as a
+// decoder that took the k arrivals through add() (kodr's route)
+static void run_inverse_case(size_t k, std::mt19937& rng) {
+  std::vector<uint8_t> C(k * k);
+  DecoderCore ref(k);
+  for (;;) {
+    for (auto& b : C) b = (uint8_t)(rng() & 0xff);
+    DecoderCore probe(k);
+    for (size_t i = 0; i < k; i++) probe.add(&C[i * k]);
+    if (probe.is_decoded()) break;
+  }
+  for (size_t i = 0; i < k; i++) ref.add(&C[i * k]);
+  const std::vector<uint8_t> tref = transform(ref), cref = coefficients(ref);
+  // C^-1 at a padded pitch
+  const size_t pitch = k + 5;
+  std::vector<uint8_t> tinv(k * pitch, 0xEE);
+  for (size_t i = 0; i < k; i++) memcpy(&tinv[i * pitch], &tref[i * k], k);
+  for (int read_rows_first = 0; read_rows_first < 2; read_rows_first++) {
+    DecoderCore d(k);
+    CHECK(d.load_inverse(tinv.data(), pitch), "k=%zu: load_inverse refused", k);
+    CHECK(!d.load_inverse(tinv.data(), pitch), "k=%zu: a second load_inverse taken", k);
+    if (read_rows_first) {  // spread the rows now: every accessor below reads them
+      for (size_t i = 0; i < k; i++)
+        CHECK(memcmp(d.t_row(i), &tref[i * k], k) == 0 && memcmp(d.coeff_row(i), &cref[i * k], k) == 0,
+              "k=%zu: row %zu", k, i);
+    }
+    CHECK(d.is_decoded() && d.useful() == ref.useful() && d.received() == ref.received() &&
+              d.rank() == ref.rank() && d.required() == 0,
+          "k=%zu rows=%d: counters", k, read_rows_first);
+    CHECK(transform(d) == tref && coefficients(d) == cref, "k=%zu rows=%d: copies", k, read_rows_first);
+    std::vector<int32_t> ro, ro_ref;
+    std::vector<uint8_t> sc, sc_ref;
+    CHECK(d.decoded(&ro, &sc) == ref.decoded(&ro_ref, &sc_ref) && ro == ro_ref && sc == sc_ref,
+          "k=%zu rows=%d: decoded()", k, read_rows_first);
+    for (size_t idx : {(size_t)0, k / 2, k - 1, k, k + 3})
+      CHECK(d.piece_available(idx) == ref.piece_available(idx), "k=%zu rows=%d: piece_available(%zu)", k,
+            read_rows_first, idx);
+    std::vector<uint8_t> extra(k, 9);
+    size_t used = 99;
+    CHECK(d.add(extra.data()) == 3 && d.add_many(extra.data(), k, 1, &used) == 3 && used == 0,
+          "k=%zu rows=%d: AddPiece after the load not refused", k, read_rows_first);
+    // and the rows spread after the block answered
+    for (size_t i = 0; i < k; i++)
+      CHECK(memcmp(d.t_row(i), &tref[i * k], k) == 0 && memcmp(d.coeff_row(i), &cref[i * k], k) == 0,
+            "k=%zu rows=%d: row %zu after", k, read_rows_first, i);
+    CHECK(transform(d) == tref && coefficients(d) == cref, "k=%zu rows=%d: copies after", k, read_rows_first);
+  }
+  DecoderCore one(k);
+  one.add(&C[0]);
+  CHECK(!one.load_inverse(tinv.data(), pitch), "k=%zu: a decoder holding a row took an inverse", k);
+}
+
 int main() {
+  {
+    std::mt19937 rng(777);
+    for (size_t k : {2, 3, 16, 64, 129, 256}) run_inverse_case(k, rng);
+  }
   std::mt19937 rng(12345);
   const size_t ks[] = {2, 3, 16, 64, 129, 256};
   for (size_t k : ks) {
