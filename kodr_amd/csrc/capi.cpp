@@ -122,6 +122,7 @@ struct rlnc_ctx {
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
   hipEvent_t rows_ready = nullptr; // ... the rows' producer work (recorded beside side_done)
   hipStream_t aux = nullptr;       // small downloads that must not queue behind the side copies
+  DevBuf copy_ctr;           // copy_bitslice_rows_grouped's work counters (zeroed once; each launch leaves them zero)
 };
 
 struct rlnc_encoder {
@@ -512,7 +513,11 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->stage.release();
   ctx->elim_tab.release();
   ctx->elim_out.release();
+  ctx->elim_in.release();
   ctx->elim_pub.release();
+  ctx->elim_tdev.release();
+  ctx->gtab.release();
+  ctx->copy_ctr.release();
   if (ctx->elim_pin) (void)hipHostFree(ctx->elim_pin);
   ctx->elim_pin = nullptr;
   ctx->gtmat[0].release();
@@ -1914,6 +1919,11 @@ bool add_side_stream() {
 }
 
 int ctx_side(rlnc_ctx* ctx) {
+  if (!ctx->copy_ctr.p) {  // ordered before the side stream's first copy by the event it waits on
+    ctx->copy_ctr.bind(ctx->device, ctx->stream);
+    TRY(ctx->copy_ctr.reserve(kodr_amd::kCopyCounterBytes));
+    HIPC(hipMemsetAsync(ctx->copy_ctr.p, 0, kodr_amd::kCopyCounterBytes, ctx->stream));
+  }
   if (ctx->side) return RLNC_OK;
   HIPC(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HIPC(hipEventCreateWithFlags(&ctx->side_done, hipEventDisableTiming));
@@ -2161,6 +2171,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       cg.rows[i] = (int)defer[c0 + i].rows;
     }
     HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len,
+                                              reinterpret_cast<uint32_t*>(ctx->copy_ctr.p),
                                               side ? ctx->side : ctx->stream));
   }
   return RLNC_OK;
