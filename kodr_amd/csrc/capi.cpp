@@ -123,6 +123,11 @@ struct rlnc_ctx {
   hipEvent_t rows_ready = nullptr; // ... the rows' producer work (recorded beside side_done)
   hipStream_t aux = nullptr;       // small downloads that must not queue behind the side copies
   DevBuf copy_ctr;           // copy_bitslice_rows_grouped's work counters (zeroed once; each launch leaves them zero)
+  // batched GPU AddPiece: the batch's coding vectors, downloaded beside every
+  // elimination launch for the decoders it leaves to the host route
+  uint8_t* vec_pin = nullptr;
+  size_t vec_pin_cap = 0;
+  hipEvent_t vec_ready = nullptr;
 };
 
 struct rlnc_encoder {
@@ -526,6 +531,9 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->aux);
     (void)hipStreamDestroy(ctx->aux);
   }
+  if (ctx->vec_pin) (void)hipHostFree(ctx->vec_pin);  // (after the aux stream's downloads into it)
+  ctx->vec_pin = nullptr;
+  if (ctx->vec_ready) (void)hipEventDestroy(ctx->vec_ready);
   if (ctx->side) {
     (void)hipStreamSynchronize(ctx->side);
     (void)hipStreamDestroy(ctx->side);
@@ -1931,6 +1939,20 @@ int ctx_side(rlnc_ctx* ctx) {
   return RLNC_OK;
 }
 
+// pinned host memory for `bytes` of a batch's coding vectors (grown as
+// needed: the aux stream's downloads into the old buffer are waited for)
+int ctx_vec_pin(rlnc_ctx* ctx, size_t bytes) {
+  if (!ctx->vec_ready) HIPC(hipEventCreateWithFlags(&ctx->vec_ready, hipEventDisableTiming));
+  if (bytes <= ctx->vec_pin_cap) return RLNC_OK;
+  if (ctx->aux) HIPC(hipStreamSynchronize(ctx->aux));
+  if (ctx->vec_pin) (void)hipHostFree(ctx->vec_pin);
+  ctx->vec_pin = nullptr;
+  ctx->vec_pin_cap = 0;
+  HIPC(hipHostMalloc((void**)&ctx->vec_pin, std::max<size_t>(bytes, 64 << 10), hipHostMallocDefault));
+  ctx->vec_pin_cap = std::max<size_t>(bytes, 64 << 10);
+  return RLNC_OK;
+}
+
 // a stream for small reads of rows whose producers are ordered before
 // ctx->rows_ready, and that must not wait for the copies queued after it
 int ctx_aux_after_rows(rlnc_ctx* ctx, hipStream_t* st) {
@@ -2298,6 +2320,23 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
       copies_out = true;
     }
+    // the chunk's coding vectors to pinned host memory by DMA on the aux
+    // stream, ordered after the rows' producers only: a decoder this launch
+    // leaves to the host route (a failed or given-up launch) reads them there.
+    // Issued for every launch, because a download issued after a failure may
+    // wait for CUs (the staged small-copy kernel) that the stalled launch or
+    // whatever keeps it from being resident holds (test_gpu_coresidency).
+    std::vector<size_t> voff(nc + 1, 0);
+    for (size_t i = 0; i < nc; i++) voff[i + 1] = voff[i] + counts[gpu[c0 + i]] * k;
+    {
+      hipStream_t vs = ctx->stream;
+      TRY(ctx_aux_after_rows(ctx, &vs));
+      TRY(ctx_vec_pin(ctx, voff[nc]));
+      for (size_t i = 0; i < nc; i++)
+        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, counts[gpu[c0 + i]],
+                              hipMemcpyDeviceToHost, vs));
+      HIPC(hipEventRecord(ctx->vec_ready, vs));
+    }
     if (timing) tt2 = tnow();
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
     // back (one 2D copy: the generations' rows are evenly strided), else the
@@ -2317,14 +2356,13 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       rlnc_decoder* d = ds[gpu[c0 + i]];
       const size_t g = gpu[c0 + i];
       if (d->core.is_decoded() || pre_fail[g]) return RLNC_OK;
-      hipStream_t vs = ctx->stream;
-      TRY(ctx_aux_after_rows(ctx, &vs));
-      d->hvecs.resize(counts[g] * k);
-      HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g], pitch, k, counts[g], vs));
       const size_t n = counts[g];
-      early[i] = std::async(std::launch::async, [d, k, n] {
+      const uint8_t* v = ctx->vec_pin + voff[i];
+      hipEvent_t ev = ctx->vec_ready;
+      early[i] = std::async(std::launch::async, [d, k, n, v, ev] {
+        if (hipEventSynchronize(ev) != hipSuccess) return std::make_pair((int)RLNC_ERR_HIP, (size_t)0);
         size_t m = 0;
-        const int st = d->core.add_many(d->hvecs.data(), k, n, &m);
+        const int st = d->core.add_many(v, k, n, &m);
         return std::make_pair(st, m);
       });
       return RLNC_OK;
@@ -2405,16 +2443,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
           st = RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED;  // full/decoder.go:52-54
         } else {
           const size_t rest = counts[g] - c;
-          d->hvecs.resize(rest * k);
-          // the vectors of a batch the GPU left (a singular panel block): read
-          // on a stream that does not wait for the rows' copies beside it
-          hipStream_t vs = ctx->stream;
+          // the vectors of a batch the GPU left (downloaded beside the launch)
           const double tf0 = timing ? tnow() : 0;
-          TRY(ctx_aux_after_rows(ctx, &vs));
-          HIPC(ctx->stage.d2h(d->hvecs.data(), k, rows[g] + c * pitch, pitch, k, rest, vs));
+          HIPC(hipEventSynchronize(ctx->vec_ready));
           const double tf1 = timing ? tnow() : 0;
           size_t m = 0;
-          st = d->core.add_many(d->hvecs.data(), k, rest, &m);
+          st = d->core.add_many(ctx->vec_pin + voff[i] + c * k, k, rest, &m);
           n += m;
           if (timing)
             fprintf(stderr, "add_pieces_gpu: decoder %zu on the host from row %zu: vectors %.1f us, solve %.1f\n", g,
