@@ -2434,6 +2434,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       // kodr's algorithm on the host, from the state the GPU left
       int st = RLNC_OK;
       size_t n = c;
+      const double tp0 = timing ? tnow() : 0;
       if (early[i].valid()) {  // started on the host while the launch ran (got[i] = 0)
         const auto res = early[i].get();
         st = res.first;
@@ -2455,7 +2456,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
                     c, tf1 - tf0, tnow() - tf1);
         }
       }
+      const double tp1 = timing ? tnow() : 0;
       int pst = dec_batch_post(d, rows[g], pitch, true, bcs[g], n);
+      if (timing && tnow() - tp0 > 1000)
+        fprintf(stderr, "add_pieces_gpu: decoder %zu post: host route %.1f us, batch post %.1f\n", g, tp1 - tp0,
+                tnow() - tp1);
       if (pst == RLNC_OK && n && d->policy == RLNC_DECODE_EAGER) pst = dec_progress(d, -1);
       consumed[g] = n;
       status[g] = pst != RLNC_OK ? pst : st;
