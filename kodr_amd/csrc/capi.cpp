@@ -120,9 +120,8 @@ struct rlnc_ctx {
   uint64_t tdev_seq = 0;     // ... one number per such call
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
-  hipEvent_t rows_ready = nullptr; // ... the rows' producer work (recorded beside side_done)
+  hipEvent_t rows_ready = nullptr; // ... the rows' producer work: the side copies and the aux reads wait on it
   hipStream_t aux = nullptr;       // small downloads that must not queue behind the side copies
-  DevBuf copy_ctr;           // copy_bitslice_rows_grouped's work counters (zeroed once; each launch leaves them zero)
   // batched GPU AddPiece: the batch's coding vectors, downloaded beside every
   // elimination launch for the decoders it leaves to the host route
   uint8_t* vec_pin = nullptr;
@@ -522,7 +521,6 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   ctx->elim_pub.release();
   ctx->elim_tdev.release();
   ctx->gtab.release();
-  ctx->copy_ctr.release();
   if (ctx->elim_pin) (void)hipHostFree(ctx->elim_pin);
   ctx->elim_pin = nullptr;
   ctx->gtmat[0].release();
@@ -1927,11 +1925,6 @@ bool add_side_stream() {
 }
 
 int ctx_side(rlnc_ctx* ctx) {
-  if (!ctx->copy_ctr.p) {  // ordered before the side stream's first copy by the event it waits on
-    ctx->copy_ctr.bind(ctx->device, ctx->stream);
-    TRY(ctx->copy_ctr.reserve(kodr_amd::kCopyCounterBytes));
-    HIPC(hipMemsetAsync(ctx->copy_ctr.p, 0, kodr_amd::kCopyCounterBytes, ctx->stream));
-  }
   if (ctx->side) return RLNC_OK;
   HIPC(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HIPC(hipEventCreateWithFlags(&ctx->side_done, hipEventDisableTiming));
@@ -2193,15 +2186,13 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       cg.rows[i] = (int)defer[c0 + i].rows;
     }
     HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len,
-                                              reinterpret_cast<uint32_t*>(ctx->copy_ctr.p),
                                               side ? ctx->side : ctx->stream));
   }
   return RLNC_OK;
   };
   if (!gpu.empty()) HIPC(hipEventRecord(ctx->rows_ready, ctx->stream));  // the rows' producer work
   if (side) {
-    HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // ... ordered before the copies
-    HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
+    HIPC(hipStreamWaitEvent(ctx->side, ctx->rows_ready, 0));  // ... ordered before the copies
   } else {
     prep_rows();
     TRY(launch_copies());

@@ -140,17 +140,11 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
 // block's halves (16 bytes per lane, contiguous over the wave: one 1 KiB
 // request per instruction instead of two half-used ones), swaps them by DPP,
 // bit-slices the whole block in both lanes and stores its half of the planes.
-// The copies run beside the elimination kernel (the batched AddPiece), whose
-// workgroups hold the CUs they land on until it ends.  Work is handed out in
-// 64 KiB chunks from a counter per set: a grid of one lane per half-block
-// filled every CU and the elimination's workgroups waited behind it; a
-// grid-stride loop over a capped grid (round 4) kept the copies on the CUs
-// the elimination left free even after it ended.  Now the workgroups
-// resident beside the elimination take chunks while it runs, and the ones
-// that find a CU only after it ended take the rest.  The last workgroup of a
-// set out resets its counters (launches sharing them are stream-ordered).
+// Grid-stride over a capped grid (copy_bitslice_rows_grouped): the copies run
+// beside the elimination kernel, whose workgroups must find free wave slots
+// even when the copies reach the CUs first (a grid of one lane per half-block
+// filled every CU, and the elimination's workgroups waited behind it).
 constexpr int kCopyUnroll = 4;
-constexpr int kCopyChunkTrips = 4;  // trips of 256 lanes x kCopyUnroll half-blocks per chunk (64 KiB)
 
 __device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r, size_t hi, size_t spitch,
                                              size_t dpitch, const uint4& a) {
@@ -172,13 +166,11 @@ __device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r
 }
 
 __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
-                                                                   int nblk, uint32_t* ctr) {
+                                                                   int nblk) {
   const int y = blockIdx.y;
   const size_t hb = (size_t)nblk * 2;
   const size_t total = (size_t)g.rows[y] * hb;  // even: a lane pair is live or done together
-  constexpr int U = kCopyUnroll;
-  constexpr size_t kChunk = (size_t)256 * U * kCopyChunkTrips;
-  const size_t nchunk = (total + kChunk - 1) / kChunk;
+  const size_t stride = (size_t)gridDim.x * 256;
   const bool narrow = total <= 0xffffffffu;  // 32-bit index arithmetic (uniform)
   const auto split = [&](size_t x, size_t* r, size_t* h) {
     if (narrow) {
@@ -190,44 +182,26 @@ __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g,
       *h = x % hb;
     }
   };
-  __shared__ uint32_t s_chunk;
-  for (;;) {
-    if (threadIdx.x == 0)
-      s_chunk = __hip_atomic_fetch_add(&ctr[y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const size_t c = s_chunk;
-    __syncthreads();  // every wave read it before the next chunk's fetch overwrites it
-    if (c >= nchunk) break;
-    // kCopyUnroll half-blocks per lane per trip, every load in flight before
-    // the stores
-    for (int t = 0; t < kCopyChunkTrips; t++) {
-      const size_t i0 = c * kChunk + (size_t)t * 256 * U + threadIdx.x;
-      size_t r[U], h[U];
-      uint4 a[U];
+  // kCopyUnroll half-blocks per lane per trip, every load in flight before
+  // the stores (the capped grid holds fewer loads in flight than one lane
+  // per half-block did)
+  constexpr int U = kCopyUnroll;
+  for (size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x; i0 < total; i0 += U * stride) {
+    size_t r[U], h[U];
+    uint4 a[U];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const size_t i = i0 + u * 256;
-        r[u] = h[u] = 0;
-        a[u] = make_uint4(0u, 0u, 0u, 0u);
-        if (i < total) {
-          split(i, &r[u], &h[u]);
-          a[u] = *reinterpret_cast<const uint4*>(g.src[y] + r[u] * spitch + h[u] * 16);
-        }
+    for (int u = 0; u < U; u++) {
+      const size_t i = i0 + u * stride;
+      r[u] = h[u] = 0;
+      a[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < total) {
+        split(i, &r[u], &h[u]);
+        a[u] = *reinterpret_cast<const uint4*>(g.src[y] + r[u] * spitch + h[u] * 16);
       }
+    }
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (i0 + u * 256 < total) copy_bs_pair(g, y, r[u], h[u], spitch, dpitch, a[u]);
-    }
-  }
-  // every workgroup of the set has taken its last chunk number when the last
-  // one counts itself out (acq_rel: the counter's increments happen before)
-  if (threadIdx.x == 0) {
-    const uint32_t out = __hip_atomic_fetch_add(&ctr[kCopyGroupMax + y], 1u, __ATOMIC_ACQ_REL,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    if (out == gridDim.x - 1) {
-      __hip_atomic_store(&ctr[y], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ctr[kCopyGroupMax + y], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int u = 0; u < U; u++)
+      if (i0 + u * stride < total) copy_bs_pair(g, y, r[u], h[u], spitch, dpitch, a[u]);
   }
 }
 
@@ -922,15 +896,14 @@ bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, con
          ncols / kBsBlock <= 0x7fffffff;
 }
 
-// copy workgroups per CU over the launch (8 x 4 waves: every wave slot of a
-// CU the elimination left free; the ones that do not fit wait for the CUs it
-// frees)
-constexpr int kCopyWgPerCu = 8;
+// copy workgroups resident per CU at most (16 of its 32 wave slots): room for
+// an elimination workgroup of 16 waves beside them
+constexpr int kCopyWgPerCu = 4;
 
 hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
-                                      uint32_t* ctr, hipStream_t stream) {
+                                      hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  if (n > kCopyGroupMax || !ctr) return hipErrorInvalidValue;
+  if (n > kCopyGroupMax) return hipErrorInvalidValue;
   int maxr = 0;
   for (int i = 0; i < n; i++) {
     if (g.rows[i] < 0 || !copy_bitslice_ok(g.src[i], spitch, g.dst[i], g.dbs[i], dpitch, ncols))
@@ -939,12 +912,12 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   }
   const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
+  // at most kCopyWgPerCu workgroups (4 waves each) per CU over the launch
   static const int wg_per_cu = tune_env("KODR_COPY_WG_PER_CU") ? atoi(tune_env("KODR_COPY_WG_PER_CU")) : kCopyWgPerCu;
-  const size_t chunks = (total + 256 * kCopyUnroll * kCopyChunkTrips - 1) / (256 * kCopyUnroll * kCopyChunkTrips);
   const size_t cap = std::max<size_t>(1, (size_t)std::max(wg_per_cu, 1) * 256 / (size_t)n);
-  const size_t gx = std::min<size_t>(chunks, cap);
+  const size_t gx = std::min<size_t>((total + 255) / 256, cap);
   hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream, g, spitch,
-                     dpitch, (int)nblk, ctr);
+                     dpitch, (int)nblk);
   return hipGetLastError();
 }
 

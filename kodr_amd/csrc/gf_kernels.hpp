@@ -181,12 +181,8 @@ struct CopyGroup {
 };
 bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, const uint8_t* dst_bs, size_t dpitch,
                       size_t ncols);
-// ctr: kCopyCounterBytes of device memory, zero before the first launch;
-// each launch takes its work from these counters and leaves them zero, so
-// launches sharing one ctr must be stream-ordered
-constexpr size_t kCopyCounterBytes = 2 * kCopyGroupMax * sizeof(uint32_t);
 hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
-                                      uint32_t* ctr, hipStream_t stream);
+                                      hipStream_t stream);
 
 // byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);
