@@ -1423,8 +1423,10 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3, regen=None):
     medians over the reps are reported beside the best."""
     import ctypes
     import statistics
+    from kodr_amd._codec import elim_stats
     best = None
     adds, tots = [], []
+    routes = {}
     for rep in range(reps):
         if regen is not None:
             regen(rep)
@@ -1445,6 +1447,8 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3, regen=None):
         decoded = bool(L_.rlnc_decoder_is_decoded(dh))
         bs = bool(L_.rlnc_decoder_last_apply_bitsliced(dh))
         recv = L_.rlnc_decoder_received(dh)
+        for key, v in elim_stats(dh).items():  # which route eliminated the batch (rlnc_decoder_elim_stats)
+            routes[key] = routes.get(key, 0) + v
         L_.rlnc_decoder_destroy(dh)
         adds.append(t1 - t0)
         tots.append(t2 - t0)
@@ -1456,6 +1460,7 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3, regen=None):
         best["s_median"] = round(statistics.median(tots), 6)
         best["add_s_median"] = round(statistics.median(adds), 6)
         best["add_s_max"] = round(max(adds), 6)
+    best["elimination_routes"] = routes
     macs = best["gf_rows"] * best["received"] * L
     best["apply_gf_macs"] = macs
     best["apply_gf_macs_per_s"] = float(f"{macs / best['get_s']:.4g}")

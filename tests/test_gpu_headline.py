@@ -117,6 +117,7 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
     hs = bench.HeadlineStep(gpu_ctx, L_, errors, 256, 131072, 32, 16, grouped=True,
                             rng=np.random.default_rng(0x5EED), nvec=2, keep_data=True)
     rt = bench.RoundTripStep(gpu_ctx, L_, errors, hs.encs, 256, 131072, np.random.default_rng(0x7E), nsets=2)
+    r0 = gpu_ctx.elim_stats()
     try:
         for i in range(2):
             rt.step(i, timed=True)
@@ -125,6 +126,10 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
                 assert np.array_equal(got[g], hs.datas[g]), (i, g)
             assert rt.ok and rt.decoded_ok(list(range(16)))
         assert len(rt.t_enc) == len(rt.t_add) == len(rt.t_get) == 2
+        # every decoder of both steps eliminated on the GPU (rlnc_ctx_elim_stats)
+        r1 = gpu_ctx.elim_stats()
+        d = {key: r1[key] - r0[key] for key in r0}
+        assert d["gpu"] == 32 and d["host_after_gpu"] == 0 and d["host"] == 0, d
     finally:
         rt.close()
         hs.close()
