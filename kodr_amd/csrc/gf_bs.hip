@@ -1028,7 +1028,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     const long kpad = ((long)K + kBsChunk - 1) / kBsChunk * kBsChunk;
     p.kw = kw;
     p.rpw = (int)(((kpad + kw - 1) / kw + kBsChunk - 1) / kBsChunk * kBsChunk);
-    p.lds_bytes = bs_lds_bytes(kw, p.rpw);
+    p.lds_bytes = bs_lds_bytes(kw, p.rpw, group && kw == 1 && bs_direct_allowed());
   }
 #endif
   // the side product's partial sums: kSideUnits x KW dwords x 4
