@@ -138,70 +138,98 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
 // copy_bitslice_kernel over several row sets at once (blockIdx.y = set), two
 // lanes per 32-byte block: lane pair (2j, 2j + 1) reads and writes its
 // block's halves (16 bytes per lane, contiguous over the wave: one 1 KiB
-// request per instruction instead of two half-used ones), swaps them by DPP,
-// bit-slices the whole block in both lanes and stores its half of the planes.
-// Grid-stride over a capped grid (copy_bitslice_rows_grouped): the copies run
-// beside the elimination kernel, whose workgroups must find free wave slots
-// even when the copies reach the CUs first (a grid of one lane per half-block
-// filled every CU, and the elimination's workgroups waited behind it).
+// request per instruction instead of two half-used ones) and swaps them by
+// DPP; each lane then computes only the four planes it stores
+// (bitslice32_half: the first butterfly stage pairs dwords across the halves,
+// the other two stay inside one).  Grid-stride over a capped grid
+// (copy_bitslice_rows_grouped): the copies run beside the elimination kernel,
+// whose workgroups must find free wave slots even when the copies reach the
+// CUs first (a grid of one lane per half-block filled every CU, and the
+// elimination's workgroups waited behind it).  The copy is bound by what one
+// CU moves (~23 GB/s per CU alone and beside the elimination), so its VALU
+// work per byte counts: no division per item (the row and half-block advance
+// by the grid stride's quotient and remainder), half the butterfly per lane.
 constexpr int kCopyUnroll = 4;
 
-__device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, size_t r, size_t hi, size_t spitch,
-                                             size_t dpitch, const uint4& a) {
-  const uint32_t ox = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false);
-  const uint32_t oy = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.y, 0xb1, 0xf, 0xf, false);
-  const uint32_t oz = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false);
-  const uint32_t ow = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false);
-  const size_t off = r * dpitch + hi * 16;
-  if (g.dst[y]) *reinterpret_cast<uint4*>(g.dst[y] + off) = a;  // (null: twin only)
-  uint32_t d[8];
-  if ((hi & 1) == 0) {
-    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = ox; d[5] = oy; d[6] = oz; d[7] = ow;
-  } else {
-    d[0] = ox; d[1] = oy; d[2] = oz; d[3] = ow; d[4] = a.x; d[5] = a.y; d[6] = a.z; d[7] = a.w;
+// planes of the 32-byte block whose dwords d[0..3] are in the lower lane of a
+// pair and d[4..7] in the upper one: h = this lane's four, p = the partner's;
+// on return h = planes 0..3 (lower lane) or 4..7 (upper), as bitslice32 leaves
+// d[0..3] / d[4..7]
+__device__ __forceinline__ void bitslice32_half(uint32_t (&h)[4], const uint32_t (&p)[4], bool lo) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {  // (q, q + 4)
+    const uint32_t a = lo ? h[q] : p[q], b = lo ? p[q] : h[q];
+    const uint32_t t = ((a >> 4) ^ b) & 0x0F0F0F0Fu;
+    h[q] = lo ? a ^ (t << 4) : b ^ t;
   }
-  bitslice32(d);
-  *reinterpret_cast<uint4*>(g.dbs[y] + off) =
-      (hi & 1) == 0 ? make_uint4(d[0], d[1], d[2], d[3]) : make_uint4(d[4], d[5], d[6], d[7]);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {  // (q, q + 2)
+    const uint32_t t = ((h[q] >> 2) ^ h[q + 2]) & 0x33333333u;
+    h[q + 2] ^= t;
+    h[q] ^= t << 2;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q += 2) {  // (q, q + 1)
+    const uint32_t t = ((h[q] >> 1) ^ h[q + 1]) & 0x55555555u;
+    h[q + 1] ^= t;
+    h[q] ^= t << 1;
+  }
+}
+
+__device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, uint32_t r, uint32_t hi, size_t dpitch,
+                                             const uint4& a) {
+  const uint32_t p[4] = {(uint32_t)__builtin_amdgcn_mov_dpp((int)a.x, 0xb1, 0xf, 0xf, false),
+                         (uint32_t)__builtin_amdgcn_mov_dpp((int)a.y, 0xb1, 0xf, 0xf, false),
+                         (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false),
+                         (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false)};
+  const size_t off = (size_t)r * dpitch + (size_t)hi * 16;
+  if (g.dst[y]) *reinterpret_cast<uint4*>(g.dst[y] + off) = a;  // (null: twin only)
+  uint32_t h[4] = {a.x, a.y, a.z, a.w};
+  bitslice32_half(h, p, (hi & 1) == 0);
+  *reinterpret_cast<uint4*>(g.dbs[y] + off) = make_uint4(h[0], h[1], h[2], h[3]);
 }
 
 __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
                                                                    int nblk) {
   const int y = blockIdx.y;
-  const size_t hb = (size_t)nblk * 2;
-  const size_t total = (size_t)g.rows[y] * hb;  // even: a lane pair is live or done together
+  const uint32_t hb = (uint32_t)nblk * 2;  // half-blocks per row (< 2^31: copy_bitslice_ok)
+  const uint32_t rows = (uint32_t)g.rows[y];
   const size_t stride = (size_t)gridDim.x * 256;
-  const bool narrow = total <= 0xffffffffu;  // 32-bit index arithmetic (uniform)
-  const auto split = [&](size_t x, size_t* r, size_t* h) {
-    if (narrow) {
-      const uint32_t q = (uint32_t)x / (uint32_t)hb;
-      *r = q;
-      *h = (uint32_t)x - q * (uint32_t)hb;
-    } else {
-      *r = x / hb;
-      *h = x % hb;
+  // item i = (row r, half-block h) = (i / hb, i % hb); a step of `stride`
+  // items adds (sr, sh) with a carry
+  const uint32_t sr = (uint32_t)(stride / hb), sh = (uint32_t)(stride % hb);
+  const size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t r = (uint32_t)(i0 / hb), h = (uint32_t)(i0 % hb);
+  const auto step = [&](uint32_t& rr, uint32_t& hh) {
+    hh += sh;
+    rr += sr;
+    if (hh >= hb) {
+      hh -= hb;
+      rr++;
     }
   };
   // kCopyUnroll half-blocks per lane per trip, every load in flight before
   // the stores (the capped grid holds fewer loads in flight than one lane
-  // per half-block did)
+  // per half-block did); rows is even per pair: a lane pair is live or done
+  // together (hb is even)
   constexpr int U = kCopyUnroll;
-  for (size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x; i0 < total; i0 += U * stride) {
-    size_t r[U], h[U];
+  while (r < rows) {
+    uint32_t ru[U], hu[U];
     uint4 a[U];
+    uint32_t rr = r, hh = h;
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const size_t i = i0 + u * stride;
-      r[u] = h[u] = 0;
+      ru[u] = rr;
+      hu[u] = hh;
       a[u] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < total) {
-        split(i, &r[u], &h[u]);
-        a[u] = *reinterpret_cast<const uint4*>(g.src[y] + r[u] * spitch + h[u] * 16);
-      }
+      if (rr < rows) a[u] = *reinterpret_cast<const uint4*>(g.src[y] + (size_t)rr * spitch + (size_t)hh * 16);
+      step(rr, hh);
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (i0 + u * stride < total) copy_bs_pair(g, y, r[u], h[u], spitch, dpitch, a[u]);
+      if (ru[u] < rows) copy_bs_pair(g, y, ru[u], hu[u], dpitch, a[u]);
+    r = rr;
+    h = hh;
   }
 }
 
