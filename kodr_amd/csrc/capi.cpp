@@ -1919,10 +1919,12 @@ namespace {
 
 // KODR_ADD_SIDE=0 keeps the batched AddPiece's row copies on the context
 // stream ahead of the elimination (A/B)
-bool add_side_stream() {
-  static const bool v = kodr_amd::tune_env("KODR_ADD_SIDE") ? atoi(kodr_amd::tune_env("KODR_ADD_SIDE")) != 0 : true;
+// (2: on the context stream after the elimination, A/B)
+int add_copy_mode() {
+  static const int v = kodr_amd::tune_env("KODR_ADD_SIDE") ? atoi(kodr_amd::tune_env("KODR_ADD_SIDE")) : 1;
   return v;
 }
+bool add_side_stream() { return add_copy_mode() == 1; }
 
 int ctx_side(rlnc_ctx* ctx) {
   if (ctx->side) return RLNC_OK;
@@ -2170,6 +2172,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   // elimination, launched after it so that its workgroups get their CUs
   // first; the context stream waits for them before anything later.
   const bool side = !gpu.empty() && add_side_stream();
+  const bool after = !gpu.empty() && add_copy_mode() == 2;
   // (the side stream's events also order the host route's vector reads of a
   // decoder whose launch failed or was given up: behind the rows' producers,
   // not behind the elimination)
@@ -2193,17 +2196,18 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
   if (!gpu.empty()) HIPC(hipEventRecord(ctx->rows_ready, ctx->stream));  // the rows' producer work
   if (side) {
     HIPC(hipStreamWaitEvent(ctx->side, ctx->rows_ready, 0));  // ... ordered before the copies
-  } else {
+  } else if (!after) {
     prep_rows();
     TRY(launch_copies());
   }
-  bool copies_out = !side;
+  bool copies_out = !side && !after;
   // an error return before the copies went out still launches them (the
   // decoders' row bookkeeping assumes them) and joins the side stream
   auto copies_guard = on_scope_exit([&] {
     if (copies_out) return;
     prep_rows();
     (void)launch_copies();
+    if (!side) return;
     (void)hipEventRecord(ctx->side_done, ctx->side);
     (void)hipStreamWaitEvent(ctx->stream, ctx->side_done, 0);
   });
@@ -2307,8 +2311,10 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     if (!copies_out) {
       prep_rows();
       TRY(launch_copies());
-      HIPC(hipEventRecord(ctx->side_done, ctx->side));
-      HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
+      if (side) {
+        HIPC(hipEventRecord(ctx->side_done, ctx->side));
+        HIPC(hipStreamWaitEvent(ctx->stream, ctx->side_done, 0));  // everything after the read-back waits for them
+      }
       copies_out = true;
     }
     // the chunk's coding vectors to pinned host memory by DMA on the aux

@@ -19,13 +19,13 @@ PY
 for rep in 1 2 3; do
   run pre_$rep kodr_amd/r5lib_pre/libkodr_rlnc.so 1 || exit 1
   run new_$rep kodr_amd/libkodr_rlnc.so 1 || exit 1
-  run serial_$rep kodr_amd/tune_c/libkodr_rlnc.so 0 || exit 1
+  run after_$rep kodr_amd/tune_c/libkodr_rlnc.so 2 || exit 1
 done
 R=$(pwd)
 cd /tmp
-for v in new:1 serial:0; do
+for v in new:1 after:2; do
   t=${v%%:*}; sd=${v##*:}
-  libp=$R/kodr_amd/libkodr_rlnc.so; [ $t = serial ] && libp=$R/kodr_amd/tune_c/libkodr_rlnc.so
+  libp=$R/kodr_amd/libkodr_rlnc.so; [ $t = after ] && libp=$R/kodr_amd/tune_c/libkodr_rlnc.so
   KODR_ADD_SIDE=$sd KODR_RLNC_LIB=$libp timeout -k 10 300 rocprofv3 --kernel-trace -d $R/$OUT/tr_$t -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline > $R/$OUT/tr_$t.json 2> $R/$OUT/tr_$t.err || { tail -20 $R/$OUT/tr_$t.err; exit 1; }
   echo "== $t"; python3 $R/tools/rt_timeline.py $R/$OUT/tr_$t/run_kernel_trace.csv 3
 done
