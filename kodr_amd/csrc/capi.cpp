@@ -1919,9 +1919,16 @@ namespace {
 
 // KODR_ADD_SIDE=0 keeps the batched AddPiece's row copies on the context
 // stream ahead of the elimination (A/B)
-// (2: on the context stream after the elimination, A/B)
+// The batched AddPiece's row copies: 2 (default) on the context stream after
+// the elimination launch, 1 on the side stream beside it, 0 on the context
+// stream ahead of it (A/B; profiles/r05/copy_order/).  Beside the elimination
+// the two slow each other down (copy 336 against 186 us alone, elimination
+// 228-258 against 150 for 16 C2 generations) and GetPieces waits on a
+// cross-stream event; after it, the round trip's GetPieces follows the copy
+// 6 us later (35 us earlier per step) and a single decoder's elimination runs
+// alone.
 int add_copy_mode() {
-  static const int v = kodr_amd::tune_env("KODR_ADD_SIDE") ? atoi(kodr_amd::tune_env("KODR_ADD_SIDE")) : 1;
+  static const int v = kodr_amd::tune_env("KODR_ADD_SIDE") ? atoi(kodr_amd::tune_env("KODR_ADD_SIDE")) : 2;
   return v;
 }
 bool add_side_stream() { return add_copy_mode() == 1; }
@@ -2329,9 +2336,15 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       hipStream_t vs = ctx->stream;
       TRY(ctx_aux_after_rows(ctx, &vs));
       TRY(ctx_vec_pin(ctx, voff[nc]));
-      for (size_t i = 0; i < nc; i++)
-        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, counts[gpu[c0 + i]],
-                              hipMemcpyDeviceToHost, vs));
+      // decoders whose rows follow each other at the pitch (one buffer, as
+      // the round trip's wire rows) share one 2D copy
+      for (size_t i = 0; i < nc;) {
+        size_t j = i + 1, nrow = counts[gpu[c0 + i]];
+        while (j < nc && rows[gpu[c0 + j]] == rows[gpu[c0 + i]] + nrow * pitch) nrow += counts[gpu[c0 + j++]];
+        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, nrow, hipMemcpyDeviceToHost,
+                              vs));
+        i = j;
+      }
       HIPC(hipEventRecord(ctx->vec_ready, vs));
     }
     if (timing) tt2 = tnow();
@@ -2648,7 +2661,7 @@ int rlnc_decoders_flush_gpu(rlnc_decoder* const* ds, size_t G) {
     const size_t tb = tab.size() * sizeof(void*);
     HIPC(ctx->stage.h2d(ctx->gtab.p, tb, reinterpret_cast<const uint8_t*>(tab.data()), tb, tb, 1, ctx->stream));
     hipStream_t gs = ctx->stream;
-    if (add_side_stream()) {
+    if (add_copy_mode() != 0) {  // (the flush's gathers stay beside its elimination)
       TRY(ctx_side(ctx));
       HIPC(hipEventRecord(ctx->side_done, ctx->stream));  // the tables and any grown receive buffers first
       HIPC(hipStreamWaitEvent(ctx->side, ctx->side_done, 0));
