@@ -2336,15 +2336,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       hipStream_t vs = ctx->stream;
       TRY(ctx_aux_after_rows(ctx, &vs));
       TRY(ctx_vec_pin(ctx, voff[nc]));
-      // decoders whose rows follow each other at the pitch (one buffer, as
-      // the round trip's wire rows) share one 2D copy
-      for (size_t i = 0; i < nc;) {
-        size_t j = i + 1, nrow = counts[gpu[c0 + i]];
-        while (j < nc && rows[gpu[c0 + j]] == rows[gpu[c0 + i]] + nrow * pitch) nrow += counts[gpu[c0 + j++]];
-        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, nrow, hipMemcpyDeviceToHost,
-                              vs));
-        i = j;
-      }
+      // (one copy per decoder: rows that merely follow each other in memory
+      // may lie in different allocations, which one copy may not span)
+      for (size_t i = 0; i < nc; i++)
+        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, counts[gpu[c0 + i]],
+                              hipMemcpyDeviceToHost, vs));
       HIPC(hipEventRecord(ctx->vec_ready, vs));
     }
     if (timing) tt2 = tnow();
