@@ -1943,6 +1943,12 @@ int ctx_side(rlnc_ctx* ctx) {
 
 // pinned host memory for `bytes` of a batch's coding vectors (grown as
 // needed: the aux stream's downloads into the old buffer are waited for)
+// KODR_VEC_PREFETCH=1 (A/B): the batch's vectors downloaded beside every launch
+bool vec_prefetch() {
+  static const bool v = kodr_amd::tune_env("KODR_VEC_PREFETCH") && atoi(kodr_amd::tune_env("KODR_VEC_PREFETCH")) != 0;
+  return v;
+}
+
 int ctx_vec_pin(rlnc_ctx* ctx, size_t bytes) {
   if (!ctx->vec_ready) HIPC(hipEventCreateWithFlags(&ctx->vec_ready, hipEventDisableTiming));
   if (bytes <= ctx->vec_pin_cap) return RLNC_OK;
@@ -2061,8 +2067,12 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // rows is ordered behind (device rows are read asynchronously on that
 // stream), and its late results are never read.
 constexpr auto kElimGiveUp = std::chrono::milliseconds(5);
+// a wait this long means the launch is probably stalled: the batch's vectors
+// are requested for the host route (on_slow) while the give-up runs out
+constexpr auto kElimVecFetch = std::chrono::microseconds(1000);
 int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt, int* att,
-                     const std::function<int(size_t)>& on_fail = nullptr) {
+                     const std::function<int(size_t)>& on_fail = nullptr,
+                     const std::function<int()>& on_slow = nullptr) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
@@ -2070,13 +2080,19 @@ int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int*
   std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed or given up
   std::vector<int> satt(nc, 0);
   size_t open = nc;
+  bool slow = false;
   for (unsigned spins = 0; open;) {
     bool late = false;
     if (++spins < 4096) {
       _mm_pause();
     } else {
       std::this_thread::yield();
-      late = std::chrono::steady_clock::now() - t0 > kElimGiveUp;
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      late = dt > kElimGiveUp;
+      if (!slow && dt > kElimVecFetch) {
+        slow = true;
+        if (on_slow) TRY(on_slow());
+      }
     }
     for (size_t g = 0; g < nc; g++) {
       if (res[g]) continue;
@@ -2327,22 +2343,30 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // the chunk's coding vectors to pinned host memory by DMA on the aux
     // stream, ordered after the rows' producers only: a decoder this launch
     // leaves to the host route (a failed or given-up launch) reads them there.
-    // Issued for every launch, because a download issued after a failure may
-    // wait for CUs (the staged small-copy kernel) that the stalled launch or
-    // whatever keeps it from being resident holds (test_gpu_coresidency).
+    // Requested once, when the first decoder fails or the wait passes
+    // kElimVecFetch; a plain DMA copy, not the staged small copy, whose
+    // kernel needs a CU that a stalled launch, or whatever keeps it from
+    // being resident, may hold for the whole stall (test_gpu_coresidency).
     std::vector<size_t> voff(nc + 1, 0);
     for (size_t i = 0; i < nc; i++) voff[i + 1] = voff[i] + counts[gpu[c0 + i]] * k;
-    {
+    // (the pinned buffer is sized on every call: an allocation may wait for
+    // the device, so it must not happen first in a stalled call)
+    TRY(ctx_vec_pin(ctx, voff[nc]));
+    bool vecs_out = false;
+    auto fetch_vecs = [&]() -> int {
+      if (vecs_out) return RLNC_OK;
+      vecs_out = true;
       hipStream_t vs = ctx->stream;
       TRY(ctx_aux_after_rows(ctx, &vs));
-      TRY(ctx_vec_pin(ctx, voff[nc]));
       // (one copy per decoder: rows that merely follow each other in memory
       // may lie in different allocations, which one copy may not span)
       for (size_t i = 0; i < nc; i++)
         HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, counts[gpu[c0 + i]],
                               hipMemcpyDeviceToHost, vs));
       HIPC(hipEventRecord(ctx->vec_ready, vs));
-    }
+      return RLNC_OK;
+    };
+    if (vec_prefetch()) TRY(fetch_vecs());
     if (timing) tt2 = tnow();
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
     // back (one 2D copy: the generations' rows are evenly strided), else the
@@ -2363,6 +2387,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       const size_t g = gpu[c0 + i];
       if (d->core.is_decoded() || pre_fail[g]) return RLNC_OK;
       const size_t n = counts[g];
+      TRY(fetch_vecs());
       const uint8_t* v = ctx->vec_pin + voff[i];
       hipEvent_t ev = ctx->vec_ready;
       early[i] = std::async(std::launch::async, [d, k, n, v, ev] {
@@ -2375,8 +2400,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     };
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(),
-                           std::function<int(size_t)>(early_host)));
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host),
+                           std::function<int()>(fetch_vecs)));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
@@ -2452,6 +2477,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
           const size_t rest = counts[g] - c;
           // the vectors of a batch the GPU left (downloaded beside the launch)
           const double tf0 = timing ? tnow() : 0;
+          TRY(fetch_vecs());
           HIPC(hipEventSynchronize(ctx->vec_ready));
           const double tf1 = timing ? tnow() : 0;
           size_t m = 0;
