@@ -1943,12 +1943,6 @@ int ctx_side(rlnc_ctx* ctx) {
 
 // pinned host memory for `bytes` of a batch's coding vectors (grown as
 // needed: the aux stream's downloads into the old buffer are waited for)
-// KODR_VEC_PREFETCH=1 (A/B): the batch's vectors downloaded beside every launch
-bool vec_prefetch() {
-  static const bool v = kodr_amd::tune_env("KODR_VEC_PREFETCH") && atoi(kodr_amd::tune_env("KODR_VEC_PREFETCH")) != 0;
-  return v;
-}
-
 int ctx_vec_pin(rlnc_ctx* ctx, size_t bytes) {
   if (!ctx->vec_ready) HIPC(hipEventCreateWithFlags(&ctx->vec_ready, hipEventDisableTiming));
   if (bytes <= ctx->vec_pin_cap) return RLNC_OK;
@@ -2067,12 +2061,8 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // rows is ordered behind (device rows are read asynchronously on that
 // stream), and its late results are never read.
 constexpr auto kElimGiveUp = std::chrono::milliseconds(5);
-// a wait this long means the launch is probably stalled: the batch's vectors
-// are requested for the host route (on_slow) while the give-up runs out
-constexpr auto kElimVecFetch = std::chrono::microseconds(1000);
 int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt, int* att,
-                     const std::function<int(size_t)>& on_fail = nullptr,
-                     const std::function<int()>& on_slow = nullptr) {
+                     const std::function<int(size_t)>& on_fail = nullptr) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
@@ -2080,19 +2070,13 @@ int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int*
   std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed or given up
   std::vector<int> satt(nc, 0);
   size_t open = nc;
-  bool slow = false;
   for (unsigned spins = 0; open;) {
     bool late = false;
     if (++spins < 4096) {
       _mm_pause();
     } else {
       std::this_thread::yield();
-      const auto dt = std::chrono::steady_clock::now() - t0;
-      late = dt > kElimGiveUp;
-      if (!slow && dt > kElimVecFetch) {
-        slow = true;
-        if (on_slow) TRY(on_slow());
-      }
+      late = std::chrono::steady_clock::now() - t0 > kElimGiveUp;
     }
     for (size_t g = 0; g < nc; g++) {
       if (res[g]) continue;
@@ -2343,10 +2327,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // the chunk's coding vectors to pinned host memory by DMA on the aux
     // stream, ordered after the rows' producers only: a decoder this launch
     // leaves to the host route (a failed or given-up launch) reads them there.
-    // Requested once, when the first decoder fails or the wait passes
-    // kElimVecFetch; a plain DMA copy, not the staged small copy, whose
-    // kernel needs a CU that a stalled launch, or whatever keeps it from
-    // being resident, may hold for the whole stall (test_gpu_coresidency).
+    // Requested beside every launch: the copy may run as a blit kernel,
+    // which needs a CU that a stalled launch, or whatever keeps it from being
+    // resident, holds for the whole stall once its workgroups are waiting
+    // (requested after a failure or after 1 ms of waiting, the 16-decoder
+    // call took 18 ms beside the co-residency test's kernel, 57 ms with the
+    // staged small copy; requested with the launch, 5.8-7 ms).
     std::vector<size_t> voff(nc + 1, 0);
     for (size_t i = 0; i < nc; i++) voff[i + 1] = voff[i] + counts[gpu[c0 + i]] * k;
     // (the pinned buffer is sized on every call: an allocation may wait for
@@ -2358,15 +2344,28 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       vecs_out = true;
       hipStream_t vs = ctx->stream;
       TRY(ctx_aux_after_rows(ctx, &vs));
-      // (one copy per decoder: rows that merely follow each other in memory
-      // may lie in different allocations, which one copy may not span)
-      for (size_t i = 0; i < nc; i++)
-        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, rows[gpu[c0 + i]], pitch, k, counts[gpu[c0 + i]],
-                              hipMemcpyDeviceToHost, vs));
+      // decoders whose rows follow each other at the pitch inside one
+      // allocation (the round trip's wire rows) share one 2D copy: a copy
+      // may not span allocations, and each is a launch of its own
+      for (size_t i = 0; i < nc;) {
+        const uint8_t* r0 = rows[gpu[c0 + i]];
+        size_t j = i + 1, nrow = counts[gpu[c0 + i]];
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (j < nc && hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)r0) == hipSuccess) {
+          const uint8_t* end = reinterpret_cast<const uint8_t*>(base) + size;
+          while (j < nc && rows[gpu[c0 + j]] == r0 + nrow * pitch &&
+                 r0 + (nrow + counts[gpu[c0 + j]] - 1) * pitch + k <= end)
+            nrow += counts[gpu[c0 + j++]];
+        }
+        (void)hipGetLastError();  // (a pointer the runtime does not know: no merge, no sticky error)
+        HIPC(hipMemcpy2DAsync(ctx->vec_pin + voff[i], k, r0, pitch, k, nrow, hipMemcpyDeviceToHost, vs));
+        i = j;
+      }
       HIPC(hipEventRecord(ctx->vec_ready, vs));
       return RLNC_OK;
     };
-    if (vec_prefetch()) TRY(fetch_vecs());
+    TRY(fetch_vecs());
     if (timing) tt2 = tnow();
     // the blocked kernel leaves [I | C^-1] or nothing: only the T halves come
     // back (one 2D copy: the generations' rows are evenly strided), else the
@@ -2400,8 +2399,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     };
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host),
-                           std::function<int()>(fetch_vecs)));
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host)));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
