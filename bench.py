@@ -283,8 +283,9 @@ class RoundTripStep:
          G decoded generations to device memory; HIP events around it;
       4. the next step's G decoders are constructed while GetPieces runs
          (host only), then this step's decoders are destroyed (their buffers
-         go back to the pool; the destroy synchronises the stream: the step
-         ends with the GPU's work).
+         go back to the pool ordered on the stream, no host wait: the next
+         step's encode is queued while GetPieces still runs, as a service
+         decoding one batch after another would).
     Decoder construction stays inside the timed steps (each step constructs
     the next one's; the first warmup step its own); kodr's decoder bench
     builds its decoder outside the timer (benches/full/decoder_test.go:71-94)."""
@@ -311,8 +312,10 @@ class RoundTripStep:
         self.earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
         self.rows = [(ctypes.c_void_p * G)(*[dw + g * n * W for g in range(G)]) for dw in self.dW]
         self.counts = (ctypes.c_size_t * G)(*([n] * G))
-        self.ev = [ctx.event() for _ in range(4)]
-        self.t_enc, self.t_add, self.t_get, self.ok = [], [], [], True
+        self.ev = [ctx.event() for _ in range(4)]     # untimed steps
+        self.pend = []                                 # timed steps' events, read after the steps
+        self.spare = []
+        self._t_enc, self.t_add, self._t_get, self._t_gpu_add, self.ok = [], [], [], [], True
         self.next_decs = None
         self.plans = None
 
@@ -333,7 +336,7 @@ class RoundTripStep:
         decs = self.next_decs if self.next_decs is not None else self._decoders()
         self.next_decs = None
         darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
-        e = self.ev
+        e = self.ev if not timed else (self.spare.pop() if self.spare else [ctx.event() for _ in range(4)])
         ctx.record(e[0])
         errors.check(L_.rlnc_encoder_group_coded_pieces_device(self.earr, G, self.dV[s_], self.n, self.dW[s_] + k,
                                                                self.W))
@@ -354,11 +357,34 @@ class RoundTripStep:
         self.ok = self.ok and all(st in (0, 3) for st in sts) and all(c == k for c in cons)
         self.next_decs = self._decoders()    # the next step's, on the host while GetPieces runs
         for x in decs:
-            L_.rlnc_decoder_destroy(x)        # synchronises the stream: the step ends here
+            L_.rlnc_decoder_destroy(x)        # no host wait: the buffers go back ordered on the stream
         if timed:
-            self.t_enc.append(kdev.Context.elapsed_ms(e[0], e[1]) / 1e3)
+            self.pend.append(e)               # (read after the timed steps: no wait inside them)
             self.t_add.append(ta1 - ta0)
-            self.t_get.append(kdev.Context.elapsed_ms(e[2], e[3]) / 1e3)
+
+    def _collect(self):
+        from kodr_amd import device as kdev
+        for e in self.pend:
+            self._t_enc.append(kdev.Context.elapsed_ms(e[0], e[1]) / 1e3)
+            self._t_gpu_add.append(kdev.Context.elapsed_ms(e[1], e[2]) / 1e3)
+            self._t_get.append(kdev.Context.elapsed_ms(e[2], e[3]) / 1e3)
+            self.spare.append(e)
+        self.pend = []
+
+    @property
+    def t_enc(self):
+        self._collect()
+        return self._t_enc
+
+    @property
+    def t_get(self):
+        self._collect()
+        return self._t_get
+
+    @property
+    def t_gpu_add(self):
+        self._collect()
+        return self._t_gpu_add
 
     def decoded_ok(self, gens=None):
         """The last step's decoded generations against the resident ones."""
@@ -423,7 +449,7 @@ def roundtrip_kernels(rt, k, L):
     its bound."""
     import statistics
     G, n = rt.G, rt.n
-    te, ta, tg = (statistics.mean(x) for x in (rt.t_enc, rt.t_add, rt.t_get))
+    te, ta, tg, tga = (statistics.mean(x) for x in (rt.t_enc, rt.t_add, rt.t_get, rt.t_gpu_add))
     enc_macs, get_macs, elim_macs = G * n * k * L, G * k * k * L, G * k ** 3
     return {
         "encode_launch": {"kernel": "gf_bs_kernel (grouped, B = k + 2 per generation)", "avg_us": round(te * 1e6, 2),
@@ -433,12 +459,15 @@ def roundtrip_kernels(rt, k, L):
                           "hbm_bytes": G * (k * L + n * k + n * L),
                           "hbm_frac": round(G * (k * L + n * k + n * L) / te / 1e9 / HBM_PEAK_GBS, 4),
                           "plan": rt.plans["encode"]},
-        "add_pieces_call": {"avg_us": round(ta * 1e6, 2), "us_per_generation": round(ta / G * 1e6, 2),
+        "add_pieces_call": {"avg_us": round(tga * 1e6, 2), "us_per_generation": round(tga / G * 1e6, 2),
+                            "call_wall_us": round(ta * 1e6, 2),
                             "elimination_gf_macs": elim_macs,
                             "row_bytes": G * 2 * n * L,
-                            "note": "host wall time: vector gather + elimination (gf_elim_mc_kernel) + the rows' "
-                                    "bit-sliced twin written beside it (read n L, write n L per generation: compact "
-                                    "rows, no plain copy) + T read back and loaded"},
+                            "note": "avg_us: the context stream from the encode's end to GetPieces' start (HIP "
+                                    "events): the elimination (gf_elim_mc_kernel), then the rows' bit-sliced twin "
+                                    "(read n L, write n L per generation: compact rows, no plain copy); "
+                                    "call_wall_us: the call's host wall time, which also waits for the work queued "
+                                    "ahead of its launch"},
         "get_pieces_call": {"kernel": "gf_bs_kernel (grouped T x R)", "avg_us": round(tg * 1e6, 2),
                             "us_per_generation": round(tg / G * 1e6, 2),
                             "gf_macs_per_s": float(f"{get_macs / tg:.4g}"),

@@ -258,6 +258,10 @@ int rlnc_recoder_coded_pieces_device(rlnc_recoder* rec, const uint8_t* d_r, size
  * (systematic/decoder.go:105-108).  ctx may be NULL: coefficient-side only
  * (counters, rank, transform; no piece data), used by host-logic tests. */
 int rlnc_decoder_create(rlnc_ctx* ctx, size_t piece_count, rlnc_decoder** out);
+/* Does not wait for the context stream: the decoder's device buffers go back
+ * to the context's pool ordered behind its pending work there (device rows a
+ * caller passed in are still read in stream order: keep them until the
+ * stream passes, e.g. rlnc_ctx_synchronize). */
 int rlnc_decoder_destroy(rlnc_decoder* dec);
 /* AddPiece (full/decoder.go:50-66): returns RLNC_ERR_ALL_USEFUL_PIECES_RECEIVED
  * once decoded.  vector: piece_count bytes; piece: L bytes (L fixed by the

@@ -75,6 +75,13 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+  // hand the block to the caller (who frees it with DevicePool::free_shared)
+  void take(uint8_t** pp, size_t* pc) {
+    *pp = p;
+    *pc = cap;
+    p = nullptr;
+    cap = 0;
+  }
 };
 
 const char* kErrText[] = {
@@ -1349,23 +1356,30 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
 
 int rlnc_decoder_destroy(rlnc_decoder* d) {
   if (!d) return RLNC_OK;
+  // The device buffers go back to the stream-ordered pool without a host
+  // wait: with the context stream idle (a query) at once, else ordered by one
+  // event on it for all of them (every use of them -- copies, products, the
+  // side stream's copies joined into it -- is ordered on that stream).  The
+  // host state goes now; no pending device work reads host memory of the
+  // decoder's own.  (Until round 5 a destroy behind pending work waited for
+  // the stream: the GPU sat idle from each round trip's GetPieces to the
+  // next step's encode while the host woke up and freed.)
+  DevBuf* bufs[] = {&d->recv, &d->tmat, &d->decoded, &d->rowbuf, &d->scratch, &d->recv_bs, &d->prog, &d->ptab};
   if (d->ctx) {
     (void)hipSetDevice(d->ctx->device);
-    // the buffers go back to the stream-ordered pool; the host's own state
-    // waits for the stream (a query first: an idle stream costs no round trip)
-    if (hipStreamQuery(d->ctx->stream) != hipSuccess) (void)hipStreamSynchronize(d->ctx->stream);
+    if (hipStreamQuery(d->ctx->stream) == hipSuccess) {
+      for (DevBuf* b : bufs) b->release(true);
+    } else {
+      (void)hipGetLastError();  // (hipErrorNotReady from the query)
+      uint8_t* ps[8];
+      size_t cs[8];
+      int n = 0;
+      for (DevBuf* b : bufs) b->take(&ps[n], &cs[n]), n++;
+      (void)kodr_amd::DevicePool::get(d->ctx->device).free_shared(ps, cs, n, d->ctx->stream);
+    }
+  } else {
+    for (DevBuf* b : bufs) b->release(false);
   }
-  // the context stream is idle here (and the side stream's copies were joined
-  // into it): the blocks go back without an event each
-  const bool idle = d->ctx != nullptr;
-  d->recv.release(idle);
-  d->tmat.release(idle);
-  d->decoded.release(idle);
-  d->rowbuf.release(idle);
-  d->scratch.release(idle);
-  d->recv_bs.release(idle);
-  d->prog.release(idle);
-  d->ptab.release(idle);
   delete d;
   return RLNC_OK;
 }

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <list>
+#include <memory>
 #include <mutex>
 
 namespace kodr_amd {
@@ -41,7 +42,7 @@ class DevicePool {
         cached_ -= b.size;
         hipError_t e = hipSuccess;
         if (b.ev && b.stream != stream) e = hipStreamWaitEvent(stream, b.ev, 0);
-        if (b.ev) events_.push_back(b.ev);
+        if (b.ev && !b.shared) events_.push_back(b.ev);
         if (e != hipSuccess) return e;
         *out = b.p;
         *cap = b.size;
@@ -65,7 +66,7 @@ class DevicePool {
     if (!p) return;
     std::lock_guard<std::mutex> lk(mu_);
     if (idle) {
-      free_.push_front(Block{p, cap, stream, nullptr});
+      free_.push_front(Block{p, cap, stream, nullptr, nullptr});
       cached_ += cap;
       while (cached_ > limit() && !free_.empty()) release_oldest();
       return;
@@ -83,7 +84,7 @@ class DevicePool {
       (void)hipFree(p);
       return;
     }
-    free_.push_front(Block{p, cap, stream, ev});
+    free_.push_front(Block{p, cap, stream, ev, nullptr});
     cached_ += cap;
     while (cached_ > limit() && !free_.empty()) release_oldest();
   }
@@ -94,17 +95,57 @@ class DevicePool {
     while (cached_ > keep && !free_.empty()) release_oldest();
   }
 
+  // n blocks no longer needed once `stream` reaches here, ordered by ONE
+  // event (a decoder's destroy while its stream still runs: one record
+  // instead of one per buffer, and no host wait)
+  hipError_t free_shared(uint8_t* const* ps, const size_t* caps, int n, hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(mu_);
+    hipEvent_t ev = nullptr;
+    if (!events_.empty()) {
+      ev = events_.back();
+      events_.pop_back();
+    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      ev = nullptr;
+    }
+    if (!ev || hipEventRecord(ev, stream) != hipSuccess) {  // cannot order reuse: free for real
+      if (ev) events_.push_back(ev);
+      (void)hipStreamSynchronize(stream);
+      for (int i = 0; i < n; i++)
+        if (ps[i]) (void)hipFree(ps[i]);
+      return hipGetLastError();
+    }
+    auto ref = std::make_shared<SharedEvent>(ev, this);
+    for (int i = 0; i < n; i++) {
+      if (!ps[i]) continue;
+      free_.push_front(Block{ps[i], caps[i], stream, ev, ref});
+      cached_ += caps[i];
+    }
+    ref.reset();
+    while (cached_ > limit() && !free_.empty()) release_oldest();
+    return hipSuccess;
+  }
+
   size_t cached() {
     std::lock_guard<std::mutex> lk(mu_);
     return cached_;
   }
 
  private:
+  // an event shared by the blocks of one free_shared: back to events_ when
+  // the last of them leaves the cache (its destructor runs with mu_ held)
+  struct SharedEvent {
+    hipEvent_t ev;
+    DevicePool* pool;
+    SharedEvent(hipEvent_t e, DevicePool* p) : ev(e), pool(p) {}
+    SharedEvent(const SharedEvent&) = delete;
+    ~SharedEvent() { pool->events_.push_back(ev); }
+  };
   struct Block {
     uint8_t* p;
     size_t size;
     hipStream_t stream;
     hipEvent_t ev;
+    std::shared_ptr<SharedEvent> shared;  // set: ev belongs to it (not returned per block)
   };
 
   static size_t round(size_t b) {
@@ -124,7 +165,7 @@ class DevicePool {
     cached_ -= b.size;
     if (b.ev) (void)hipEventSynchronize(b.ev);
     (void)hipFree(b.p);
-    if (b.ev) events_.push_back(b.ev);
+    if (b.ev && !b.shared) events_.push_back(b.ev);
   }
 
   std::mutex mu_;
