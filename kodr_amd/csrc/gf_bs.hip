@@ -1058,6 +1058,10 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
     p.rpw = (int)(((kpad + kw - 1) / kw + kBsChunk - 1) / kBsChunk * kBsChunk);
     p.lds_bytes = bs_lds_bytes(kw, p.rpw, group && kw == 1 && bs_direct_allowed());
   }
+  if (const char* env = tune_env("KODR_BS_WG_PER_CU")) {  // occupancy probe: LDS padding caps workgroups per CU
+    const size_t n = (size_t)std::max(1, atoi(env));
+    p.lds_bytes = std::max(p.lds_bytes, kLdsPerCu / n - 64);
+  }
 #endif
   // the side product's partial sums: kSideUnits x KW dwords x 4
   const size_t side_lds = sk.ncols ? (size_t)kSideUnits * p.kw * 16 : 0;
