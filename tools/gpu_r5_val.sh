@@ -44,3 +44,12 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-f
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- "${HB[@]}" \
   > "$OUT/bench_write.json" 2> "$OUT/write.err" || { tail -20 "$OUT/write.err"; exit 1; }
 python3 "$R/tools/pmc_roundtrip.py" "$OUT" "$OUT/bench_fetch.json" > "$OUT/pmc_roundtrip.json" && cat "$OUT/pmc_roundtrip.json"
+# the N = 2 line rehearsed on one GPU (two ranks on device 0 over gloo,
+# KODR_BENCH_REHEARSE=1: plumbing, not scaling)
+cd "$R"
+KODR_BENCH_REHEARSE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 --cpu-seconds 2 > "$OUT/bench_n2.json" 2> "$OUT/bench_n2.err" || { tail -30 "$OUT/bench_n2.err"; exit 1; }
+python3 - "$OUT/bench_n2.json" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+print("N=2 rehearsal value", d["value"], d["n_gpus"], "rt", d["roundtrip"]["us_per_generation"], "encode", d["encode"]["value"], "cpu", (d.get("cpu_baseline") or {}).get("value"))
+PY
