@@ -75,7 +75,7 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
-  // hand the block to the caller (who frees it with DevicePool::free_shared)
+  // hand the block to the caller (who frees it with DevicePool::defer_free)
   void take(uint8_t** pp, size_t* pc) {
     *pp = p;
     *pc = cap;
@@ -521,6 +521,7 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
   if (!ctx) return RLNC_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  kodr_amd::DevicePool::get(ctx->device).drop_stream(ctx->stream);  // destroyed decoders' blocks, now idle
   ctx->stage.release();
   ctx->elim_tab.release();
   ctx->elim_out.release();
@@ -1357,9 +1358,10 @@ int rlnc_decoder_create(rlnc_ctx* ctx, size_t k, rlnc_decoder** out) {
 int rlnc_decoder_destroy(rlnc_decoder* d) {
   if (!d) return RLNC_OK;
   // The device buffers go back to the stream-ordered pool without a host
-  // wait: with the context stream idle (a query) at once, else ordered by one
-  // event on it for all of them (every use of them -- copies, products, the
-  // side stream's copies joined into it -- is ordered on that stream).  The
+  // wait: with the context stream idle (a query) at once, else pending until
+  // the pool's next allocation orders them behind one event on that stream
+  // (every use of them -- copies, products, the side stream's copies joined
+  // into it -- is ordered there; DevicePool::defer_free).  The
   // host state goes now; no pending device work reads host memory of the
   // decoder's own.  (Until round 5 a destroy behind pending work waited for
   // the stream: the GPU sat idle from each round trip's GetPieces to the
@@ -1371,11 +1373,13 @@ int rlnc_decoder_destroy(rlnc_decoder* d) {
       for (DevBuf* b : bufs) b->release(true);
     } else {
       (void)hipGetLastError();  // (hipErrorNotReady from the query)
-      uint8_t* ps[8];
-      size_t cs[8];
-      int n = 0;
-      for (DevBuf* b : bufs) b->take(&ps[n], &cs[n]), n++;
-      (void)kodr_amd::DevicePool::get(d->ctx->device).free_shared(ps, cs, n, d->ctx->stream);
+      kodr_amd::DevicePool& pool = kodr_amd::DevicePool::get(d->ctx->device);
+      for (DevBuf* b : bufs) {
+        uint8_t* p;
+        size_t c;
+        b->take(&p, &c);
+        pool.defer_free(p, c, d->ctx->stream);
+      }
     }
   } else {
     for (DevBuf* b : bufs) b->release(false);

@@ -33,6 +33,7 @@ class DevicePool {
     const size_t need = round(bytes);
     {
       std::lock_guard<std::mutex> lk(mu_);
+      if (!pending_.empty()) flush_pending();
       auto best = free_.end();
       for (auto it = free_.begin(); it != free_.end(); ++it)
         if (it->size >= need && it->size <= 2 * need && (best == free_.end() || it->size < best->size)) best = it;
@@ -92,37 +93,35 @@ class DevicePool {
   // free cached blocks until at most `keep` bytes remain
   void trim(size_t keep) {
     std::lock_guard<std::mutex> lk(mu_);
+    if (!pending_.empty()) flush_pending();
     while (cached_ > keep && !free_.empty()) release_oldest();
   }
 
-  // n blocks no longer needed once `stream` reaches here, ordered by ONE
-  // event (a decoder's destroy while its stream still runs: one record
-  // instead of one per buffer, and no host wait)
-  hipError_t free_shared(uint8_t* const* ps, const size_t* caps, int n, hipStream_t stream) {
+  // p is no longer needed once `stream` reaches its current end, but the
+  // caller records nothing: the block waits in a pending list, and the next
+  // alloc() orders all pending blocks of a stream behind ONE event recorded
+  // there (a decoder's destroy while its stream still runs: no GPU packet
+  // per buffer, no host wait; an event per buffer, or per decoder, sat as
+  // marker packets between a round trip's GetPieces and the next encode)
+  void defer_free(uint8_t* p, size_t cap, hipStream_t stream) {
+    if (!p) return;
     std::lock_guard<std::mutex> lk(mu_);
-    hipEvent_t ev = nullptr;
-    if (!events_.empty()) {
-      ev = events_.back();
-      events_.pop_back();
-    } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-      ev = nullptr;
+    pending_.push_back(Block{p, cap, stream, nullptr, nullptr});
+  }
+  // the stream is idle (the caller synchronised it) and about to go away:
+  // its pending blocks are reusable at once
+  void drop_stream(hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto it = pending_.begin(); it != pending_.end();) {
+      if (it->stream == stream) {
+        free_.push_front(Block{it->p, it->size, nullptr, nullptr, nullptr});
+        cached_ += it->size;
+        it = pending_.erase(it);
+      } else {
+        ++it;
+      }
     }
-    if (!ev || hipEventRecord(ev, stream) != hipSuccess) {  // cannot order reuse: free for real
-      if (ev) events_.push_back(ev);
-      (void)hipStreamSynchronize(stream);
-      for (int i = 0; i < n; i++)
-        if (ps[i]) (void)hipFree(ps[i]);
-      return hipGetLastError();
-    }
-    auto ref = std::make_shared<SharedEvent>(ev, this);
-    for (int i = 0; i < n; i++) {
-      if (!ps[i]) continue;
-      free_.push_front(Block{ps[i], caps[i], stream, ev, ref});
-      cached_ += caps[i];
-    }
-    ref.reset();
     while (cached_ > limit() && !free_.empty()) release_oldest();
-    return hipSuccess;
   }
 
   size_t cached() {
@@ -131,7 +130,7 @@ class DevicePool {
   }
 
  private:
-  // an event shared by the blocks of one free_shared: back to events_ when
+  // an event shared by the pending blocks of one stream (flush_pending): back to events_ when
   // the last of them leaves the cache (its destructor runs with mu_ held)
   struct SharedEvent {
     hipEvent_t ev;
@@ -159,6 +158,36 @@ class DevicePool {
     }();
     return lim;
   }
+  // the pending blocks into the cache, one event per stream (mu_ held)
+  void flush_pending() {
+    while (!pending_.empty()) {
+      const hipStream_t st = pending_.front().stream;
+      hipEvent_t ev = nullptr;
+      if (!events_.empty()) {
+        ev = events_.back();
+        events_.pop_back();
+      } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        ev = nullptr;
+      }
+      const bool ok = ev && hipEventRecord(ev, st) == hipSuccess;
+      if (!ok) {  // cannot order reuse: wait for the stream
+        if (ev) events_.push_back(ev);
+        (void)hipGetLastError();
+        (void)hipStreamSynchronize(st);
+      }
+      auto ref = ok ? std::make_shared<SharedEvent>(ev, this) : nullptr;
+      for (auto it = pending_.begin(); it != pending_.end();) {
+        if (it->stream == st) {
+          free_.push_front(Block{it->p, it->size, st, ok ? ev : nullptr, ref});
+          cached_ += it->size;
+          it = pending_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    while (cached_ > limit() && !free_.empty()) release_oldest();
+  }
   void release_oldest() {  // mu_ held
     Block b = free_.back();
     free_.pop_back();
@@ -170,6 +199,7 @@ class DevicePool {
 
   std::mutex mu_;
   std::list<Block> free_;  // most recently freed first
+  std::list<Block> pending_;  // defer_free'd, not yet ordered by an event
   std::list<hipEvent_t> events_;
   size_t cached_ = 0;
 };
