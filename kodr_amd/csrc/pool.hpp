@@ -198,9 +198,11 @@ class DevicePool {
   }
 
   std::mutex mu_;
+  // (declared before the block lists: a block's SharedEvent returns its event
+  // here when the lists are destroyed at exit)
+  std::list<hipEvent_t> events_;
   std::list<Block> free_;  // most recently freed first
   std::list<Block> pending_;  // defer_free'd, not yet ordered by an event
-  std::list<hipEvent_t> events_;
   size_t cached_ = 0;
 };
 
