@@ -2214,7 +2214,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       cg.rows[i] = (int)defer[c0 + i].rows;
     }
     HIPC(kodr_amd::copy_bitslice_rows_grouped(cg, (int)nc, pitch, defer[c0].dpitch, piece_len,
-                                              side ? ctx->side : ctx->stream));
+                                              side ? ctx->side : ctx->stream, side));
   }
   return RLNC_OK;
   };

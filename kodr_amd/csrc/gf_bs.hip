@@ -924,12 +924,14 @@ bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, con
          ncols / kBsBlock <= 0x7fffffff;
 }
 
-// copy workgroups resident per CU at most (16 of its 32 wave slots): room for
-// an elimination workgroup of 16 waves beside them
-constexpr int kCopyWgPerCu = 4;
+// copy workgroups per CU over the launch beside the elimination (16 of a
+// CU's 32 wave slots: room for an elimination workgroup of 16 waves), and
+// alone (after it: 187 against 198 us for the round trip's 16 generations at
+// 4, profiles/r05/copy_order/)
+constexpr int kCopyWgPerCu = 4, kCopyWgPerCuAlone = 16;
 
 hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
-                                      hipStream_t stream) {
+                                      hipStream_t stream, bool beside) {
   if (n <= 0) return hipSuccess;
   if (n > kCopyGroupMax) return hipErrorInvalidValue;
   int maxr = 0;
@@ -941,7 +943,8 @@ hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, 
   const size_t nblk = ncols / kBsBlock, total = (size_t)maxr * nblk * 2;  // two lanes per block
   if (!total) return hipSuccess;
   // at most kCopyWgPerCu workgroups (4 waves each) per CU over the launch
-  static const int wg_per_cu = tune_env("KODR_COPY_WG_PER_CU") ? atoi(tune_env("KODR_COPY_WG_PER_CU")) : kCopyWgPerCu;
+  static const int wg_tune = tune_env("KODR_COPY_WG_PER_CU") ? atoi(tune_env("KODR_COPY_WG_PER_CU")) : 0;
+  const int wg_per_cu = wg_tune ? wg_tune : beside ? kCopyWgPerCu : kCopyWgPerCuAlone;
   const size_t cap = std::max<size_t>(1, (size_t)std::max(wg_per_cu, 1) * 256 / (size_t)n);
   const size_t gx = std::min<size_t>((total + 255) / 256, cap);
   hipLaunchKernelGGL(copy_bitslice_grouped_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, stream, g, spitch,

@@ -181,8 +181,10 @@ struct CopyGroup {
 };
 bool copy_bitslice_ok(const uint8_t* src, size_t spitch, const uint8_t* dst, const uint8_t* dst_bs, size_t dpitch,
                       size_t ncols);
+// beside: the copies share the GPU with the elimination kernel (capped
+// residency, so its workgroups find room); else they run alone
 hipError_t copy_bitslice_rows_grouped(const CopyGroup& g, int n, size_t spitch, size_t dpitch, size_t ncols,
-                                      hipStream_t stream);
+                                      hipStream_t stream, bool beside = false);
 
 // byte offsets of the 256 coefficient bodies (copy 0) from body 0 (diagnostics)
 hipError_t bs_body_offsets(int device, uint32_t* host_out);
