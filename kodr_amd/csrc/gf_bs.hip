@@ -364,8 +364,27 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     }
     return;
   }
+  // MODE 34 (tuning): the row groups of one (generation, column chunk) on one
+  // CU -- blocks L, L + 256, ... of the launch land on CU L mod 256 in the
+  // dispatcher's first round -- so that their rows are shared through the
+  // CU's L1 instead of each re-read from L2
+  int cm_g = blockIdx.y, cm_rg = -1, cm_cx = -1;
+  if constexpr (MODE == 34 && GRP) {
+    const int S = nrg < 16 ? nrg : 16;
+    const long nb = gridDim.x, T = nb * gridDim.y;
+    if (16 % S == 0 && nrg % S == 0 && nb % nrg == 0 && T % (256L * S) == 0) {
+      const long L = (long)blockIdx.y * nb + blockIdx.x;
+      const long c = L & 255, q = L >> 8;
+      const long u = (q / S) * 256 + c;
+      const int nhi = nrg / S, ncxp = (int)(nb / nrg);
+      const long t = u / nhi;
+      cm_rg = (int)(u % nhi) * S + (int)(q % S);
+      cm_cx = (int)(t % ncxp);
+      cm_g = (int)(t / ncxp);
+    }
+  }
   if constexpr (GRP) {
-    const int g = blockIdx.y;
+    const int g = cm_g;
     A += (size_t)g * grp.a_stride;
     X = grp.x[g];
     Y += (size_t)g * grp.y_stride;
@@ -374,7 +393,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // rows of its task, so there is no cross-wave fold; its accumulators leave
   // the asm in registers and are transposed and stored straight from there
   // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
-  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33) &&
+  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34) &&
                          (RP == 2 || RP == 3);
   uint32_t* red = lds;
   uint32_t* tgt_l = DIRECT ? lds : lds + 64 * 64;
@@ -484,8 +503,8 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // XCD-aware order: the nrg row groups of one column chunk go to blocks
   // b, b+8, ... (one XCD) and re-read that chunk from its L2.  Speed only.
   const int b = blockIdx.x;
-  const int rg = (b >> 3) % nrg;
-  const int cx = (b / (8 * nrg)) * 8 + (b & 7);
+  const int rg = cm_rg >= 0 ? cm_rg : (b >> 3) % nrg;
+  const int cx = cm_cx >= 0 ? cm_cx : (b / (8 * nrg)) * 8 + (b & 7);
   // the side product's partial sums: past the programs (bs_lds_bytes)
   constexpr bool SIDE = !GRP && MODE == 0;
   uint32_t* side_part = lds + 64 * 64 + 256 + KW * rpw * kBsRows + 4;
@@ -876,7 +895,7 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     g.y_stride = group->y_stride;
     // gridDim.x is a multiple of 8, so the XCD order of each generation's
     // blocks is the single-generation one; the two-row ring (plain loop only)
-    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 ? 2 : KODR_BS_P;
+    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 34 ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
                        lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, BsSideK{});
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
@@ -1104,6 +1123,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 14 ? KODR_BS_CALL(KW_, 14) : mode == 20 ? KODR_BS_CALL(KW_, 20)           \
          : mode == 30 ? KODR_BS_CALL(KW_, 30) : mode == 31 ? KODR_BS_CALL(KW_, 31)           \
          : mode == 32 ? KODR_BS_CALL(KW_, 32) : mode == 33 ? KODR_BS_CALL(KW_, 33)           \
+         : mode == 34 ? KODR_BS_CALL(KW_, 34)                                                 \
                                                : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
