@@ -364,15 +364,25 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     }
     return;
   }
-  // MODE 34 (tuning): the row groups of one (generation, column chunk) on one
-  // CU -- blocks L, L + 256, ... of the launch land on CU L mod 256 in the
-  // dispatcher's first round -- so that their rows are shared through the
-  // CU's L1 instead of each re-read from L2
+  // DIRECT (one wave per workgroup in a grouped launch): the wave runs all K
+  // rows of its task, so there is no cross-wave fold; its accumulators leave
+  // the asm in registers and are transposed and stored straight from there
+  // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
+  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34) &&
+                         (RP == 2 || RP == 3);
+  // A direct launch whose grid is resident at once (<= 16 workgroups per CU
+  // on 256 CUs: blocks L, L + 256, ... land on CU L mod 256) puts the row
+  // groups of one (generation, column chunk) on one CU, which then share the
+  // rows through its L1 instead of re-reading them from L2: the B = 32 x 16
+  // generation launch 228-229 -> 222-223 us at 2,262 -> 2,302 MHz
+  // (profiles/r05/cumap/).  Launches of several rounds keep the XCD order
+  // below (co-located there: +4.5 % at B = 256, the placement of later rounds
+  // is the dispatcher's).  MODE 34 (tuning) co-locates in any launch.
   int cm_g = blockIdx.y, cm_rg = -1, cm_cx = -1;
-  if constexpr (MODE == 34 && GRP) {
+  if constexpr (DIRECT) {
     const int S = nrg < 16 ? nrg : 16;
     const long nb = gridDim.x, T = nb * gridDim.y;
-    if (16 % S == 0 && nrg % S == 0 && nb % nrg == 0 && T % (256L * S) == 0) {
+    if ((MODE == 34 || T <= 256L * 16) && 16 % S == 0 && nrg % S == 0 && nb % nrg == 0 && T % (256L * S) == 0) {
       const long L = (long)blockIdx.y * nb + blockIdx.x;
       const long c = L & 255, q = L >> 8;
       const long u = (q / S) * 256 + c;
@@ -389,12 +399,6 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     X = grp.x[g];
     Y += (size_t)g * grp.y_stride;
   }
-  // DIRECT (one wave per workgroup in a grouped launch): the wave runs all K
-  // rows of its task, so there is no cross-wave fold; its accumulators leave
-  // the asm in registers and are transposed and stored straight from there
-  // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
-  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34) &&
-                         (RP == 2 || RP == 3);
   uint32_t* red = lds;
   uint32_t* tgt_l = DIRECT ? lds : lds + 64 * 64;
   uint32_t* prog_l = tgt_l + 256;
