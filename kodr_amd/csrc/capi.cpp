@@ -2318,7 +2318,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // a lone decoder's attempts side by side (gf_elim_mc_spec): virtual
     // decoder v runs attempt v on the same vectors; the first that succeeds
     // is the decoder's result
-    int S = gpu.size() == 1 ? kodr_amd::gf_elim_mc_spec((int)k, 1) : 1;
+    const int S = gpu.size() == 1 ? kodr_amd::gf_elim_mc_spec((int)k, 1) : 1;
+    const size_t nv = nc * (size_t)S;
     if (S > 1) {
       for (int v = 1; v < S; v++) {
         a.vecs[v] = a.vecs[0];
@@ -2326,15 +2327,10 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       }
       a.spec = S;
     }
-    TRY(ctx_elim_mc(ctx, k, nc * (size_t)S, &a));
-    if (S > 1 && !kodr_amd::gf_elim_mc_direct(a, S)) {  // not a launch mc4 takes (a partial batch, small k)
-      S = 1;
-      a.spec = 0;
-      TRY(ctx_elim_mc(ctx, k, nc, &a));
-    }
-    const size_t nv = nc * (size_t)S;
+    TRY(ctx_elim_mc(ctx, k, nv, &a));
     const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nv);
     const bool direct = kodr_amd::gf_elim_mc_direct(a, (int)nv);
+    if (S > 1 && !direct) return RLNC_ERR_HIP;  // (cannot happen: the side-by-side attempts are mc4's)
     if (direct) {  // T and status straight into pinned host memory
       TRY(ctx_elim_pin(ctx, hdr + nv * k * k));
       a.direct = 1;
