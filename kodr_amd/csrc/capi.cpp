@@ -2315,24 +2315,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     a.out_pitch = opitch;
     a.counts = reinterpret_cast<int*>(ctx->elim_out.p);
     a.k = (int)k;
-    // a lone decoder's attempts side by side (gf_elim_mc_spec): virtual
-    // decoder v runs attempt v on the same vectors; the first that succeeds
-    // is the decoder's result
-    const int S = gpu.size() == 1 ? kodr_amd::gf_elim_mc_spec((int)k, 1) : 1;
-    const size_t nv = nc * (size_t)S;
-    if (S > 1) {
-      for (int v = 1; v < S; v++) {
-        a.vecs[v] = a.vecs[0];
-        a.n[v] = a.n[0];
-      }
-      a.spec = S;
-    }
-    TRY(ctx_elim_mc(ctx, k, nv, &a));
-    const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nv);
-    const bool direct = kodr_amd::gf_elim_mc_direct(a, (int)nv);
-    if (S > 1 && !direct) return RLNC_ERR_HIP;  // (cannot happen: the side-by-side attempts are mc4's)
+    TRY(ctx_elim_mc(ctx, k, nc, &a));
+    const bool mc = kodr_amd::gf_elim_mc_taken(a, (int)nc);
+    const bool direct = kodr_amd::gf_elim_mc_direct(a, (int)nc);
     if (direct) {  // T and status straight into pinned host memory
-      TRY(ctx_elim_pin(ctx, hdr + nv * k * k));
+      TRY(ctx_elim_pin(ctx, hdr + nc * k * k));
       a.direct = 1;
       a.out = ctx->elim_pin_dev + hdr;
       a.out_pitch = k;
@@ -2340,12 +2327,12 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       a.counts = reinterpret_cast<int*>(ctx->elim_pin_dev);
       if (!cont && c0 == 0) {  // fresh decoders: T on the device too, for a grouped GetPieces
         ctx->elim_tdev.bind(ctx->device, ctx->stream);
-        TRY(ctx->elim_tdev.reserve((gpu.size() - 1 + S) * k * k));
+        TRY(ctx->elim_tdev.reserve(gpu.size() * k * k));
         ctx->tdev_seq++;
       }
       if (!cont) a.out_dev = ctx->elim_tdev.p + c0 * k * k;
     }
-    HIPC(kodr_amd::gf_elim(a, (int)nv, ctx->stream));
+    HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
       prep_rows();
       TRY(launch_copies());
@@ -2406,9 +2393,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
 #else
     const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
 #endif
-    std::vector<int> cntv(nv), attv(nv, 0);
+    std::vector<int> cntv(nc), attv(nc, 0);
     const uint8_t* tstates = hostp + hdr;  // T rows (tonly: k x k per decoder) or whole states
-    size_t spec_off = 0;                   // side-by-side attempts: the successful one's T
     // a decoder whose launch failed (a singular panel block, or a singular C)
     // takes kodr's route on the host from its state before the batch: started
     // on its own thread as soon as it reports, beside the rest of the launch
@@ -2431,20 +2417,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     };
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      // (side-by-side attempts: a failed attempt is not the decoder's failure;
-      // one that none of them eliminates takes the host route below)
-      TRY(elim_direct_wait(ctx, a, nv, cntv.data(), attv.data(),
-                           S > 1 ? std::function<int(size_t)>() : std::function<int(size_t)>(early_host)));
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host)));
       tstates = ctx->elim_pin + hdr;
-      if (S > 1) {
-        int s1 = -1;
-        for (int v = 0; v < S && s1 < 0; v++)
-          if (cntv[v] == (int)k) s1 = v;
-        cntv.assign(nc, s1 >= 0 ? (int)k : 0);
-        attv.assign(nc, s1 >= 0 ? s1 : 0);
-        spec_off = s1 > 0 ? (size_t)s1 * k * k : 0;
-        tstates += spec_off;
-      }
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
       HIPC(ctx->stage.d2h(hostp + hdr, k, ctx->elim_out.p + hdr + k, opitch, k, nc * k, ctx->stream));
@@ -2494,7 +2468,7 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       else
         count_elim(d, kElimHostAfterGpu);
       const bool on_dev = ok && c == k && !cont && a.out_dev;
-      d->tdev = on_dev ? a.out_dev + spec_off + i * k * k : nullptr;
+      d->tdev = on_dev ? a.out_dev + i * k * k : nullptr;
       d->tdev_seq = on_dev ? ctx->tdev_seq : 0;
     });
     if (timing) fprintf(stderr, "add_pieces_gpu: states loaded %.1f us (%zu decoders)\n", tnow() - tl0, nc);

@@ -1521,10 +1521,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
 
   const int row0 = RW * x, pr = row0 / 16, lo = row0 - 16 * pr;  // row workgroup: its panel, offset in it
   uint32_t Tout[RPW];  // row workgroup: T rows of the successful attempt (assigned on the way out)
-  // a side-by-side attempt (args.spec > 1) runs its one attempt only
-  const int spec = args.spec > 1 ? args.spec : 0;
-  const int att_last = spec ? g % spec : kMcAttempts - 1;
-  int fail = late ? 2 : 0, att = spec ? g % spec : 0;
+  int fail = late ? 2 : 0, att = 0;
   for (; !late; att++) {
     const uint32_t tag = tag0 + att;
     const int rot = mc_rot(att, k);
@@ -1765,7 +1762,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
     };
     attempt(mc_opaque_s(g), mc_opaque_s(w), mc_opaque(lane), mc_opaque_s(pubS));
     __syncthreads();  // every wave read lds.fail before the next attempt resets it
-    if (fail != 1 || att >= att_last) break;
+    if (fail != 1 || att + 1 == kMcAttempts) break;
   }
   const bool ok = fail == 0;
   if (!ok && tid == 0) mc_put_fail(pubA, tag0, tlast, 2);  // late workgroups read no input
@@ -1894,14 +1891,6 @@ size_t gf_elim_mc_pub_bytes(int k, int G) {
   return ((size_t)G * 2 * P * kMc2PanelGran + (size_t)G) * 8;
 }
 int gf_elim_mc_attempts() { return kMcAttempts; }
-
-// A lone decoder's attempts side by side: kMcAttempts virtual decoders on
-// the same vectors, attempt a on the a-th (4 x 33 workgroups at k = 256, all
-// resident), so a singular panel block costs no second pass (it took the
-// C2 AddPiece from 0.075 to 0.13 ms)
-int gf_elim_mc_spec(int k, int G) {
-  return G == 1 && k >= 2 && k <= 256 && elim_mc_mode() == 3 && mc_kernel_for(k, kMcAttempts) == 4 ? kMcAttempts : 1;
-}
 
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;

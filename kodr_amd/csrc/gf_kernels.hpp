@@ -119,9 +119,6 @@ struct ElimArgs {
   // mc2 / mc4 only (optional): the T rows of a finished decoder also to
   // device memory, out_dev + g * k * k + row * k (GetPieces reads them there)
   uint8_t* out_dev;
-  // mc4, spec > 1: decoder g runs attempt g % spec only (the same vectors
-  // launched spec times side by side: gf_elim_mc_spec)
-  int spec;
 };
 // [256][8] tables of f, 64 dwords of inverse bytes, [256][8] tables of inv(f)
 constexpr size_t kElimInvTables = 256 * 8 + 64;
@@ -148,10 +145,6 @@ size_t gf_elim_mc_pub_bytes(int k, int G);
 // tags per launch: attempts with the rows in another order after a singular
 // panel block (gf_elim.hip, kMcAttempts)
 int gf_elim_mc_attempts();
-// a launch of G decoders as G * S side-by-side attempts (S = the return
-// value: gf_elim_mc_attempts() for a lone decoder whose attempts fit one mc4
-// launch, else 1)
-int gf_elim_mc_spec(int k, int G);
 bool gf_elim_mc_taken(const ElimArgs& args, int G);
 // true when gf_elim_mc_taken and the launch honours args.direct (mc2)
 bool gf_elim_mc_direct(const ElimArgs& args, int G);
