@@ -1489,6 +1489,7 @@ def time_decode(ctx, L_, errors, dWire, n, W, k, L, dDec, reps=3, regen=None):
         best["s_median"] = round(statistics.median(tots), 6)
         best["add_s_median"] = round(statistics.median(adds), 6)
         best["add_s_max"] = round(max(adds), 6)
+        best["add_s_reps"] = [round(x * 1e6, 1) for x in adds]  # us, in rep order (each rep a fresh vector set)
     best["elimination_routes"] = routes
     macs = best["gf_rows"] * best["received"] * L
     best["apply_gf_macs"] = macs
