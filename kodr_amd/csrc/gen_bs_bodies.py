@@ -558,6 +558,10 @@ def main():
     # (the ring's stale rows; wrong products), with threaded / inlined bodies:
     # what any load path (LDS staging, deeper prefetch) could save at most
     out += emit("KODR_BS_MAIN_P2_NL", main_loop(True, False))
+    # tuning (MODE 35): the grouped two-row loop without the priority rotation
+    out += emit("KODR_BS_MAIN_P2_NOPRIO", main_loop(True, True, None))
+    # tuning (MODE 36): the rotation over the rows' pairs (priority j // 2 % 4)
+    out += emit("KODR_BS_MAIN_P2_PRIO2", main_loop(True, True, lambda j: (j // 2) % 4))
     out += emit("KODR_BS_MAIN_P2_INLINE_NL", main_loop(True, False, inline=19))
     ops2 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
     out.append("#define KODR_BS_RING_OPERANDS_P2 " + ", ".join(ops2))
