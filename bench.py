@@ -663,7 +663,7 @@ def main():
                          "hbm": {"achieved_GBps": round(legs["encode_launch"]["hbm_bytes"] / te / 1e9, 1),
                                  "peak_GBps": HBM_PEAK_GBS, "frac": legs["encode_launch"]["hbm_frac"]},
                          "note": "the round trip's dominant kernel is gf_bs_kernel (the grouped encode launch, k + 2 "
-                                 "pieces of 16 generations, and the grouped GetPieces, together ~85 % of a step): "
+                                 "pieces of 16 generations, and the grouped GetPieces, together ~89 % of a step): "
                                  "258 GF MACs per generation byte read, so neither HBM (hbm.frac) nor MFMA (a "
                                  "byte-field product) bounds it; SURVEY 8(d) prices decode against the VALU ceiling. "
                                  "achieved/frac: the encode leg's GF MACs per second (HIP events around the launch) "
