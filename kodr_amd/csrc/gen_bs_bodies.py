@@ -239,7 +239,8 @@ def ROW_PRIO(j):
     return j % 4
 
 
-def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None):
+def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None,
+              body_prio=None):
     """Input row j (0..7) of an 8-row chunk, from ring slot j % P.  v[PG]
     holds the chunk's program: lane 8j + m = the target of output row m
     (absolute lo word; hi words preset), read with v_readlane, so no LDS round
@@ -282,6 +283,8 @@ def row_lines(j, dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice
             t += [f"s_mov_b64 s[{RT}:{RT + 1}], s[{RET + 2 * j}:{RET + 2 * j + 1}]"]
         else:
             t += [f"s_add_u32 s{RT}, s{GPC}, .Lret{j}_%= - .Lpc_%=", f"s_addc_u32 s{RT + 1}, s{GPC + 1}, 0"]
+        if body_prio is not None:  # tuning: another priority for the bodies than for the row's preparation
+            t += [f"s_setprio {body_prio}"]
         t += ["s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)",
               f"s_setpc_b64 s[{h(0)}:{h(0) + 1}]",
               f".Lret{j}_%=:",
@@ -337,7 +340,8 @@ def prologue_lines(dispatch=True, sload=False):
     return pro
 
 
-def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None):
+def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=(), sload=False, inline=None,
+              body_prio=None):
     """Prologue, the shared stub (branched over) and the 8-row loop; the
     ring's first P rows arrive as asm operands (loaded by the compiler before
     the program build).  At the end of each iteration the next chunk moves
@@ -350,7 +354,7 @@ def main_loop(dispatch=True, loads=True, prio=ROW_PRIO, half_prio=None, twice=()
                 t += stub_lines(f"stub{j}", half_prio(j))
     t += [".Lloop_%=:"]
     for j in range(8):
-        t += row_lines(j, dispatch, loads, prio, half_prio, twice, sload, inline)
+        t += row_lines(j, dispatch, loads, prio, half_prio, twice, sload, inline, body_prio)
     if not sload:
         t += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32 v{PG}, v{PGN}", f"ds_read_b32 v{PGN}, v{PL}",
               f"v_add_u32_e32 v{PL}, 256, v{PL}"]
@@ -562,6 +566,9 @@ def main():
     out += emit("KODR_BS_MAIN_P2_NOPRIO", main_loop(True, True, None))
     # tuning (MODE 36): the rotation over the rows' pairs (priority j // 2 % 4)
     out += emit("KODR_BS_MAIN_P2_PRIO2", main_loop(True, True, lambda j: (j // 2) % 4))
+    # tuning (MODE 37): the row's preparation (tables, targets) at priority 3,
+    # its bodies at 0 (the preparation is the wave's dependency chain)
+    out += emit("KODR_BS_MAIN_P2_PREP", main_loop(True, True, lambda j: 3, body_prio=0))
     out += emit("KODR_BS_MAIN_P2_INLINE_NL", main_loop(True, False, inline=19))
     ops2 = [f'"+{{v[{RING + 4 * i}:{RING + 4 * i + 3}]}}"(ring[{i}])' for i in range(2 * P)]
     out.append("#define KODR_BS_RING_OPERANDS_P2 " + ", ".join(ops2))

@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // rows of its task, so there is no cross-wave fold; its accumulators leave
   // the asm in registers and are transposed and stored straight from there
   // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
-  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34 || MODE == 35 || MODE == 36) &&
+  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34 || MODE == 35 || MODE == 36 || MODE == 37) &&
                          (RP == 2 || RP == 3);
   // A direct launch whose grid is resident at once (<= 16 workgroups per CU
   // on 256 CUs: blocks L, L + 256, ... land on CU L mod 256) puts the row
@@ -696,6 +696,11 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
                    : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
                    : KODR_BS_ASM_INPUTS
                    : KODR_BS_CLOBBERS_P2_DIRECT);
+    } else if (nr > 0 && MODE == 37) {  // tuning: preparation at priority 3, bodies at 0
+      asm volatile(KODR_BS_MAIN_P2_PREP "s_waitcnt lgkmcnt(0)\n\t"
+                   : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
+                   : KODR_BS_ASM_INPUTS
+                   : KODR_BS_CLOBBERS_P2_DIRECT);
     } else if (nr > 0 && MODE == 36) {  // tuning: the rotation over row pairs
       asm volatile(KODR_BS_MAIN_P2_PRIO2 "s_waitcnt lgkmcnt(0)\n\t"
                    : KODR_BS_RING_OPERANDS_P2, KODR_BS_ACC_OUTPUTS
@@ -909,7 +914,7 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     g.y_stride = group->y_stride;
     // gridDim.x is a multiple of 8, so the XCD order of each generation's
     // blocks is the single-generation one; the two-row ring (plain loop only)
-    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || (MODE >= 30 && MODE <= 36) ? 2 : KODR_BS_P;
+    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || (MODE >= 30 && MODE <= 37) ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
                        lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, BsSideK{});
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
@@ -1138,7 +1143,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 30 ? KODR_BS_CALL(KW_, 30) : mode == 31 ? KODR_BS_CALL(KW_, 31)           \
          : mode == 32 ? KODR_BS_CALL(KW_, 32) : mode == 33 ? KODR_BS_CALL(KW_, 33)           \
          : mode == 34 ? KODR_BS_CALL(KW_, 34) : mode == 35 ? KODR_BS_CALL(KW_, 35)           \
-         : mode == 36 ? KODR_BS_CALL(KW_, 36)                                                 \
+         : mode == 36 ? KODR_BS_CALL(KW_, 36) : mode == 37 ? KODR_BS_CALL(KW_, 37)           \
                                                : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \
