@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md: 8.0 TB/s spec
 class host_elimination:
     """The comparisons' host legs run kodr's elimination on the host:
     rlnc_decoder_add_pieces and the lazy AddPiece flush would otherwise take
-    the GPU elimination themselves for large full batches (capi.cpp
+    the GPU elimination themselves for large full batches (capi_decoder.cpp
     dec_route_gpu, the context's rlnc_ctx_set_route_min_k)."""
 
     def __init__(self, ctx):

@@ -1,7 +1,7 @@
 """kodr_amd -- MI355X-native (gfx950) RLNC engine with itzmeanjan/kodr's API.
 
 Layout:
-  csrc/            HIP kernel (gf_kernels.hip), C ABI (capi.cpp), host mirror of
+  csrc/            HIP kernel (gf_kernels.hip), C ABI (capi.cpp, capi_decoder.cpp), host mirror of
                    kodr's decoder state (decoder_core.cpp)
   libkodr_rlnc.so  built in-tree by build.sh; the only compute path
   full, systematic, kodr_internals, errors

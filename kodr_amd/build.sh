@@ -16,8 +16,9 @@ pids=()
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_bs.hip -o "$OBJ"/gf_bs.o & pids+=($!)
 "$HIPCC" --offload-arch="$ARCH" "${FLAGS[@]}" -c csrc/gf_elim.hip -o "$OBJ"/gf_elim.o & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c csrc/capi.cpp -o "$OBJ"/capi.o & pids+=($!)
+"$HIPCC" "${FLAGS[@]}" -c csrc/capi_decoder.cpp -o "$OBJ"/capi_decoder.o & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c csrc/decoder_core.cpp -o "$OBJ"/decoder_core.o & pids+=($!)
 for p in "${pids[@]}"; do wait "$p" || { echo "build failed" >&2; exit 1; }; done
-"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o "$OUT" "$OBJ"/gf_kernels.o "$OBJ"/gf_bs.o "$OBJ"/gf_elim.o "$OBJ"/capi.o "$OBJ"/decoder_core.o \
+"$HIPCC" --offload-arch="$ARCH" -shared -fPIC -o "$OUT" "$OBJ"/gf_kernels.o "$OBJ"/gf_bs.o "$OBJ"/gf_elim.o "$OBJ"/capi.o "$OBJ"/capi_decoder.o "$OBJ"/decoder_core.o \
   -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "built $HERE/$OUT"

@@ -767,7 +767,7 @@ GemmConfig choose_gemm_config(size_t M, size_t K, size_t ncols) {
   // X from L2).  Timed there only at M <= 32, K = 16-128, 128 KiB and 1 MiB
   // rows (tools/bs_vs_gemm_small_k.py, profiles/r01/bs_vs_gemm_small_k.log);
   // callers with M >= 9 normally take the bit-sliced kernel instead
-  // (capi.cpp kBsMinRows, few_narrow_rows), so larger M reaches this only
+  // (capi_internal.hpp kBsMinRows, few_narrow_rows), so larger M reaches this only
   // where that kernel cannot take the shape.
   const size_t nxc = (ncols + 511) / 512;
   if (K <= 32 || (K <= 64 && (M >= 4 || nxc >= 256)) || (K <= 128 && nxc >= 512)) {

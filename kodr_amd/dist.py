@@ -30,7 +30,7 @@ def shard_generations(n_generations, world_size, rank):
 def wire_pitch(k, L):
     """Row pitch of the engine's device wire rows (vector ++ piece, k + L
     bytes, CodedPiece.Flatten data.go:52-57) padded to the 256-byte alignment
-    of its recoder and decoder rows (capi.cpp kPitchAlign)."""
+    of its recoder and decoder rows (capi_internal.hpp kPitchAlign)."""
     return (k + L + 255) // 256 * 256
 
 

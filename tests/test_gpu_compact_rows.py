@@ -1,4 +1,4 @@
-"""Compact received rows (capi.cpp dec_batch_pre, dec_uncompact): a batched
+"""Compact received rows (capi_decoder.cpp dec_batch_pre, dec_uncompact): a batched
 AddPiece of device rows writes only their bit-sliced twin; the plain bytes
 are rebuilt from it when a plain-row path needs them (the v_perm kernel of a
 few-row product, a growing receive buffer) and systematic rows are gathered

@@ -3,7 +3,7 @@ GPU (tests/cpp/occupy.hip: every CU but a few taken by a 1024-thread
 workgroup with 150 KiB of LDS for 60 ms, on another stream): gf_elim_mc2
 needs all of a launch's workgroups resident, and here most cannot start.
 The resident ones stop after a bounded wait (gf_elim.hip kMcPollSpins), the
-host gives up on decoders that never reported (capi.cpp kElimGiveUp) and
+host gives up on decoders that never reported (capi_decoder.cpp kElimGiveUp) and
 takes kodr's route with the coding vectors downloaded beside the launch, so
 the batched AddPiece call returns within 10 ms -- not after the 60 ms kernel
 -- and every decoder ends in kodr's state (the host route: the oracle's

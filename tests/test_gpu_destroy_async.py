@@ -1,4 +1,4 @@
-"""rlnc_decoder_destroy without a host wait (capi.cpp; pool.hpp free_shared):
+"""rlnc_decoder_destroy without a host wait (capi_decoder.cpp; pool.hpp defer_free):
 a decoder destroyed right after its GetPieces, with the product still
 queued, gives its buffers back ordered behind it by one event.  The next
 decoder on the same stream reuses them in stream order, and a decoder on

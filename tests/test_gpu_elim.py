@@ -92,7 +92,7 @@ def _rows(ctx, V, P, L):
 def host_references(gpu_ctx):
     # the reference decoders here run kodr's elimination on the host:
     # rlnc_decoder_add_pieces and the lazy flush would otherwise route large
-    # full batches to the GPU elimination themselves (capi.cpp dec_route_gpu)
+    # full batches to the GPU elimination themselves (capi_decoder.cpp dec_route_gpu)
     prev = gpu_ctx.route_min_k
     gpu_ctx.set_route_min_k(100000)
     yield
@@ -386,7 +386,7 @@ def test_gpu_elimination_continued_batches(gpu_ctx, k):
 def test_routed_single_decoder_vs_oracle(gpu_ctx, monkeypatch, kind, k):
     """rlnc_decoder_add_pieces (device rows) and lazy AddPiece flushes route a
     large decoder's full batch to the multi-workgroup GPU elimination
-    (capi.cpp dec_route_gpu); singular blocks fall back to the host.  Both
+    (capi_decoder.cpp dec_route_gpu); singular blocks fall back to the host.  Both
     entry points against the oracle's literal decoder: return code, rows
     consumed, counters, coefficients and decoded pieces."""
     gpu_ctx.set_route_min_k(128)

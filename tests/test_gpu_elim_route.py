@@ -1,6 +1,6 @@
 """Which route eliminated a decoder's batch, and that the GPU route is total
 for invertible C (gf_elim.hip attempts: a singular panel block re-runs the
-launch with the rows rotated; capi.cpp rlnc_decoder_elim_stats reports it).
+launch with the rows rotated; capi_decoder.cpp rlnc_decoder_elim_stats reports it).
 
 kodr eliminates on every AddPiece (full/decoder.go:50-66) with a pivot search
 down the whole column (kodr_internals/matrix/decoder_state.go:23-35); the GPU

@@ -136,7 +136,7 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
 
 
 # grouped bit-sliced launches that plan each KW instance of
-# gf_bs_kernel<KW, 0, true, 2> (capi.cpp plan_gemm_bs): (G, k, L, count) -> KW
+# gf_bs_kernel<KW, 0, true, 2> (gf_bs.hip plan_gemm_bs): (G, k, L, count) -> KW
 GROUPED_KW_SHAPES = [((2, 8, 4096, 40), 1), ((2, 16, 4096, 40), 2), ((2, 24, 4096, 17), 3),
                      ((2, 32, 4096, 17), 4), ((2, 40, 4096, 9), 6), ((2, 64, 4096, 9), 8),
                      ((2, 96, 4096, 9), 16)]

@@ -1,4 +1,4 @@
-"""GPU parity of lazy AddPiece (capi.cpp dec_add): coding vectors that cannot
+"""GPU parity of lazy AddPiece (capi_decoder.cpp dec_add): coding vectors that cannot
 complete the rank are queued and eliminated as one batch when the state is
 next observed, and device pieces are copied by one gather at the next data
 flush (the opt-in borrowed entry point; the default one copies each piece in
@@ -166,7 +166,7 @@ def test_lazy_counters_every_call(gpu_ctx):
 
 
 def test_lazy_queue_past_gather_limit(gpu_ctx):
-    # k = 1100: more queued device pieces than one gather takes (capi.cpp
+    # k = 1100: more queued device pieces than one gather takes (capi_decoder.cpp
     # kPendMax = 1024), short pieces
     rng = np.random.default_rng(0x44C)
     k, L = 1100, 64

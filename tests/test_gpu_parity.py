@@ -764,7 +764,7 @@ def test_contexts_on_threads_run_concurrently(gpu_ctx):
 def test_decoder_kernel_choice_and_result(gpu_ctx, k, lost, bs):
     """Systematic decode with `lost` pieces replaced by coded ones: the GF
     rows run on the bit-sliced kernel from 16 rows, or from 9 rows when the
-    twin to build is at most 16 MiB (capi.cpp dec_gemm); bytes equal P
+    twin to build is at most 16 MiB (capi_decoder.cpp dec_gemm); bytes equal P
     either way."""
     L = 131072
     rng = np.random.default_rng(k + lost)
@@ -818,7 +818,7 @@ def test_batch_add_many_dependent_rows_past_the_precopy(gpu_ctx, dev):
     """A batch whose accepted rows exceed what AddPieces copies ahead of the
     elimination (required + 16): 40 rows spanning only 8 dimensions come
     first, then independent ones; the late rows are copied after the
-    elimination and the decode still equals P (capi.cpp add_pieces)."""
+    elimination and the decode still equals P (capi_decoder.cpp rlnc_decoder_add_pieces)."""
     k, L = 16, 4096
     rng = np.random.default_rng(77 + dev)
     P = rng.integers(0, 256, (k, L), dtype=np.uint8)
@@ -855,7 +855,7 @@ def test_generation_past_4_gib(gpu_ctx):
     # A 5 GiB generation (40 pieces of 128 MiB): past the kernels' 32-bit
     # buffer offsets, so gf_gemm (B = 1) runs it in 3 row chunks and gf_bs
     # (B >= 9, decode) in 2, with the partial products XORed together
-    # (capi.cpp gemm_k_chunked).  Column windows at the start, the middle
+    # (capi_internal.hpp gemm_k_chunked).  Column windows at the start, the middle
     # (unaligned) and the ragged end are checked against the oracle; the
     # round trip through the decoder is checked on the same windows.
     L_ = _lib.lib()
