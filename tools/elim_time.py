@@ -44,12 +44,12 @@ for k in ks:
                 ctx.synchronize()
                 t0 = time.perf_counter()
                 if mode == "host":
-                    os.environ["KODR_ROUTE_MIN_K"] = "100000"  # kodr's elimination on the host (no GPU route)
+                    ctx.set_route_min_k(100000)  # kodr's elimination on the host (no GPU route)
                     for g in range(G):
                         c = ctypes.c_size_t()
                         st = L_.rlnc_decoder_add_pieces(decs[g], bufs[g], n, pitch, L, 1, ctypes.byref(c))
                         assert st in (0, 3), st
-                    os.environ.pop("KODR_ROUTE_MIN_K")
+                    ctx.set_route_min_k(224)
                 else:
                     arr = (ctypes.c_void_p * G)(*[x.value for x in decs])
                     rp = (ctypes.c_void_p * G)(*bufs)
