@@ -746,9 +746,6 @@ constexpr uint32_t kMcAbort = 1u;
 // (>= ~50 cycles) 2^17 times >= ~3 ms.  Counted, not timed: a clock read in
 // the poll loops (s_memrealtime) slowed the chain by ~13 % (58 -> 66 us).
 constexpr int kMcPollSpins = 1 << 13;
-#ifndef KODR_MC_PROBE  // mc4 hand-off waits: probe one granule between full polls
-#define KODR_MC_PROBE 0
-#endif
 constexpr int kMcLdsSpins = 1 << 17;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -1419,24 +1416,6 @@ __device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t ta
       if (const int lf = __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return lf;
     if (spins > kMcPollSpins) return 2;
     __builtin_amdgcn_s_sleep(1);
-#if KODR_MC_PROBE
-    // not there yet: wait on lane 0's first granule alone (one address for
-    // the wave, one request) before the next full poll -- the full polls of
-    // many waiting workgroups otherwise fill the fabric (16 decoders' mc4:
-    // 528 workgroups re-reading up to 2 KiB per wave)
-    if (__builtin_amdgcn_readfirstlane(mc_tag_state(x[0], tag, tlast)) < 0) {  // lane 0's: wave-uniform
-      const uint64_t pa = reinterpret_cast<uint64_t>(src);
-      const gu64* p0 = reinterpret_cast<const gu64*>(
-          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)pa));
-      for (;; spins++) {
-        const uint64_t y = __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readfirstlane(mc_tag_state(y, tag, tlast)) >= 0 || spins > kMcPollSpins) break;
-        if (lfail && __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-#endif
   }
 }
 
