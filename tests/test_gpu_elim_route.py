@@ -264,3 +264,41 @@ def test_tags_stay_fresh_across_buffer_growth(gpu_ctx):
         gpu_ctx.synchronize()
         for d in ds:
             gpu_ctx.free(d)
+
+
+@pytest.mark.parametrize("G", [2, 7])
+def test_largest_mc4_launch(gpu_ctx, G):
+    """rlnc_decoders_add_pieces_gpu at k = 256 with up to 7 decoders: one
+    gf_elim_mc4 launch of G x 33 workgroups (7: 231, the most the
+    kElimMcMaxBlocks = 256 cap admits), seed 7 (a rotated attempt) among
+    them; every decoder equals the oracle and stays on the GPU."""
+    k, L = 256, 48
+    seeds = [7] + list(range(200, 200 + G - 1))
+    hs, ds, Ps, Vs, Cs = [], [], [], [], []
+    for seed in seeds:
+        V = pr.device_vectors(seed, k + 2, k)
+        P = np.random.default_rng(seed).integers(0, 256, (k, L), dtype=np.uint8)
+        C = oracle.encode(P, V)
+        d, pitch = _rows(gpu_ctx, V, C)
+        hs.append(_new(gpu_ctx, k))
+        ds.append(d)
+        Ps.append(P)
+        Vs.append(V)
+        Cs.append(C)
+    arr = (ctypes.c_void_p * G)(*[h.value for h in hs])
+    rows = (ctypes.c_void_p * G)(*ds)
+    counts = (ctypes.c_size_t * G)(*([k + 2] * G))
+    cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+    errors.check(_lib.lib().rlnc_decoders_add_pieces_gpu(arr, G, rows, counts, pitch, L, cons, sts))
+    for g in range(G):
+        assert sts[g] in (0, 3)
+        _check_vs_oracle(hs[g], Ps[g], Vs[g], Cs[g], consumed=cons[g])
+        s = _stats(hs[g])
+        att = pr.expected_attempt(Vs[g][:k])
+        assert s["gpu"] == 1 and s["host_after_gpu"] == 0, (g, s)
+        assert s["gpu_retried"] == (1 if att > 0 else 0), (g, s, att)
+    for h in hs:
+        _lib.lib().rlnc_decoder_destroy(h)
+    gpu_ctx.synchronize()
+    for d in ds:
+        gpu_ctx.free(d)
