@@ -276,24 +276,37 @@ class RoundTripStep:
          the piece columns of set i % nsets -- full/encoder.go:61-71 n times
          per generation; HIP events around it;
       2. G fresh decoders take their n wire rows in ONE batched AddPiece call
-         (rlnc_decoders_add_pieces_gpu: row copies + bit-sliced twin beside
-         the multi-workgroup elimination, gf_elim_mc_kernel) --
+         (rlnc_decoders_add_pieces_gpu: the multi-workgroup elimination,
+         gf_elim_mc_kernel, then the rows' bit-sliced twin) --
          full/decoder.go:50-66 row by row, same state;
       3. ONE grouped GetPieces (rlnc_decoders_get_pieces_device) writes the
          G decoded generations to device memory; HIP events around it;
       4. the next step's G decoders are constructed while GetPieces runs
          (host only), then this step's decoders are destroyed (their buffers
-         go back to the pool ordered on the stream, no host wait: the next
-         step's encode is queued while GetPieces still runs, as a service
-         decoding one batch after another would).
+         go back to the pool ordered on the stream, no host wait).
+    Pipelined (dctx: the decoders' own context, so their own stream): the
+    encoders stay on ctx, and once step i's AddPiece call has returned (its
+    elimination done), step i + 1's encode -- which depends on nothing of
+    step i's decode -- is queued on the encoders' stream before step i's
+    GetPieces, so it runs beside step i's twin copy and GetPieces instead of
+    after them.  The decoders' stream waits for the encode it reads (an
+    event); the encode of step i + 1 rewrites the wire rows of set
+    (i + 1) % nsets, which only step i - 1's twin copy read, and that copy
+    precedes step i's elimination on the decoders' stream (done when the
+    AddPiece call returns; a given-up decoder's give-up clock starts only
+    once everything ahead of the launch is done).  Within the timed phase
+    no encode is queued past its last step (begin_phase), so K timed steps
+    are exactly K encodes and K decodes.
     Decoder construction stays inside the timed steps (each step constructs
     the next one's; the first warmup step its own); kodr's decoder bench
     builds its decoder outside the timer (benches/full/decoder_test.go:71-94)."""
 
-    def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2):
+    def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2, dctx=None):
         import ctypes
         import numpy as np
         self.ctx, self.L_, self.errors, self.encs = ctx, L_, errors, encs
+        self.dctx = dctx if dctx is not None else ctx
+        self.pipelined = self.dctx is not ctx
         self.k, self.L, self.G, self.n = k, L, len(encs), k + 2
         self.W = (k + L + 255) // 256 * 256
         G, n, W = self.G, self.n, self.W
@@ -312,45 +325,80 @@ class RoundTripStep:
         self.earr = (ctypes.c_void_p * G)(*[e.value for e in encs])
         self.rows = [(ctypes.c_void_p * G)(*[dw + g * n * W for g in range(G)]) for dw in self.dW]
         self.counts = (ctypes.c_size_t * G)(*([n] * G))
-        self.ev = [ctx.event() for _ in range(4)]     # untimed steps
+        self.ev = [[ctx.event() for _ in range(4)] for _ in range(2)]  # untimed steps (by parity)
         self.pend = []                                 # timed steps' events, read after the steps
         self.spare = []
         self._t_enc, self.t_add, self._t_get, self._t_gpu_add, self.ok = [], [], [], [], True
         self.next_decs = None
         self.plans = None
+        self.ahead = None      # (step, events) of the encode a pipelined step queued for the next one
+        self.limit = None      # no encode is queued for a step >= limit (None: no limit)
+        self.encodes = 0       # encode launches so far, and at the start of the current phase
+        self.encodes_before_phase = 0
+
+    def begin_phase(self, limit=None):
+        """A new phase of steps 0, 1, ... (limit: its length, when known): an
+        encode queued ahead by the previous phase is dropped (its result is
+        never read; the barrier between the phases waits for it)."""
+        self.ahead, self.limit = None, limit
+        self.encodes_before_phase = self.encodes
+
+    def synchronize(self):
+        self.ctx.synchronize()
+        if self.pipelined:
+            self.dctx.synchronize()
 
     def _decoders(self):
         import ctypes
         decs = []
         for g in range(self.G):
             h = ctypes.c_void_p()
-            self.errors.check(self.L_.rlnc_decoder_create(self.ctx.handle, self.k, ctypes.byref(h)))
+            self.errors.check(self.L_.rlnc_decoder_create(self.dctx.handle, self.k, ctypes.byref(h)))
             decs.append(h)
         return decs
 
+    def _events(self, i, timed):
+        if not timed:
+            return self.ev[i & 1]
+        return self.spare.pop() if self.spare else [self.ctx.event() for _ in range(4)]
+
+    def _encode(self, i, e):
+        s_ = i % len(self.dW)
+        self.ctx.record(e[0])
+        self.errors.check(self.L_.rlnc_encoder_group_coded_pieces_device(self.earr, self.G, self.dV[s_], self.n,
+                                                                         self.dW[s_] + self.k, self.W))
+        self.ctx.record(e[1])
+        self.encodes += 1
+        if self.plans is None:   # the launches' kernel instances (first warmup step: tools/prof_roundtrip.py)
+            from kodr_amd._lib import last_launch_plan
+            self.plans = {"encode": last_launch_plan()}
+
     def step(self, i, timed=True):
         import ctypes
-        from kodr_amd import device as kdev
-        ctx, L_, errors, G, k, L = self.ctx, self.L_, self.errors, self.G, self.k, self.L
+        L_, errors, G, k, L = self.L_, self.errors, self.G, self.k, self.L
         s_ = i % len(self.dW)
         decs = self.next_decs if self.next_decs is not None else self._decoders()
         self.next_decs = None
         darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
-        e = self.ev if not timed else (self.spare.pop() if self.spare else [ctx.event() for _ in range(4)])
-        ctx.record(e[0])
-        errors.check(L_.rlnc_encoder_group_coded_pieces_device(self.earr, G, self.dV[s_], self.n, self.dW[s_] + k,
-                                                               self.W))
-        ctx.record(e[1])
-        if self.plans is None:   # the launches' kernel instances (first warmup step: tools/prof_driver.py)
-            from kodr_amd._lib import last_launch_plan
-            self.plans = {"encode": last_launch_plan()}
+        if self.ahead is not None and self.ahead[0] == i:
+            e = self.ahead[1]                  # queued by the previous step
+            self.ahead = None
+        else:
+            e = self._events(i, timed)
+            self._encode(i, e)
+        if self.pipelined:
+            self.dctx.wait(e[1])              # the decoders' stream reads the rows this encode wrote
         ta0 = time.perf_counter()
         cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
         errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[s_], self.counts, self.W, L, cons, sts))
         ta1 = time.perf_counter()
-        ctx.record(e[2])
+        self.dctx.record(e[2])
+        if self.pipelined and (self.limit is None or i + 1 < self.limit):
+            en = self._events(i + 1, timed)
+            self._encode(i + 1, en)            # beside this step's twin copy and GetPieces
+            self.ahead = (i + 1, en)
         errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
-        ctx.record(e[3])
+        self.dctx.record(e[3])
         if "get" not in self.plans:
             from kodr_amd._lib import last_launch_plan
             self.plans["get"] = last_launch_plan()
@@ -386,10 +434,51 @@ class RoundTripStep:
         self._collect()
         return self._t_gpu_add
 
+    def encode_alone(self, reps):
+        """The round trip's encode launch alone, `reps` back to back on the
+        encoders' stream (nothing beside it): HIP events, seconds per launch."""
+        from kodr_amd import device as kdev
+        self.synchronize()
+        e0, e1 = self.ctx.event(), self.ctx.event()
+        self.ctx.record(e0)
+        for i in range(reps):
+            s_ = i % len(self.dW)
+            self.errors.check(self.L_.rlnc_encoder_group_coded_pieces_device(self.earr, self.G, self.dV[s_], self.n,
+                                                                             self.dW[s_] + self.k, self.W))
+        self.ctx.record(e1)
+        return kdev.Context.elapsed_ms(e0, e1) / 1e3 / reps
+
+    def get_alone(self, reps):
+        """The round trip's grouped GetPieces alone: G fresh decoders fed set
+        0's rows (one batched AddPiece), then `reps` GetPieces calls back to
+        back on the decoders' stream: HIP events, seconds per call."""
+        import ctypes
+        from kodr_amd import device as kdev
+        self.synchronize()
+        G = self.G
+        decs = self.next_decs if self.next_decs is not None else self._decoders()
+        self.next_decs = None
+        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
+        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+        self.errors.check(self.L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[0], self.counts, self.W, self.L,
+                                                                cons, sts))
+        self.errors.check(self.L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, self.L))
+        self.dctx.synchronize()
+        e0, e1 = self.dctx.event(), self.dctx.event()
+        self.dctx.record(e0)
+        for _ in range(reps):
+            self.errors.check(self.L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, self.L))
+        self.dctx.record(e1)
+        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / reps
+        for x in decs:
+            self.L_.rlnc_decoder_destroy(x)
+        return t
+
     def decoded_ok(self, gens=None):
         """The last step's decoded generations against the resident ones."""
         import ctypes
         import numpy as np
+        self.synchronize()
         ok = self.ok
         pitch = ctypes.c_size_t()
         for g in (gens if gens is not None else sorted({0, self.G - 1})):
@@ -406,24 +495,31 @@ class RoundTripStep:
         return self.G * (self.n * setbytes(self.k, self.L) + self.k * (self.k + self.L))
 
     def close(self):
+        self.synchronize()
         for x in self.next_decs or []:
             self.L_.rlnc_decoder_destroy(x)
         self.next_decs = None
+        self.dctx.synchronize()
         for p_ in self.dV + self.dW + [self.dO]:
             self.ctx.free(p_)
 
 
-def run_timed(step, steps, warmup, barrier, warm_s, max_warm=20000):
+def run_timed(step, steps, warmup, barrier, warm_s, max_warm=20000, phase=None):
     """W untimed steps, never fewer than one and never less than warm_s of
     back-to-back work (the clock transient, DESIGN.md Roofline), a barrier,
-    then exactly `steps` timed steps bracketed by barriers.  Returns (wall
-    seconds of the timed steps on this rank, warmup steps run)."""
+    then exactly `steps` timed steps bracketed by barriers.  phase(limit), if
+    given, is called before each phase (RoundTripStep.begin_phase).  Returns
+    (wall seconds of the timed steps on this rank, warmup steps run)."""
     n_warm = 0
+    if phase:
+        phase(None)
     tw0 = time.perf_counter()
     while n_warm < max(warmup, 1) or (time.perf_counter() - tw0 < warm_s and n_warm < max_warm):
         step(n_warm, False)
         n_warm += 1
     barrier()
+    if phase:
+        phase(steps)
     t0 = time.perf_counter()
     for i in range(steps):
         step(i, True)
@@ -474,8 +570,11 @@ def roundtrip_kernels(rt, k, L):
                             "issue_frac": round(get_macs / tg / VALU_FLOOR_MACS_PER_S, 4),
                             "hbm_bytes": G * 2 * k * L, "plan": rt.plans["get"]},
         "issue_peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
+        "pipelined": rt.pipelined,
         "note": "issue_frac against the one bit-sliced VALU floor (ISSUE_PER_S x MACS_PER_INST_BS); kernel durations "
-                "of the same command under rocprofv3 in profiles/r05/"}
+                "of the same command under rocprofv3 in profiles/r06/.  Pipelined: the encode and GetPieces of "
+                "consecutive steps share the GPU, so these in-step event times include each other's share; the "
+                "kernel's own rate is roofline.achieved (the encode launch alone)"}
 
 
 def main():
@@ -491,6 +590,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--serial-roundtrip", action="store_true",
+                    help="encoders and decoders on one context (stream): no encode of step i + 1 beside step i's "
+                         "GetPieces (rounds 4-5 step)")
     ap.add_argument("--no-encode-decode", action="store_true",
                     help="skip the encode_decode round trip (PMC runs of the headline launch alone)")
     args = ap.parse_args()
@@ -550,10 +652,21 @@ def main():
     # (--no-encode-decode: the encode leg alone, for the PMC passes of tools/)
     ed = None
     if not args.no_encode_decode:
-        elim0 = ctx.elim_stats()
-        rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng)
-        t_rt, n_warm_rt = run_timed(rt.step, args.steps, args.warmup, barrier, WARM_S)
-        elim1 = ctx.elim_stats()
+        # the decoders on a context of their own (own stream): the pipelined
+        # round trip (RoundTripStep); --serial-roundtrip keeps every call on ctx
+        dctx = ctx if args.serial_roundtrip else kdev.Context(local)
+        elim0 = dctx.elim_stats()
+        rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng, dctx=dctx)
+
+        def rt_barrier():
+            rt.synchronize()
+            if world > 1:
+                dist.barrier()
+            rt.synchronize()
+
+        t_rt, n_warm_rt = run_timed(rt.step, args.steps, args.warmup, rt_barrier, WARM_S, phase=rt.begin_phase)
+        warm_encodes = rt.encodes_before_phase
+        elim1 = dctx.elim_stats()
         ed = roundtrip_block(t_rt, args.steps, args.warmup, n_warm_rt, rt.units(), world, kdist, device="cuda")
         ed["us_per_generation"] = round(ed["ms_per_step"] / G * 1e3, 2)
         ed["payload_MBps"] = round(world * args.steps * G * k * L / (ed["ms_per_step"] * args.steps / 1e3) / 1e6, 1)
@@ -561,11 +674,35 @@ def main():
         legs = roundtrip_kernels(rt, k, L)
         rt_ok = rt.decoded_ok()
         rt_n = rt.n
+        rt_pipelined = rt.pipelined
+        # the dominant kernel's own rate: the round trip's encode launch alone
+        # (in the pipelined step it shares the GPU with the previous step's
+        # GetPieces, so its in-step event time is not the kernel's)
+        t_enc_alone = rt.encode_alone(max(args.steps, 5))
+        t_get_alone = rt.get_alone(max(args.steps, 5))
+        legs["encode_launch"]["alone_us"] = round(t_enc_alone * 1e6, 2)
+        legs["get_pieces_call"]["alone_us"] = round(t_get_alone * 1e6, 2)
+        legs["get_pieces_call"]["alone_issue_frac"] = round(G * k * k * L / t_get_alone / VALU_FLOOR_MACS_PER_S, 4)
+        # the hardware anchor: VALU instructions per launch from the committed
+        # PMC pass of this command (tools/pmc_valu.py), against the SIMDs' VALU
+        # issue capacity at the nominal 2.4 GHz over the launch alone
+        pv = pmc_valu(G, k, L)
+        for leg, t_alone in (("encode_launch", t_enc_alone), ("get_pieces_call", t_get_alone)):
+            if pv and leg in pv:
+                q = pv[leg]
+                legs[leg]["valu"] = {
+                    "insts_per_launch": q["valu_insts_per_launch"],
+                    "busy_at_nominal_clock": round(q["valu_insts_per_launch"] * 2 / (1024 * 2.4e9 * t_alone), 4),
+                    "busy_at_measured_clock_pmc": q.get("valu_busy_at_measured_clock"),
+                    "clock_ghz_pmc": q.get("clock_ghz"),
+                    "source": pmc_valu_file(G, k, L)}
         # the elimination routes of every decoder of the warmup and timed steps
         # (rlnc_ctx_elim_stats): host_after_gpu counts the launches that left a
         # batch to kodr's algorithm on the host
         elim_routes = {key: elim1[key] - elim0[key] for key in elim0}
         rt.close()
+        if dctx is not ctx:
+            dctx.close()
 
     # W warmup steps, but never fewer than one pass over the G generations (no
     # generation is first touched inside the timed region) and never less than
@@ -629,7 +766,9 @@ def main():
                           "avg_launch_us": round(t_launch * 1e6, 3)}), flush=True)
     elif rank == 0:
         enc_macs = G * rt_n * k * L
-        te = legs["encode_launch"]["avg_us"] / 1e6
+        te = t_enc_alone
+        step_s = ed["ms_per_step"] / 1e3
+        gfbs_macs_step = enc_macs + G * k * k * L
         line = {
             "metric": "coded MB/s device-resident, Full-RLNC encode+decode, 32M/256 pieces @1/2/4/8 GPU",
             "value": ed["value"],
@@ -647,11 +786,15 @@ def main():
                                     f"configs[1] encode + configs[2] decode), device-resident: a step = {G} resident "
                                     f"generations x (k + 2 = {k + 2} coded pieces in one grouped encode launch, a "
                                     "fresh decoder each fed them in one batched AddPiece call (GPU elimination), one "
-                                    "grouped GetPieces); value in kodr units: (k + 2) x SetBytes (encoder bench) + "
-                                    "DecodableLen (decoder bench) per generation"),
+                                    "grouped GetPieces)"
+                                    + ("; pipelined: step i + 1's encode (encoders' stream) beside step i's twin "
+                                       "copy and GetPieces (decoders' stream)" if rt_pipelined else "")
+                                    + "; value in kodr units: (k + 2) x SetBytes (encoder bench) + DecodableLen "
+                                      "(decoder bench) per generation"),
                        "value_covers": "encode+decode",
                        "piece_count": k, "piece_size": L, "generations_per_step": G,
                        "coded_pieces_per_generation_per_step": k + 2, "resident_generations": G,
+                       "pipelined": rt_pipelined,
                        "parallelism": f"generation-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": float(f"{enc_macs / te:.4g}"),
                          "peak": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"), "unit": "GF-MAC/s",
@@ -659,20 +802,31 @@ def main():
                          "traffic": pmc_traffic(k + 2, k, L, G),
                          "traffic_source": pmc_traffic_file(k + 2, k, L, G),
                          "kernel": "gf_bs_kernel",
+                         "avg_launch_us": round(te * 1e6, 2),
+                         "launches_timed": max(args.steps, 5),
                          "legs": legs,
+                         "step_share": {"gf_bs_macs_per_step": gfbs_macs_step,
+                                        "gf_macs_per_s": float(f"{gfbs_macs_step / step_s:.4g}"),
+                                        "frac": round(gfbs_macs_step / step_s / VALU_FLOOR_MACS_PER_S, 4),
+                                        "note": "both gf_bs launches of a step (encode + GetPieces) over the whole "
+                                                "step time: the kernel's rate with every other leg counted against it"},
                          "hbm": {"achieved_GBps": round(legs["encode_launch"]["hbm_bytes"] / te / 1e9, 1),
-                                 "peak_GBps": HBM_PEAK_GBS, "frac": legs["encode_launch"]["hbm_frac"]},
+                                 "peak_GBps": HBM_PEAK_GBS,
+                                 "frac": round(legs["encode_launch"]["hbm_bytes"] / te / 1e9 / HBM_PEAK_GBS, 4)},
                          "note": "the round trip's dominant kernel is gf_bs_kernel (the grouped encode launch, k + 2 "
-                                 "pieces of 16 generations, and the grouped GetPieces, together ~89 % of a step): "
-                                 "258 GF MACs per generation byte read, so neither HBM (hbm.frac) nor MFMA (a "
+                                 "pieces of 16 generations, and the grouped GetPieces, together ~89 % of a step's GPU "
+                                 "time): 258 GF MACs per generation byte read, so neither HBM (hbm.frac) nor MFMA (a "
                                  "byte-field product) bounds it; SURVEY 8(d) prices decode against the VALU ceiling. "
-                                 "achieved/frac: the encode leg's GF MACs per second (HIP events around the launch) "
-                                 "against the bit-sliced method's VALU issue floor; legs: each leg's own fractions"},
+                                 "achieved/frac: the round trip's encode launch (same kernel instance and shape) "
+                                 "timed alone, launches_timed back to back on the encoders' stream with HIP events, "
+                                 "right after the timed steps, against the bit-sliced method's VALU issue floor; "
+                                 "legs: each leg's in-step event times"},
             "cpu_baseline": (cpu_baseline_roundtrip(cpu, cpu_dec) if cpu is not None and cpu_dec is not None
                              else None),
             "roundtrip": {"us_per_generation": ed["us_per_generation"], "payload_MBps": ed["payload_MBps"],
                           "warmup_steps_run": ed["warmup_steps_run"],
                           "units_per_step_per_rank": ed["units_per_step_per_rank"],
+                          "warmup_encodes_run": warm_encodes,
                           "roundtrip_ok": rt_ok, "elimination_routes": elim_routes},
             "encode": {
                 "value": round(value, 1), "unit": "MB/s", "ms_per_step": round(t_max / args.steps * 1e3, 5),
@@ -725,6 +879,20 @@ def kernel_name(plan):
 def pmc_traffic_file(B, k, L, G=1):
     name = f"pmc_traffic_B{B}_k{k}_L{L}.json" if G == 1 else f"pmc_traffic_G{G}_B{B}_k{k}_L{L}.json"
     return "profiles/" + name
+
+
+def pmc_valu_file(G, k, L):
+    return f"profiles/pmc_valu_G{G}_k{k}_L{L}.json"
+
+
+def pmc_valu(G, k, L):
+    """VALU instructions per launch of the round trip's two gf_bs_kernel legs
+    from the committed rocprofv3 --pmc summary (tools/pmc_valu.py)."""
+    path = os.path.join(ROOT, pmc_valu_file(G, k, L))
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
 
 
 def pmc_traffic(B, k, L, G=1):

@@ -102,6 +102,10 @@ int rlnc_host_unregister(rlnc_ctx* ctx, void* ptr);
 int rlnc_event_create(rlnc_ctx* ctx, void** ev);
 int rlnc_event_record(rlnc_ctx* ctx, void* ev);
 int rlnc_event_elapsed_ms(void* ev_start, void* ev_end, float* ms);   /* syncs ev_end */
+/* the context's stream waits (on the device, no host wait) for ev, recorded
+ * on any context's stream of the same device: e.g. decoders on one context
+ * fed the wire rows an encoder on another context produced */
+int rlnc_ctx_wait_event(rlnc_ctx* ctx, void* ev);
 int rlnc_event_destroy(void* ev);
 
 /* ---- piece splitting: data.go:103-166 (host only) ---------------------- */

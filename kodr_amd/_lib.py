@@ -43,6 +43,7 @@ SIGNATURES = {
     "rlnc_event_create": (_int, [_vp, _vpp]),
     "rlnc_event_record": (_int, [_vp, _vp]),
     "rlnc_event_elapsed_ms": (_int, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
+    "rlnc_ctx_wait_event": (_int, [_vp, _vp]),
     "rlnc_event_destroy": (_int, [_vp]),
     "rlnc_split_by_piece_count": (_int, [_sz, _sz, _szp, _szp]),
     "rlnc_split_by_piece_size": (_int, [_sz, _sz, _szp, _szp]),

@@ -111,6 +111,7 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
     (void)hipStreamDestroy(ctx->side);
     (void)hipEventDestroy(ctx->side_done);
     (void)hipEventDestroy(ctx->rows_ready);
+    if (ctx->elim_ready) (void)hipEventDestroy(ctx->elim_ready);
   }
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -120,6 +121,10 @@ int rlnc_ctx_destroy(rlnc_ctx* ctx) {
 int rlnc_ctx_synchronize(rlnc_ctx* ctx) {
   TRY(set_dev(ctx));
   HIPC(hipStreamSynchronize(ctx->stream));
+  // the aux stream's downloads of a batched AddPiece's coding vectors read the
+  // caller's rows and are never joined into ctx->stream: covered here, so a
+  // caller may reuse its rows once this returns (kodr_rlnc.h)
+  if (ctx->aux) HIPC(hipStreamSynchronize(ctx->aux));
   return RLNC_OK;
 }
 
@@ -212,6 +217,12 @@ int rlnc_event_create(rlnc_ctx* ctx, void** ev) {
 int rlnc_event_record(rlnc_ctx* ctx, void* ev) {
   TRY(set_dev(ctx));
   HIPC(hipEventRecord((hipEvent_t)ev, ctx->stream));
+  return RLNC_OK;
+}
+int rlnc_ctx_wait_event(rlnc_ctx* ctx, void* ev) {
+  if (!ev) return RLNC_ERR_INVALID_ARGUMENT;
+  TRY(set_dev(ctx));
+  HIPC(hipStreamWaitEvent(ctx->stream, (hipEvent_t)ev, 0));
   return RLNC_OK;
 }
 int rlnc_event_elapsed_ms(void* a, void* b, float* ms) {

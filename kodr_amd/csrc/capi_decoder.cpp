@@ -623,6 +623,7 @@ int ctx_side(rlnc_ctx* ctx) {
   HIPC(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
   HIPC(hipEventCreateWithFlags(&ctx->side_done, hipEventDisableTiming));
   HIPC(hipEventCreateWithFlags(&ctx->rows_ready, hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&ctx->elim_ready, hipEventDisableTiming));
   return RLNC_OK;
 }
 
@@ -642,8 +643,17 @@ int ctx_vec_pin(rlnc_ctx* ctx, size_t bytes) {
 
 // a stream for small reads of rows whose producers are ordered before
 // ctx->rows_ready, and that must not wait for the copies queued after it
+// (at the device's highest stream priority: a high-priority stream takes a
+// hardware queue of its own pool, so the download -- a blit kernel for a
+// strided D2H copy -- never queues behind a kernel of an application stream
+// that shares a normal-priority hardware queue with it; beyond
+// GPU_MAX_HW_QUEUES streams share those)
 int ctx_aux_after_rows(rlnc_ctx* ctx, hipStream_t* st) {
-  if (!ctx->aux) HIPC(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  if (!ctx->aux) {
+    int least = 0, greatest = 0;
+    HIPC(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPC(hipStreamCreateWithPriority(&ctx->aux, hipStreamNonBlocking, greatest));
+  }
   HIPC(hipStreamWaitEvent(ctx->aux, ctx->rows_ready, 0));
   *st = ctx->aux;
   return RLNC_OK;
@@ -739,19 +749,23 @@ int ctx_elim_pin(rlnc_ctx* ctx, size_t bytes) {
 // reported success (cnt[i] = k, att[i] = the attempt that succeeded) or any
 // reported failure (cnt[i] = 0: kodr's route on the host).  on_fail(i) runs
 // as soon as decoder i fails, while the launch may still run.
-// A decoder still unresolved kElimGiveUp after the launch was issued -- its
-// workgroups not resident, e.g. behind another kernel on the same GPU -- is
-// given up the same way: the launch finishes in the background on the
-// context stream, which every later use of its buffers and of the caller's
-// rows is ordered behind (device rows are read asynchronously on that
-// stream), and its late results are never read.
+// A decoder still unresolved kElimGiveUp after the launch became eligible to
+// run -- its workgroups not resident, e.g. behind another kernel on the same
+// GPU -- is given up the same way: the launch finishes in the background on
+// the context stream, which every later use of its buffers and of the
+// caller's rows is ordered behind (device rows are read asynchronously on
+// that stream), and its late results are never read.  "Eligible": `ready`,
+// recorded on the context stream right before the launch, has completed (the
+// work queued ahead of the launch on the same stream -- a large encode, the
+// previous step's GetPieces -- does not count against the launch).
 constexpr auto kElimGiveUp = std::chrono::milliseconds(5);
 int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int* cnt, int* att,
-                     const std::function<int(size_t)>& on_fail = nullptr) {
+                     const std::function<int(size_t)>& on_fail, hipEvent_t ready) {
   const int P = kodr_amd::gf_elim_mc_groups(a.k, (int)nc);
   const uint32_t na = (uint32_t)kodr_amd::gf_elim_mc_attempts();
   const volatile uint32_t* st = reinterpret_cast<const volatile uint32_t*>(ctx->elim_pin);
-  const auto t0 = std::chrono::steady_clock::now();
+  auto t0 = std::chrono::steady_clock::now();
+  bool started = ready == nullptr;  // the give-up clock runs from t0 once the launch is eligible
   std::vector<int8_t> res(nc, 0);  // 0 open, 1 done, -1 failed or given up
   std::vector<int> satt(nc, 0);
   size_t open = nc;
@@ -761,7 +775,16 @@ int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int*
       _mm_pause();
     } else {
       std::this_thread::yield();
-      late = std::chrono::steady_clock::now() - t0 > kElimGiveUp;
+      if (!started) {
+        const hipError_t q = hipEventQuery(ready);
+        if (q == hipSuccess) {
+          started = true;
+          t0 = std::chrono::steady_clock::now();
+        } else if (q != hipErrorNotReady) {
+          HIPC(q);
+        }
+      }
+      late = started && std::chrono::steady_clock::now() - t0 > kElimGiveUp;
     }
     for (size_t g = 0; g < nc; g++) {
       if (res[g]) continue;
@@ -999,6 +1022,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
       }
       if (!cont) a.out_dev = ctx->elim_tdev.p + c0 * k * k;
     }
+    // (the first launch starts right behind rows_ready; a later one behind the launch before it)
+    if (direct && c0 > 0) HIPC(hipEventRecord(ctx->elim_ready, ctx->stream));
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
     if (!copies_out) {
       prep_rows();
@@ -1084,7 +1109,8 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     };
     // (a launch error below leaves the futures to their destructors, which wait)
     if (direct) {
-      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host)));
+      TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), std::function<int(size_t)>(early_host),
+                           c0 == 0 ? ctx->rows_ready : ctx->elim_ready));
       tstates = ctx->elim_pin + hdr;
     } else if (tonly) {
       HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));
@@ -1265,13 +1291,17 @@ int dec_elim_queues_gpu(rlnc_decoder* const* ds, size_t G, F before_read) {
         a.out_gen_stride = k * k;
         a.counts = reinterpret_cast<int*>(ctx->elim_pin_dev);
       }
+      if (direct) {
+        TRY(ctx_side(ctx));
+        HIPC(hipEventRecord(ctx->elim_ready, ctx->stream));
+      }
       HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
       TRY(join());
       const bool tonly = kodr_amd::gf_elim_blocked(a, (int)nc);
       std::vector<int> cntv(nc), attv(nc, 0);
       const uint8_t* tstates = hostp + hdr;
       if (direct) {
-        TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data()));
+        TRY(elim_direct_wait(ctx, a, nc, cntv.data(), attv.data(), nullptr, ctx->elim_ready));
         tstates = ctx->elim_pin + hdr;
       } else {
         HIPC(ctx->stage.d2h(hostp, hdr, ctx->elim_out.p, hdr, hdr, 1, ctx->stream));

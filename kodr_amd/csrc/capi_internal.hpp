@@ -113,6 +113,7 @@ struct rlnc_ctx {
   hipStream_t side = nullptr;      // batched GPU AddPiece: row copies beside the elimination
   hipEvent_t side_done = nullptr;  // ... and the context stream's wait for them
   hipEvent_t rows_ready = nullptr; // ... the rows' producer work: the side copies and the aux reads wait on it
+  hipEvent_t elim_ready = nullptr; // recorded right before a direct elimination launch (its give-up clock)
   hipStream_t aux = nullptr;       // small downloads that must not queue behind the side copies
   // batched GPU AddPiece: the batch's coding vectors, downloaded beside every
   // elimination launch for the decoders it leaves to the host route

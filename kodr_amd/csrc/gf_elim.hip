@@ -750,6 +750,35 @@ constexpr int kMcLdsSpins = 1 << 17;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
+#ifdef KODR_MC_CHECK
+// Tuning build (round 6, the round-5 mc4 fault): every global access of mc2 /
+// mc4 is checked against the allocations the host sized for the launch
+// (gf_elim sets them before each launch); an access outside is printed and
+// skipped instead of issued.
+struct McBounds {
+  const uint8_t *pub, *out, *cnt, *odev, *tab;
+  uint64_t pub_bytes, out_bytes, cnt_bytes, odev_bytes, tab_bytes;
+};
+__device__ McBounds g_mcb;
+__device__ __forceinline__ bool mc_in(const void* p, size_t len, const uint8_t* base, uint64_t bytes) {
+  const uintptr_t a = (uintptr_t)p, b = (uintptr_t)base;
+  return base && a >= b && a + len <= b + bytes;
+}
+__device__ __noinline__ void mc_report(int site, const void* p) {
+  printf("KODR_MC_CHECK site %d block (%d,%d) thread %d addr %p pub %p+%lu out %p+%lu cnt %p+%lu odev %p+%lu\n",
+         site, (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x, p, g_mcb.pub, (unsigned long)g_mcb.pub_bytes,
+         g_mcb.out, (unsigned long)g_mcb.out_bytes, g_mcb.cnt, (unsigned long)g_mcb.cnt_bytes, g_mcb.odev,
+         (unsigned long)g_mcb.odev_bytes);
+}
+#define MC_CK(p, len, base, bytes, site)                                                          \
+  (mc_in((const void*)(uintptr_t)(p), (len), (base), (bytes)) ||                                  \
+   (mc_report((site), (const void*)(uintptr_t)(p)), false))
+#define MC_CK_PUB(p, site) MC_CK((p), 8, g_mcb.pub, g_mcb.pub_bytes, site)
+#else
+#define MC_CK(p, len, base, bytes, site) true
+#define MC_CK_PUB(p, site) true
+#endif
+
 // input row of row i < k in attempt att: (i + s) mod k, s = 0, k/2, k/4, 3k/4
 __device__ __forceinline__ int mc_rot(int att, int k) {
   return att == 0 ? 0 : att == 1 ? k / 2 : att == 2 ? k / 4 : (3 * k) / 4;
@@ -778,10 +807,12 @@ __device__ __forceinline__ void mc_set_fail(int* lfail, int why) {
 }
 
 __device__ __forceinline__ void mc_put(gu64* dst, uint32_t tag, uint32_t v) {
+  if (!MC_CK_PUB(dst, 1)) return;
   __hip_atomic_store(dst, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // FAIL for attempt `tag` (why 1) or an abort for every attempt (why 2)
 __device__ __forceinline__ void mc_put_fail(gu64* dst, uint32_t tag, uint32_t tlast, int why) {
+  if (!MC_CK_PUB(dst, 2)) return;
   const uint32_t t = why >= 2 ? tlast : tag;
   __hip_atomic_store(dst, ((unsigned long long)(t | kMcFail) << 32) | (why >= 2 ? kMcAbort : 0u), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -841,6 +872,15 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int cd) {
 // store where the row is 4-byte aligned and the dword lies below k (pinned
 // host memory takes whole coalesced writes), bytes otherwise
 __device__ __forceinline__ void mc_store_row(uint8_t* row, uint32_t v, int lane, int k) {
+#ifdef KODR_MC_CHECK
+  if (4 * lane < k) {
+    const int n = k - 4 * lane < 4 ? k - 4 * lane : 4;
+    if (!mc_in(row + 4 * lane, n, g_mcb.out, g_mcb.out_bytes) && !mc_in(row + 4 * lane, n, g_mcb.odev, g_mcb.odev_bytes)) {
+      mc_report(3, row + 4 * lane);
+      return;
+    }
+  }
+#endif
   if (((uintptr_t)row & 3) == 0 && 4 * lane + 3 < k) {
     *reinterpret_cast<uint32_t*>(row + 4 * lane) = v;
     return;
@@ -856,6 +896,7 @@ __device__ __forceinline__ uint32_t mc_load_row(const ElimArgs& args, int g, int
   const int k = args.k;
   if (gr >= k) return gr >> 2 == lane ? 1u << (8 * (gr & 3)) : 0u;
   const uint8_t* src = args.vecs[g] + (size_t)mc_src_row(gr, k, rot) * args.vpitch;
+  if (!MC_CK(src, k, args.vecs[g], (uint64_t)(args.n[g] - 1) * args.vpitch + k, 5)) return 0u;
   uint32_t v = 0;
 #pragma unroll
   for (int b = 0; b < 4; b++)
@@ -1400,7 +1441,9 @@ __device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t ta
     uint64_t x[N];
 #pragma unroll
     for (int i = 0; i < N; i++)  // every load in flight before the first wait
-      x[i] = __hip_atomic_load(src + (size_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x[i] = MC_CK_PUB(src + (size_t)i * stride, 6)
+                 ? __hip_atomic_load(src + (size_t)i * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : 0ull;
 #pragma unroll
     for (int i = 0; i < N; i++) {
       const int s = mc_tag_state(x[i], tag, tlast);
@@ -1416,6 +1459,24 @@ __device__ __forceinline__ int mc4_poll(const gu64* src, int stride, uint32_t ta
       if (const int lf = __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return lf;
     if (spins > kMcPollSpins) return 2;
     __builtin_amdgcn_s_sleep(1);
+#if defined(KODR_TUNE) && defined(KODR_MC_PROBE)
+    // tuning build (round 5's measurement, rebuilt for the fault check of
+    // round 6): not there yet -- wait on lane 0's first granule alone (one
+    // address for the wave) before the next full poll
+    if (__builtin_amdgcn_readfirstlane(mc_tag_state(x[0], tag, tlast)) < 0) {
+      const uint64_t pa = reinterpret_cast<uint64_t>(src);
+      const gu64* p0 = reinterpret_cast<const gu64*>(
+          ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) << 32) |
+          __builtin_amdgcn_readfirstlane((uint32_t)pa));
+      for (;; spins++) {
+        const uint64_t y =
+            MC_CK_PUB(p0, 11) ? __hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        if (__builtin_amdgcn_readfirstlane(mc_tag_state(y, tag, tlast)) >= 0 || spins > kMcPollSpins) break;
+        if (lfail && __hip_atomic_load(lfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+#endif
   }
 }
 
@@ -1505,7 +1566,12 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
   } while (0)
 #endif
   if (w == 0) MC4_STAMP(96);
-  const uint64_t ab = tid == 0 ? __hip_atomic_load(pubA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const uint64_t ab =
+      tid == 0 && MC_CK_PUB(pubA, 7) ? __hip_atomic_load(pubA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+#ifdef KODR_MC_CHECK
+  if (!mc_in(args.tables + kElimInvTables + 4 * (256 * 2 - 1), 16, g_mcb.tab, g_mcb.tab_bytes)) mc_report(8, args.tables);
+  if (!mc_in(&args.counts[g * (gridDim.x) + x], 4, g_mcb.cnt, g_mcb.cnt_bytes)) mc_report(10, &args.counts[g * gridDim.x + x]);
+#endif
   for (int i = tid; i < 256 * 2; i += kMc4Threads) {
     const uint32_t* a = args.tables + 4 * i;
     lds.tab[i] = make_uint4(a[0], a[1], a[2], a[3]);
@@ -1552,6 +1618,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
           auto orig = [&](int gr, int dw) -> uint32_t {
             if (gr >= k) return gr >> 2 == dw ? 1u << (8 * (gr & 3)) : 0u;
             const uint8_t* src = args.vecs[g] + (size_t)mc_src_row(gr, k, rot) * args.vpitch;
+            if (!MC_CK(src, k, args.vecs[g], (uint64_t)(args.n[g] - 1) * args.vpitch + k, 9)) return 0u;
             uint32_t o = 0;
 #pragma unroll
             for (int b = 0; b < 4; b++)
@@ -1892,11 +1959,46 @@ size_t gf_elim_mc_pub_bytes(int k, int G) {
 }
 int gf_elim_mc_attempts() { return kMcAttempts; }
 
+#ifdef KODR_MC_CHECK
+// the allocation that holds p (hipMemGetAddressRange), else [p, p + fallback)
+static void mc_alloc_range(const void* p, size_t fallback, const uint8_t** base, uint64_t* bytes) {
+  hipDeviceptr_t b = nullptr;
+  size_t n = 0;
+  if (p && hipMemGetAddressRange(&b, &n, (hipDeviceptr_t)p) == hipSuccess && b) {
+    *base = reinterpret_cast<const uint8_t*>(b);
+    *bytes = n;
+  } else {
+    (void)hipGetLastError();
+    *base = reinterpret_cast<const uint8_t*>(p);
+    *bytes = p ? fallback : 0;
+  }
+}
+#endif
+
 hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream) {
   if (G <= 0) return hipSuccess;
   if (G <= kElimMaxGens && args.k >= 2 && args.k <= 256 && gf_elim_mc_taken(args, G)) {
     const int m = mc_kernel_for(args.k, G);
     const dim3 grid(gf_elim_mc_groups(args.k, G), G);
+#ifdef KODR_MC_CHECK
+    {  // the launch's bounds: the hand-off layout the host sized, the real allocations of the rest
+      McBounds mb = {};
+      mb.pub = reinterpret_cast<const uint8_t*>(args.pub);
+      mb.pub_bytes = gf_elim_mc_pub_bytes(args.k, G);
+      const size_t k = (size_t)args.k;
+      mc_alloc_range(args.out, (size_t)G * k * k, &mb.out, &mb.out_bytes);
+      mc_alloc_range(args.counts, 4 * (size_t)kElimMcMaxBlocks, &mb.cnt, &mb.cnt_bytes);
+      mc_alloc_range(args.out_dev, (size_t)G * k * k, &mb.odev, &mb.odev_bytes);
+      mc_alloc_range(args.tables, kElimTableWords * 4, &mb.tab, &mb.tab_bytes);
+      fprintf(stderr, "KODR_MC_CHECK launch mc%d G %d grid %d x %d: pub %p+%lu out %p+%lu cnt %p+%lu odev %p+%lu\n", m,
+              G, (int)grid.x, (int)grid.y, (const void*)mb.pub, (unsigned long)mb.pub_bytes, (const void*)mb.out,
+              (unsigned long)mb.out_bytes, (const void*)mb.cnt, (unsigned long)mb.cnt_bytes, (const void*)mb.odev,
+              (unsigned long)mb.odev_bytes);
+      const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mcb), &mb, sizeof(mb), 0, hipMemcpyHostToDevice, stream);
+      if (e != hipSuccess) return e;
+      (void)hipStreamSynchronize(stream);  // (mb is on this stack frame)
+    }
+#endif
     if (m == 4) {
       if (!args.direct) return hipErrorInvalidValue;  // mc4 reports directly only
 #ifdef KODR_TUNE

@@ -103,10 +103,14 @@ class DevicePool {
   // there (a decoder's destroy while its stream still runs: no GPU packet
   // per buffer, no host wait; an event per buffer, or per decoder, sat as
   // marker packets between a round trip's GetPieces and the next encode)
+  // (pending bytes count against the cache cap: past it they are ordered and
+  // the oldest cached blocks released at once)
   void defer_free(uint8_t* p, size_t cap, hipStream_t stream) {
     if (!p) return;
     std::lock_guard<std::mutex> lk(mu_);
     pending_.push_back(Block{p, cap, stream, nullptr, nullptr});
+    pending_bytes_ += cap;
+    if (cached_ + pending_bytes_ > limit()) flush_pending();
   }
   // the stream is idle (the caller synchronised it) and about to go away:
   // its pending blocks are reusable at once
@@ -116,6 +120,7 @@ class DevicePool {
       if (it->stream == stream) {
         free_.push_front(Block{it->p, it->size, nullptr, nullptr, nullptr});
         cached_ += it->size;
+        pending_bytes_ -= it->size;
         it = pending_.erase(it);
       } else {
         ++it;
@@ -124,9 +129,10 @@ class DevicePool {
     while (cached_ > limit() && !free_.empty()) release_oldest();
   }
 
+  // idle cached blocks plus those still pending (defer_free)
   size_t cached() {
     std::lock_guard<std::mutex> lk(mu_);
-    return cached_;
+    return cached_ + pending_bytes_;
   }
 
  private:
@@ -180,6 +186,7 @@ class DevicePool {
         if (it->stream == st) {
           free_.push_front(Block{it->p, it->size, st, ok ? ev : nullptr, ref});
           cached_ += it->size;
+          pending_bytes_ -= it->size;
           it = pending_.erase(it);
         } else {
           ++it;
@@ -204,6 +211,7 @@ class DevicePool {
   std::list<Block> free_;  // most recently freed first
   std::list<Block> pending_;  // defer_free'd, not yet ordered by an event
   size_t cached_ = 0;
+  size_t pending_bytes_ = 0;  // bytes in pending_
 };
 
 }  // namespace kodr_amd

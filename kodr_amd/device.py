@@ -89,6 +89,10 @@ class Context:
     def record(self, ev):
         errors.check(lib().rlnc_event_record(self._h, ev))
 
+    def wait(self, ev):
+        """this context's stream waits (on the device) for ev, recorded on any context"""
+        errors.check(lib().rlnc_ctx_wait_event(self._h, ev))
+
     @staticmethod
     def elapsed_ms(a, b):
         ms = ctypes.c_float()

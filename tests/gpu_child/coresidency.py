@@ -42,7 +42,7 @@ def add(lib, hs, ds, k, pitch, L):
     return cons, sts
 
 
-def main():
+def run():
     lib = _lib.lib()
     ctx = device.Context(0)
     occ = occupier()
@@ -110,7 +110,12 @@ def main():
     for d in ds:
         ctx.free(d)
     occ.kodr_test_stream_destroy(s2)
-    print(json.dumps({"call_s": dt, "routes": routes, "ok": ok}), flush=True)
+    ctx.close()
+    return {"call_s": dt, "routes": routes, "ok": ok}
+
+
+def main():
+    print(json.dumps(run()), flush=True)
 
 
 if __name__ == "__main__":

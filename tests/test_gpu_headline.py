@@ -135,6 +135,42 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
         hs.close()
 
 
+def test_bench_roundtrip_pipelined_exact(gpu_ctx):
+    # The bench's pipelined round trip (the decoders on a context of their
+    # own; step i + 1's encode queued beside step i's GetPieces): a phase of
+    # three steps over both vector sets, every decoded generation equal to the
+    # original bytes after each step, no encode queued past the phase, every
+    # decoder on the GPU route.
+    import bench
+    from kodr_amd import device
+    L_ = _lib.lib()
+    hs = bench.HeadlineStep(gpu_ctx, L_, errors, 256, 131072, 32, 16, grouped=True,
+                            rng=np.random.default_rng(0x5EEE), nvec=2, keep_data=True)
+    dctx = device.Context(0)
+    rt = bench.RoundTripStep(gpu_ctx, L_, errors, hs.encs, 256, 131072, np.random.default_rng(0x7F), nsets=2,
+                             dctx=dctx)
+    r0 = dctx.elim_stats()
+    try:
+        assert rt.pipelined
+        rt.begin_phase(3)
+        for i in range(3):
+            rt.step(i, timed=True)
+            assert (rt.ahead is not None) == (i < 2)
+            rt.synchronize()
+            got = dctx.d2h(rt.dO, 16 * 256 * 131072).reshape(16, -1)
+            for g in range(16):
+                assert np.array_equal(got[g], hs.datas[g]), (i, g)
+            assert rt.ok and rt.decoded_ok(list(range(16)))
+        assert len(rt.t_enc) == len(rt.t_add) == len(rt.t_get) == 3
+        r1 = dctx.elim_stats()
+        d = {key: r1[key] - r0[key] for key in r0}
+        assert d["gpu"] == 48 and d["host_after_gpu"] == 0 and d["host"] == 0, d
+    finally:
+        rt.close()
+        hs.close()
+        dctx.close()
+
+
 # grouped bit-sliced launches that plan each KW instance of
 # gf_bs_kernel<KW, 0, true, 2> (gf_bs.hip plan_gemm_bs): (G, k, L, count) -> KW
 GROUPED_KW_SHAPES = [((2, 8, 4096, 40), 1), ((2, 16, 4096, 40), 2), ((2, 24, 4096, 17), 3),

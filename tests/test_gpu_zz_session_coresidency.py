@@ -1,0 +1,30 @@
+"""The co-residency scenario of tests/test_gpu_coresidency.py inside the
+pytest process itself (this file sorts last, so it runs after every other GPU
+test has created its contexts and streams).  Streams beyond
+GPU_MAX_HW_QUEUES (4 on the box) share hardware queues: in round 5 the
+give-up route's vector download ran on a normal-priority stream, landed on
+the occupier's queue inside the session and waited for it (57 ms,
+profiles/r05/coresidency/in_pytest_session.txt).  The download stream now
+has the device's highest priority (capi_decoder.cpp ctx_aux_after_rows)."""
+import importlib.util
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def test_elimination_beside_a_long_kernel_in_this_process():
+    """The same scenario in the pytest process (its streams share hardware queues with
+    every context the session created)."""
+    if not os.path.exists(os.path.join(HERE, "cpp", "libkodr_occupy.so")):
+        pytest.skip("test occupier not built (__graft_entry__.build)")
+    spec = importlib.util.spec_from_file_location("kodr_coresidency_child", os.path.join(HERE, "gpu_child",
+                                                                                           "coresidency.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    res = mod.run()
+    print(f"call {res['call_s'] * 1e3:.2f} ms; routes {res['routes']}")
+    assert all(res["ok"]), res
+    assert res["call_s"] <= 0.010, res

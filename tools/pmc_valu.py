@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""VALU instructions, wave count and clock per launch of the round trip's two
+gf_bs_kernel legs (the encode launch and the grouped GetPieces) from one
+rocprofv3 --pmc pass of the driver's bench command (SQ_INSTS_VALU
+SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT; no tracing domains), and
+the hardware VALU-busy fraction each implies:
+
+  SIMD-cycles of a launch  = 1,024 SIMDs x GRBM_GUI_ACTIVE / 8
+                             (GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles,
+                             MI355X_MICROARCH.md "DVFS give-back")
+  VALU-busy                = SQ_INSTS_VALU x 2 / SIMD-cycles
+                             (a wave64 VALU instruction holds a SIMD-32 for 2
+                             cycles, MI355X_MICROARCH.md wave scheduling)
+  VALU-busy at 2.4 GHz     = SQ_INSTS_VALU x 2 / (1,024 x 2.4e9 x duration)
+
+The launches are those whose grid is the kernel instance the bench line
+(same run) records in roofline.legs.*.plan.  Writes the JSON that bench.py
+reads (profiles/pmc_valu_G{G}_k{k}_L{L}.json) to stdout.
+
+  python tools/pmc_valu.py <pmc dir> <bench.json>"""
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+SIMDS, NOMINAL_HZ = 1024, 2.4e9
+
+d, bj = sys.argv[1], sys.argv[2]
+line = json.loads([x for x in open(bj) if x.startswith("{")][-1])
+legs = line["roofline"]["legs"]
+G, k, L = line["config"]["generations_per_step"], line["config"]["piece_count"], line["config"]["piece_size"]
+
+per = collections.defaultdict(dict)
+for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "gf_bs_kernel" not in r["Kernel_Name"]:
+            continue
+        key = (r["Dispatch_Id"], int(r["Grid_Size"]))
+        per[key][r["Counter_Name"]] = float(r["Counter_Value"])
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            per[key]["us"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+
+out = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT of "
+                 "bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline (tools/gpu_r6_val.sh)",
+       "simds": SIMDS, "cycles_per_wave64_valu": 2, "nominal_clock_hz": NOMINAL_HZ}
+for leg, macs in (("encode_launch", G * (k + 2) * k * L), ("get_pieces_call", G * k * k * L)):
+    plan = legs[leg]["plan"]
+    grid = plan["workgroups"] * 64 * plan["waves"] * plan["generations"]
+    vs = [v for (disp, g), v in per.items() if g == grid and "SQ_INSTS_VALU" in v]
+    if not vs:
+        continue
+    med = {c: statistics.median(v[c] for v in vs if c in v)
+           for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "GRBM_COUNT", "us")
+           if any(c in v for v in vs)}
+    e = {"plan": plan, "counter_grid_threads": grid, "launches": len(vs),
+         "valu_insts_per_launch": int(med["SQ_INSTS_VALU"]), "salu_insts_per_launch": int(med.get("SQ_INSTS_SALU", 0)),
+         "waves_per_launch": int(med.get("SQ_WAVES", 0)), "gf_macs_per_launch": macs,
+         "gf_macs_per_valu_inst": round(macs / med["SQ_INSTS_VALU"], 2)}
+    if "GRBM_GUI_ACTIVE" in med:
+        simd_cycles = SIMDS * med["GRBM_GUI_ACTIVE"] / 8
+        e["grbm_gui_active_per_launch"] = int(med["GRBM_GUI_ACTIVE"])
+        e["valu_busy_at_measured_clock"] = round(med["SQ_INSTS_VALU"] * 2 / simd_cycles, 4)
+        if "us" in med:
+            e["pmc_launch_us"] = round(med["us"], 2)
+            e["clock_ghz"] = round(med["GRBM_GUI_ACTIVE"] / 8 / (med["us"] * 1e3), 3)
+            e["valu_busy_at_nominal_clock"] = round(med["SQ_INSTS_VALU"] * 2 / (SIMDS * NOMINAL_HZ * med["us"] * 1e-6), 4)
+    out[leg] = e
+print(json.dumps(out, indent=1))

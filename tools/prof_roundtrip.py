@@ -58,11 +58,13 @@ def main():
                       % (steps, line["warmup"]),
            "bench_value": line["value"], "bench_ms_per_step": line["ms_per_step"], "legs": {}}
 
-    def leg(name, sel, events_us, macs=None, hbm=None):
-        if len(sel) < n_warm + steps:
-            out["legs"][name] = {"error": f"{len(sel)} launches, expected {n_warm + steps}"}
+    def leg(name, sel, events_us, macs=None, hbm=None, first=None, count=None):
+        first = n_warm if first is None else first
+        count = steps if count is None else count
+        if len(sel) < first + count:
+            out["legs"][name] = {"error": f"{len(sel)} launches, expected {first + count}"}
             return None
-        timed = [r[4] for r in sel[n_warm:n_warm + steps]]
+        timed = [r[4] for r in sel[first:first + count]]
         avg = statistics.mean(timed)
         e = {"kernel": sel[0][1].replace("(anonymous namespace)::", "").split("(")[0][-100:],
              "grid": [sel[0][2], sel[0][3]], "timed_launches": len(timed), "rocprof_avg_us": round(avg, 2),
@@ -75,19 +77,29 @@ def main():
         if hbm is not None:
             e["hbm_frac_from_rocprof"] = round(hbm / avg / 1e3 / bench.HBM_PEAK_GBS, 4)
         out["legs"][name] = e
-        return sel[n_warm + steps - 1][0]
+        return sel[first + count - 1][0]
 
-    leg("roundtrip_encode", of_plan(rows, legs["encode_launch"]["plan"]), legs["encode_launch"]["avg_us"],
-        macs=G * n * k * L)
-    leg("roundtrip_get_pieces", of_plan(rows, legs["get_pieces_call"]["plan"]), legs["get_pieces_call"]["avg_us"],
-        macs=G * k * k * L)
+    # the round trip's encodes: warmup (a pipelined warmup queues one more
+    # than its steps), the timed steps, then bench's encode_alone launches
+    wenc = rt.get("warmup_encodes_run", n_warm)
+    reps = line["roofline"].get("launches_timed", 0)
+    enc_sel = of_plan(rows, legs["encode_launch"]["plan"])
+    get_sel = of_plan(rows, legs["get_pieces_call"]["plan"])
+    leg("roundtrip_encode", enc_sel, legs["encode_launch"]["avg_us"], macs=G * n * k * L, first=wenc)
+    leg("roundtrip_get_pieces", get_sel, legs["get_pieces_call"]["avg_us"], macs=G * k * k * L)
+    if reps:
+        leg("encode_alone", enc_sel, legs["encode_launch"].get("alone_us"), macs=G * n * k * L, first=wenc + steps,
+            count=reps)
+        # (get_alone: one untimed GetPieces after its AddPiece, then the timed ones)
+        leg("get_pieces_alone", get_sel, legs["get_pieces_call"].get("alone_us"), macs=G * k * k * L,
+            first=n_warm + steps + 1, count=reps)
     elim = [r for r in rows if "gf_elim_mc" in r[1] and r[3] == G]
     leg("roundtrip_elimination", elim, None, macs=G * k ** 3)
     twin = [r for r in rows if "copy_bitslice" in r[1]]
     leg("roundtrip_rows_twin", twin, None, hbm=G * 2 * n * L)
     # the encode leg (bench.py's second timed phase): its own warmup count
     enc = line["encode"]["roofline"]
-    last_rt = max((r[0] for r in of_plan(rows, legs["encode_launch"]["plan"])[:n_warm + steps]), default=0)
+    last_rt = max((r[0] for r in enc_sel[:wenc + steps + reps]), default=0)
     sel = of_plan(rows, enc["plan"], after=last_rt)
     w = enc["warmup_launches"]
     if len(sel) >= w + steps:
@@ -101,7 +113,7 @@ def main():
     else:
         out["legs"]["encode_B32"] = {"error": f"{len(sel)} launches, expected {w + steps}"}
     out["roofline_frac_bench"] = line["roofline"]["frac"]
-    rte = out["legs"].get("roundtrip_encode", {})
+    rte = out["legs"].get("encode_alone" if reps else "roundtrip_encode", {})
     if "rocprof_avg_us" in rte:
         out["roofline_frac_from_rocprof"] = rte["issue_frac_from_rocprof"]
     with open(a.out, "w") if a.out else sys.stdout as f:
