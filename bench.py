@@ -301,12 +301,17 @@ class RoundTripStep:
     the next one's; the first warmup step its own); kodr's decoder bench
     builds its decoder outside the timer (benches/full/decoder_test.go:71-94)."""
 
-    def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2, dctx=None):
+    def __init__(self, ctx, L_, errors, encs, k, L, rng, nsets=2, dctx=None, overlap="elim"):
         import ctypes
         import numpy as np
         self.ctx, self.L_, self.errors, self.encs = ctx, L_, errors, encs
         self.dctx = dctx if dctx is not None else ctx
         self.pipelined = self.dctx is not ctx
+        # what step i + 1's encode runs beside: "elim" -- step i's elimination
+        # (queued from inside the AddPiece call right after its launch) and
+        # twin copy; "copy" -- the twin copy only (queued after the call); both
+        # make GetPieces wait for it; "get" -- the copy and GetPieces
+        self.overlap = overlap
         self.k, self.L, self.G, self.n = k, L, len(encs), k + 2
         self.W = (k + L + 255) // 256 * 256
         G, n, W = self.G, self.n, self.W
@@ -388,15 +393,34 @@ class RoundTripStep:
             self._encode(i, e)
         if self.pipelined:
             self.dctx.wait(e[1])              # the decoders' stream reads the rows this encode wrote
+        ahead = self.pipelined and (self.limit is None or i + 1 < self.limit)
         ta0 = time.perf_counter()
         cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
-        errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[s_], self.counts, self.W, L, cons, sts))
+        if ahead and self.overlap in ("elim", "elim_only"):
+            # step i + 1's encode queued from inside the AddPiece call, right
+            # after the elimination's launch: it runs beside the elimination
+            # (on the CUs its workgroups leave free) and the twin copy
+            # ("elim_only": the copy waits for the encode -- the hook returns
+            # its end event)
+            en = self._events(i + 1, timed)
+
+            def _hook(_u, en=en):
+                self._encode(i + 1, en)
+                return en[1].value if self.overlap == "elim_only" else None
+            hook = _lib_hook(_hook)
+            errors.check(L_.rlnc_decoders_add_pieces_gpu_hook(darr, G, self.rows[s_], self.counts, self.W, L, cons,
+                                                              sts, hook, None))
+        else:
+            errors.check(L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[s_], self.counts, self.W, L, cons, sts))
         ta1 = time.perf_counter()
         self.dctx.record(e[2])
-        if self.pipelined and (self.limit is None or i + 1 < self.limit):
-            en = self._events(i + 1, timed)
-            self._encode(i + 1, en)            # beside this step's twin copy and GetPieces
+        if ahead:
+            if self.overlap not in ("elim", "elim_only"):
+                en = self._events(i + 1, timed)
+                self._encode(i + 1, en)        # beside this step's twin copy (and GetPieces)
             self.ahead = (i + 1, en)
+            if self.overlap in ("copy", "elim", "elim_only"):
+                self.dctx.wait(en[1])          # GetPieces after it: two bit-sliced launches side by side lose
         errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
         self.dctx.record(e[3])
         if "get" not in self.plans:
@@ -434,46 +458,6 @@ class RoundTripStep:
         self._collect()
         return self._t_gpu_add
 
-    def encode_alone(self, reps):
-        """The round trip's encode launch alone, `reps` back to back on the
-        encoders' stream (nothing beside it): HIP events, seconds per launch."""
-        from kodr_amd import device as kdev
-        self.synchronize()
-        e0, e1 = self.ctx.event(), self.ctx.event()
-        self.ctx.record(e0)
-        for i in range(reps):
-            s_ = i % len(self.dW)
-            self.errors.check(self.L_.rlnc_encoder_group_coded_pieces_device(self.earr, self.G, self.dV[s_], self.n,
-                                                                             self.dW[s_] + self.k, self.W))
-        self.ctx.record(e1)
-        return kdev.Context.elapsed_ms(e0, e1) / 1e3 / reps
-
-    def get_alone(self, reps):
-        """The round trip's grouped GetPieces alone: G fresh decoders fed set
-        0's rows (one batched AddPiece), then `reps` GetPieces calls back to
-        back on the decoders' stream: HIP events, seconds per call."""
-        import ctypes
-        from kodr_amd import device as kdev
-        self.synchronize()
-        G = self.G
-        decs = self.next_decs if self.next_decs is not None else self._decoders()
-        self.next_decs = None
-        darr = (ctypes.c_void_p * G)(*[x.value for x in decs])
-        cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
-        self.errors.check(self.L_.rlnc_decoders_add_pieces_gpu(darr, G, self.rows[0], self.counts, self.W, self.L,
-                                                                cons, sts))
-        self.errors.check(self.L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, self.L))
-        self.dctx.synchronize()
-        e0, e1 = self.dctx.event(), self.dctx.event()
-        self.dctx.record(e0)
-        for _ in range(reps):
-            self.errors.check(self.L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, self.L))
-        self.dctx.record(e1)
-        t = kdev.Context.elapsed_ms(e0, e1) / 1e3 / reps
-        for x in decs:
-            self.L_.rlnc_decoder_destroy(x)
-        return t
-
     def decoded_ok(self, gens=None):
         """The last step's decoded generations against the resident ones."""
         import ctypes
@@ -502,6 +486,11 @@ class RoundTripStep:
         self.dctx.synchronize()
         for p_ in self.dV + self.dW + [self.dO]:
             self.ctx.free(p_)
+
+
+def _lib_hook(fn):
+    from kodr_amd._lib import HOOK_FN
+    return HOOK_FN(fn)
 
 
 def run_timed(step, steps, warmup, barrier, warm_s, max_warm=20000, phase=None):
@@ -570,11 +559,8 @@ def roundtrip_kernels(rt, k, L):
                             "issue_frac": round(get_macs / tg / VALU_FLOOR_MACS_PER_S, 4),
                             "hbm_bytes": G * 2 * k * L, "plan": rt.plans["get"]},
         "issue_peak_gf_macs_per_s": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"),
-        "pipelined": rt.pipelined,
         "note": "issue_frac against the one bit-sliced VALU floor (ISSUE_PER_S x MACS_PER_INST_BS); kernel durations "
-                "of the same command under rocprofv3 in profiles/r06/.  Pipelined: the encode and GetPieces of "
-                "consecutive steps share the GPU, so these in-step event times include each other's share; the "
-                "kernel's own rate is roofline.achieved (the encode launch alone)"}
+                "of the same command under rocprofv3 in profiles/r06/"}
 
 
 def main():
@@ -590,6 +576,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
+    ap.add_argument("--overlap", choices=("elim", "elim_only", "copy", "get"), default="elim",
+                    help="pipelined round trip: what step i + 1's encode runs beside (RoundTripStep)")
     ap.add_argument("--serial-roundtrip", action="store_true",
                     help="encoders and decoders on one context (stream): no encode of step i + 1 beside step i's "
                          "GetPieces (rounds 4-5 step)")
@@ -656,7 +644,7 @@ def main():
         # round trip (RoundTripStep); --serial-roundtrip keeps every call on ctx
         dctx = ctx if args.serial_roundtrip else kdev.Context(local)
         elim0 = dctx.elim_stats()
-        rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng, dctx=dctx)
+        rt = RoundTripStep(ctx, L_, errors, encs, k, L, rng, dctx=dctx, overlap=args.overlap)
 
         def rt_barrier():
             rt.synchronize()
@@ -671,31 +659,11 @@ def main():
         ed["us_per_generation"] = round(ed["ms_per_step"] / G * 1e3, 2)
         ed["payload_MBps"] = round(world * args.steps * G * k * L / (ed["ms_per_step"] * args.steps / 1e3) / 1e6, 1)
         ed["wall_s"] = round(t_rt, 4)
-        legs = roundtrip_kernels(rt, k, L)
+        legs_in_step = roundtrip_kernels(rt, k, L)
         rt_ok = rt.decoded_ok()
         rt_n = rt.n
         rt_pipelined = rt.pipelined
-        # the dominant kernel's own rate: the round trip's encode launch alone
-        # (in the pipelined step it shares the GPU with the previous step's
-        # GetPieces, so its in-step event time is not the kernel's)
-        t_enc_alone = rt.encode_alone(max(args.steps, 5))
-        t_get_alone = rt.get_alone(max(args.steps, 5))
-        legs["encode_launch"]["alone_us"] = round(t_enc_alone * 1e6, 2)
-        legs["get_pieces_call"]["alone_us"] = round(t_get_alone * 1e6, 2)
-        legs["get_pieces_call"]["alone_issue_frac"] = round(G * k * k * L / t_get_alone / VALU_FLOOR_MACS_PER_S, 4)
-        # the hardware anchor: VALU instructions per launch from the committed
-        # PMC pass of this command (tools/pmc_valu.py), against the SIMDs' VALU
-        # issue capacity at the nominal 2.4 GHz over the launch alone
-        pv = pmc_valu(G, k, L)
-        for leg, t_alone in (("encode_launch", t_enc_alone), ("get_pieces_call", t_get_alone)):
-            if pv and leg in pv:
-                q = pv[leg]
-                legs[leg]["valu"] = {
-                    "insts_per_launch": q["valu_insts_per_launch"],
-                    "busy_at_nominal_clock": round(q["valu_insts_per_launch"] * 2 / (1024 * 2.4e9 * t_alone), 4),
-                    "busy_at_measured_clock_pmc": q.get("valu_busy_at_measured_clock"),
-                    "clock_ghz_pmc": q.get("clock_ghz"),
-                    "source": pmc_valu_file(G, k, L)}
+        rt_overlap = rt.overlap if rt.pipelined else None
         # the elimination routes of every decoder of the warmup and timed steps
         # (rlnc_ctx_elim_stats): host_after_gpu counts the launches that left a
         # batch to kodr's algorithm on the host
@@ -703,6 +671,35 @@ def main():
         rt.close()
         if dctx is not ctx:
             dctx.close()
+        # The legs: in the pipelined step the encode shares the GPU with the
+        # elimination and the twin copy, so its event time is not the kernel's.
+        # The same round trip run in series right after (rounds 4-5's step,
+        # every call on ctx; one untimed step, the GPU being warm) times each
+        # leg alone in the step as it occurs; the roofline prices that encode.
+        n_warm_serial = 0
+        if rt_pipelined:
+            rs = RoundTripStep(ctx, L_, errors, encs, k, L, rng)
+            _, n_warm_serial = run_timed(rs.step, args.steps, 1, barrier, 0.0, phase=rs.begin_phase)
+            legs = roundtrip_kernels(rs, k, L)
+            rs.close()
+            legs["pipelined_in_step"] = {key: {"avg_us": v["avg_us"]} for key, v in legs_in_step.items()
+                                         if isinstance(v, dict) and "avg_us" in v}
+        else:
+            legs = legs_in_step
+        legs["serial_warmup_steps"] = n_warm_serial
+        # the hardware anchor: VALU instructions per launch from the committed
+        # PMC pass of this command (tools/pmc_valu.py) over the SIMDs' VALU
+        # issue capacity at the nominal 2.4 GHz during the leg's launch
+        pv = pmc_valu(G, k, L)
+        for leg in ("encode_launch", "get_pieces_call"):
+            if pv and leg in pv:
+                q, t_leg = pv[leg], legs[leg]["avg_us"] * 1e-6
+                legs[leg]["valu"] = {
+                    "insts_per_launch": q["valu_insts_per_launch"],
+                    "busy_at_nominal_clock": round(q["valu_insts_per_launch"] * 2 / (1024 * 2.4e9 * t_leg), 4),
+                    "busy_at_measured_clock_pmc": q.get("valu_busy_at_measured_clock"),
+                    "clock_ghz_pmc": q.get("clock_ghz"),
+                    "source": pmc_valu_file(G, k, L)}
 
     # W warmup steps, but never fewer than one pass over the G generations (no
     # generation is first touched inside the timed region) and never less than
@@ -766,7 +763,7 @@ def main():
                           "avg_launch_us": round(t_launch * 1e6, 3)}), flush=True)
     elif rank == 0:
         enc_macs = G * rt_n * k * L
-        te = t_enc_alone
+        te = legs["encode_launch"]["avg_us"] / 1e6
         step_s = ed["ms_per_step"] / 1e3
         gfbs_macs_step = enc_macs + G * k * k * L
         line = {
@@ -787,14 +784,15 @@ def main():
                                     f"generations x (k + 2 = {k + 2} coded pieces in one grouped encode launch, a "
                                     "fresh decoder each fed them in one batched AddPiece call (GPU elimination), one "
                                     "grouped GetPieces)"
-                                    + ("; pipelined: step i + 1's encode (encoders' stream) beside step i's twin "
-                                       "copy and GetPieces (decoders' stream)" if rt_pipelined else "")
+                                    + (f"; pipelined (overlap {rt_overlap}): step i + 1's encode (encoders' stream) "
+                                       "queued beside step i's elimination and twin copy (decoders' stream)"
+                                       if rt_pipelined else "")
                                     + "; value in kodr units: (k + 2) x SetBytes (encoder bench) + DecodableLen "
                                       "(decoder bench) per generation"),
                        "value_covers": "encode+decode",
                        "piece_count": k, "piece_size": L, "generations_per_step": G,
                        "coded_pieces_per_generation_per_step": k + 2, "resident_generations": G,
-                       "pipelined": rt_pipelined,
+                       "pipelined": rt_pipelined, "overlap": rt_overlap,
                        "parallelism": f"generation-sharded x{world}"},
             "roofline": {"bound": "valu", "achieved": float(f"{enc_macs / te:.4g}"),
                          "peak": float(f"{VALU_FLOOR_MACS_PER_S:.4g}"), "unit": "GF-MAC/s",
@@ -803,7 +801,6 @@ def main():
                          "traffic_source": pmc_traffic_file(k + 2, k, L, G),
                          "kernel": "gf_bs_kernel",
                          "avg_launch_us": round(te * 1e6, 2),
-                         "launches_timed": max(args.steps, 5),
                          "legs": legs,
                          "step_share": {"gf_bs_macs_per_step": gfbs_macs_step,
                                         "gf_macs_per_s": float(f"{gfbs_macs_step / step_s:.4g}"),
@@ -817,10 +814,11 @@ def main():
                                  "pieces of 16 generations, and the grouped GetPieces, together ~89 % of a step's GPU "
                                  "time): 258 GF MACs per generation byte read, so neither HBM (hbm.frac) nor MFMA (a "
                                  "byte-field product) bounds it; SURVEY 8(d) prices decode against the VALU ceiling. "
-                                 "achieved/frac: the round trip's encode launch (same kernel instance and shape) "
-                                 "timed alone, launches_timed back to back on the encoders' stream with HIP events, "
-                                 "right after the timed steps, against the bit-sliced method's VALU issue floor; "
-                                 "legs: each leg's in-step event times"},
+                                 "achieved/frac: the round trip's encode launch (HIP events around it) in the same "
+                                 "round trip run in series right after the timed (pipelined) steps, against the "
+                                 "bit-sliced method's VALU issue floor; legs: every leg of that serial run, "
+                                 "legs.pipelined_in_step: the timed steps' in-step event times; legs.*.valu: the "
+                                 "hardware VALU-busy anchor from the committed PMC pass"},
             "cpu_baseline": (cpu_baseline_roundtrip(cpu, cpu_dec) if cpu is not None and cpu_dec is not None
                              else None),
             "roundtrip": {"us_per_generation": ed["us_per_generation"], "payload_MBps": ed["payload_MBps"],

@@ -325,6 +325,20 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
                                  const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                  int* status);
+/* The same, calling after_launch(user) once from inside the call right after
+ * the first elimination launch is on its way (or, when no batch goes to the
+ * GPU, before returning), while the call still waits for the result: a
+ * caller queues its own independent work on another context's stream there
+ * (e.g. the next batch's encode), so that it runs beside the elimination on
+ * the CUs the elimination's workgroups leave free -- queued before, it could
+ * hold the CUs those workgroups need to be resident together.  The hook may
+ * return a hipEvent_t (or NULL): the rest of the call's work on this
+ * context's stream (the received rows' copies) is then ordered behind it.
+ * The hook must not call into this context. */
+typedef void* (*rlnc_hook_fn)(void* user);
+int rlnc_decoders_add_pieces_gpu_hook(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
+                                      const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
+                                      int* status, rlnc_hook_fn after_launch, void* user);
 /* The pending AddPiece calls of G decoders (one context, one piece_count),
  * eliminated together: one AddPiece call per piece only queues the coding
  * vector while the queue cannot complete the rank (lazy AddPiece), and a

@@ -9,6 +9,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+# rlnc_hook_fn (rlnc_decoders_add_pieces_gpu_hook): keep the wrapped object alive for the call
+HOOK_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p)
 LIB_PATH = os.environ.get("KODR_RLNC_LIB", os.path.join(_HERE, "libkodr_rlnc.so"))
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -90,6 +92,7 @@ SIGNATURES = {
     "rlnc_decoder_get_decoded": (_int, [_vp, _sz, _vp, _int]),
     "rlnc_decoder_bind_output": (_int, [_vp, _vp, _sz]),
     "rlnc_decoders_add_pieces_gpu": (_int, [_vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp]),
+    "rlnc_decoders_add_pieces_gpu_hook": (_int, [_vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp, _vp]),
     "rlnc_decoders_flush_gpu": (_int, [_vp, _sz]),
     "rlnc_decoders_get_pieces_device": (_int, [_vp, _sz, _vp, _sz]),
     "rlnc_recoder_group_coded_pieces_device": (_int, [_vpp, _sz, _vp, _sz, _vp, _sz]),

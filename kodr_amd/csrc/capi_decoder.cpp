@@ -822,7 +822,23 @@ int elim_direct_wait(rlnc_ctx* ctx, const kodr_amd::ElimArgs& a, size_t nc, int*
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_t* const* rows,
                                  const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                  int* status) {
+  return rlnc_decoders_add_pieces_gpu_hook(ds, G, rows, counts, pitch, piece_len, consumed, status, nullptr,
+                                           nullptr);
+}
+
+int rlnc_decoders_add_pieces_gpu_hook(rlnc_decoder* const* ds, size_t G, const uint8_t* const* rows,
+                                      const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
+                                      int* status, rlnc_hook_fn after_launch, void* user) {
   if (!ds || !rows || !counts || !consumed || !status || !G) return RLNC_ERR_INVALID_ARGUMENT;
+  // the caller's hook, once: right after the first elimination launch, else on the way out
+  bool hooked = after_launch == nullptr;
+  hipEvent_t hook_ev = nullptr;  // what the hook asked this call's later work to wait for
+  auto run_hook = [&] {
+    if (hooked) return;
+    hooked = true;
+    hook_ev = static_cast<hipEvent_t>(after_launch(user));
+  };
+  auto hook_guard = on_scope_exit([&] { run_hook(); });
   rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
   if (!ctx) return RLNC_ERR_NO_DEVICE;
   const size_t k = ds[0]->core.piece_count();
@@ -1025,6 +1041,11 @@ int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* ds, size_t G, const uint8_
     // (the first launch starts right behind rows_ready; a later one behind the launch before it)
     if (direct && c0 > 0) HIPC(hipEventRecord(ctx->elim_ready, ctx->stream));
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
+    run_hook();
+    if (hook_ev) {
+      HIPC(hipStreamWaitEvent(ctx->stream, hook_ev, 0));  // the copies (context stream) after the caller's work
+      hook_ev = nullptr;
+    }
     if (!copies_out) {
       prep_rows();
       TRY(launch_copies());

@@ -135,7 +135,10 @@ hipError_t gf_elim(const ElimArgs& args, int G, hipStream_t stream);
 // Instead of counts[g] it writes one status word per workgroup,
 // counts[g * groups + q] = 1 (done) or 0 (a singular block or a timeout: the
 // host then takes kodr's route); the decoder's T is valid when all are 1.
-constexpr int kElimMcMaxBlocks = 256;
+#ifndef KODR_ELIM_MC_MAX_BLOCKS  // (tuning builds only: more decoders per mc4 launch, the round-5 fault check)
+#define KODR_ELIM_MC_MAX_BLOCKS 256
+#endif
+constexpr int kElimMcMaxBlocks = KODR_ELIM_MC_MAX_BLOCKS;
 // workgroups per decoder of the multi-workgroup kernel a launch of G
 // decoders takes: ceil(k / 32) (gf_elim_mc / mc2), or one per 8 rows plus the
 // chain workgroup (mc4); and the most decoders one such launch takes

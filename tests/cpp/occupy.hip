@@ -28,6 +28,20 @@ void* kodr_test_stream_create(int device) {
   return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? (void*)s : nullptr;
 }
 
+// a stream at the device's highest priority (its own hardware queue pool)
+void* kodr_test_stream_create_high(int device) {
+  hipStream_t s = nullptr;
+  int least = 0, greatest = 0;
+  if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+    return nullptr;
+  return hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) == hipSuccess ? (void*)s : nullptr;
+}
+
+int kodr_test_stream_priority_range(int device, int* least, int* greatest) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  return hipDeviceGetStreamPriorityRange(least, greatest) == hipSuccess ? 0 : -1;
+}
+
 int kodr_test_stream_destroy(void* s) { return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : -1; }
 
 int kodr_test_stream_sync(void* s) { return hipStreamSynchronize((hipStream_t)s) == hipSuccess ? 0 : -1; }

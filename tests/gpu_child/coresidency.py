@@ -26,6 +26,7 @@ U8P = _lib._u8p
 def occupier():
     lib = ctypes.CDLL(os.path.join(ROOT, "tests", "cpp", "libkodr_occupy.so"))  # built by __graft_entry__.build()
     lib.kodr_test_stream_create.restype = ctypes.c_void_p
+    lib.kodr_test_stream_create_high.restype = ctypes.c_void_p
     lib.kodr_test_occupy.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int]
     lib.kodr_test_stream_sync.argtypes = [ctypes.c_void_p]
     lib.kodr_test_stream_destroy.argtypes = [ctypes.c_void_p]
@@ -42,10 +43,17 @@ def add(lib, hs, ds, k, pitch, L):
     return cons, sts
 
 
-def run():
+def run(own_priority=False):
+    """own_priority: the scenario's context runs on a stream of the device's
+    highest priority, created here (the condition INTEGRATION.md states: a
+    context's stream must not share a hardware queue with a foreign
+    long-running kernel)."""
     lib = _lib.lib()
-    ctx = device.Context(0)
     occ = occupier()
+    hs_stream = occ.kodr_test_stream_create_high(0) if own_priority else None
+    if own_priority:
+        assert hs_stream
+    ctx = device.Context(0, stream=hs_stream)
     k, L, G = 256, 256, 16
     rng = np.random.default_rng(99)
     pitch = (k + L + 15) // 16 * 16
@@ -111,6 +119,8 @@ def run():
         ctx.free(d)
     occ.kodr_test_stream_destroy(s2)
     ctx.close()
+    if hs_stream:
+        occ.kodr_test_stream_destroy(ctypes.c_void_p(hs_stream))
     return {"call_s": dt, "routes": routes, "ok": ok}
 
 

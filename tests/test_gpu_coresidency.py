@@ -105,7 +105,7 @@ def test_work_queued_ahead_does_not_start_the_give_up_clock():
         assert dt >= 0.015, dt  # it did wait for the queued work
         assert all(r["gpu"] == 1 and r["host_after_gpu"] == 0 for r in routes), routes
         for g in range(G):
-            assert cons[g] == k and sts[g] == 0
+            assert cons[g] == k and sts[g] in (0, 3)  # (3: the rows past k, kodr's ErrAllUsefulPiecesReceived)
             out = np.empty((k, L), np.uint8)
             errors.check(lib.rlnc_decoder_get_pieces(hs[g], out.ctypes.data_as(_lib._u8p)))
             assert np.array_equal(out, Ps[g])

@@ -135,9 +135,11 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
         hs.close()
 
 
-def test_bench_roundtrip_pipelined_exact(gpu_ctx):
+@pytest.mark.parametrize("overlap", ["elim", "elim_only", "copy", "get"])
+def test_bench_roundtrip_pipelined_exact(gpu_ctx, overlap):
     # The bench's pipelined round trip (the decoders on a context of their
-    # own; step i + 1's encode queued beside step i's GetPieces): a phase of
+    # own; step i + 1's encode queued beside step i's elimination -- from the
+    # AddPiece call's hook --, its twin copy or its GetPieces): a phase of
     # three steps over both vector sets, every decoded generation equal to the
     # original bytes after each step, no encode queued past the phase, every
     # decoder on the GPU route.
@@ -148,7 +150,7 @@ def test_bench_roundtrip_pipelined_exact(gpu_ctx):
                             rng=np.random.default_rng(0x5EEE), nvec=2, keep_data=True)
     dctx = device.Context(0)
     rt = bench.RoundTripStep(gpu_ctx, L_, errors, hs.encs, 256, 131072, np.random.default_rng(0x7F), nsets=2,
-                             dctx=dctx)
+                             dctx=dctx, overlap=overlap)
     r0 = dctx.elim_stats()
     try:
         assert rt.pipelined

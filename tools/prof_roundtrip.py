@@ -79,27 +79,32 @@ def main():
         out["legs"][name] = e
         return sel[first + count - 1][0]
 
-    # the round trip's encodes: warmup (a pipelined warmup queues one more
-    # than its steps), the timed steps, then bench's encode_alone launches
+    # the round trip's launches in order: the pipelined warmup (which queues
+    # one encode more than its steps) and timed steps, then -- when the line
+    # is pipelined -- the same round trip in series (legs.serial_warmup_steps
+    # untimed, then the timed steps whose events make `legs`)
     wenc = rt.get("warmup_encodes_run", n_warm)
-    reps = line["roofline"].get("launches_timed", 0)
+    nws = legs.get("serial_warmup_steps", 0)
+    pip = line["config"].get("pipelined", False)
+    pis = legs.get("pipelined_in_step", {})
     enc_sel = of_plan(rows, legs["encode_launch"]["plan"])
     get_sel = of_plan(rows, legs["get_pieces_call"]["plan"])
-    leg("roundtrip_encode", enc_sel, legs["encode_launch"]["avg_us"], macs=G * n * k * L, first=wenc)
-    leg("roundtrip_get_pieces", get_sel, legs["get_pieces_call"]["avg_us"], macs=G * k * k * L)
-    if reps:
-        leg("encode_alone", enc_sel, legs["encode_launch"].get("alone_us"), macs=G * n * k * L, first=wenc + steps,
-            count=reps)
-        # (get_alone: one untimed GetPieces after its AddPiece, then the timed ones)
-        leg("get_pieces_alone", get_sel, legs["get_pieces_call"].get("alone_us"), macs=G * k * k * L,
-            first=n_warm + steps + 1, count=reps)
     elim = [r for r in rows if "gf_elim_mc" in r[1] and r[3] == G]
-    leg("roundtrip_elimination", elim, None, macs=G * k ** 3)
     twin = [r for r in rows if "copy_bitslice" in r[1]]
-    leg("roundtrip_rows_twin", twin, None, hbm=G * 2 * n * L)
+    ser_enc = wenc + steps + nws if pip else wenc
+    ser = n_warm + steps + nws if pip else n_warm
+    leg("roundtrip_encode", enc_sel, legs["encode_launch"]["avg_us"], macs=G * n * k * L, first=ser_enc)
+    leg("roundtrip_get_pieces", get_sel, legs["get_pieces_call"]["avg_us"], macs=G * k * k * L, first=ser)
+    leg("roundtrip_elimination", elim, None, macs=G * k ** 3, first=ser)
+    leg("roundtrip_rows_twin", twin, None, hbm=G * 2 * n * L, first=ser)
+    if pip:
+        leg("pipelined_encode", enc_sel, pis.get("encode_launch", {}).get("avg_us"), macs=G * n * k * L, first=wenc)
+        leg("pipelined_get_pieces", get_sel, pis.get("get_pieces_call", {}).get("avg_us"), macs=G * k * k * L)
+        leg("pipelined_elimination", elim, None, macs=G * k ** 3)
+        leg("pipelined_rows_twin", twin, None, hbm=G * 2 * n * L)
     # the encode leg (bench.py's second timed phase): its own warmup count
     enc = line["encode"]["roofline"]
-    last_rt = max((r[0] for r in enc_sel[:wenc + steps + reps]), default=0)
+    last_rt = max((r[0] for r in enc_sel[:ser_enc + steps]), default=0)
     sel = of_plan(rows, enc["plan"], after=last_rt)
     w = enc["warmup_launches"]
     if len(sel) >= w + steps:
@@ -113,7 +118,7 @@ def main():
     else:
         out["legs"]["encode_B32"] = {"error": f"{len(sel)} launches, expected {w + steps}"}
     out["roofline_frac_bench"] = line["roofline"]["frac"]
-    rte = out["legs"].get("encode_alone" if reps else "roundtrip_encode", {})
+    rte = out["legs"].get("roundtrip_encode", {})
     if "rocprof_avg_us" in rte:
         out["roofline_frac_from_rocprof"] = rte["issue_frac_from_rocprof"]
     with open(a.out, "w") if a.out else sys.stdout as f:
