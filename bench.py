@@ -394,6 +394,16 @@ class RoundTripStep:
         if self.pipelined:
             self.dctx.wait(e[1])              # the decoders' stream reads the rows this encode wrote
         ahead = self.pipelined and (self.limit is None or i + 1 < self.limit)
+        if self.pipelined and self.overlap in ("elim", "elim_only"):
+            # the elimination needs all of its workgroups resident at once:
+            # launched into a GPU still running the previous step's GetPieces
+            # (or this step's encode) it starts behind them, and the next
+            # encode queued by the hook takes the CUs first -- measured, its
+            # 16 x 8 workgroups then took 1.45 ms instead of 0.16.  So the
+            # call starts on an idle GPU (one host wait per step), and the
+            # hook's encode fills the CUs the elimination leaves.
+            self.dctx.synchronize()
+            self.ctx.synchronize()
         ta0 = time.perf_counter()
         cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
         if ahead and self.overlap in ("elim", "elim_only"):
@@ -538,6 +548,7 @@ def roundtrip_kernels(rt, k, L):
     enc_macs, get_macs, elim_macs = G * n * k * L, G * k * k * L, G * k ** 3
     return {
         "encode_launch": {"kernel": "gf_bs_kernel (grouped, B = k + 2 per generation)", "avg_us": round(te * 1e6, 2),
+                          "split_tail_rows": n % 8 if n >= 64 and n % 8 in (1, 2) else 0,
                           "us_per_generation": round(te / G * 1e6, 2),
                           "gf_macs_per_s": float(f"{enc_macs / te:.4g}"),
                           "issue_frac": round(enc_macs / te / VALU_FLOOR_MACS_PER_S, 4),

@@ -243,6 +243,28 @@ def group_run(ctx, gens, count, V, out_pitch=None, expect=0, prepare=False):
     return rows[:, :, :L]
 
 
+@pytest.mark.parametrize("G,k,L,count,prepare", [(3, 64, 4096, 66, True), (2, 64, 4096, 65, True),
+                                                  (2, 128, 8192, 130, False), (34, 32, 2048, 66, True),
+                                                  (2, 64, 4096, 67, True), (2, 64, 4096 + 16, 72, True)])
+def test_grouped_encode_split_tail(gpu_ctx, G, k, L, count, prepare):
+    # a grouped bit-sliced batch of 8m + 1 or 8m + 2 pieces (the round trip's
+    # k + 2) hands its tail rows to the grouped gf_gemm launch over the plain
+    # rows (capi.cpp group_encode); 67 and 72 keep the whole batch in the
+    # bit-sliced launch; the plan reported is the bit-sliced launch's; 34
+    # generations span two launches of each kind; every piece against the oracle
+    rng = np.random.default_rng(G * 7 + k + count)
+    gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
+    V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
+    V[0, count - 1] = 0                       # a zero vector in the tail codes the zero piece
+    V[-1, count - 2, :] = 0
+    V[-1, count - 2, 3] = 1                   # a unit vector in the tail codes piece 3 itself
+    got = group_run(gpu_ctx, gens, count, V, out_pitch=L + 32, prepare=prepare)
+    plan = _lib.last_launch_plan()
+    assert plan["kernel"] == 2, plan
+    for g in range(G):
+        assert np.array_equal(got[g], oracle.encode(gens[g], V[g])), g
+
+
 @pytest.mark.parametrize("G,k,L,count", [(1, 16, 4096, 1), (3, 16, 4096 + 16, 2), (5, 100, 8192 + 48, 1),
                                          (8, 256, 65536, 4), (40, 32, 1024, 1), (33, 64, 2048, 8),
                                          (6, 64, 4096, 12), (4, 20, 1000, 3), (35, 64, 2048, 9),

@@ -23,13 +23,23 @@ G, k, L = line["config"]["generations_per_step"], line["config"]["piece_count"],
 n = k + 2
 
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from rt_roles import get_ids  # noqa: E402
+
+
 def vals(sub, counter):
-    v = []
+    """the counter per encode launch (GetPieces may share the grid: tools/rt_roles.py)"""
+    rows = {}
     for f in glob.glob(os.path.join(out, sub, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "gf_bs_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter and int(r["Grid_Size"]) == grid:
-                v.append(float(r["Counter_Value"]))
-    return v
+            key = (int(r["Dispatch_Id"]), int(r["Grid_Size"]))
+            kind = "bs" if "gf_bs_kernel" in r["Kernel_Name"] else "copy" if "copy_bitslice" in r["Kernel_Name"] else ""
+            rows.setdefault(key, [kind, None])
+            if r["Counter_Name"] == counter:
+                rows[key][1] = float(r["Counter_Value"])
+    keys = sorted(rows)
+    gets = get_ids(keys, lambda x: x[1] if rows[x][0] == "bs" else None, lambda x: rows[x][0] == "copy", lambda x: x)
+    return [rows[x][1] for x in keys if rows[x][0] == "bs" and x[1] == grid and x not in gets and rows[x][1] is not None]
 
 
 fetch, write = vals("fetch", "FETCH_SIZE"), vals("write", "WRITE_SIZE")

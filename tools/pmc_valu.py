@@ -34,22 +34,32 @@ legs = line["roofline"]["legs"]
 G, k, L = line["config"]["generations_per_step"], line["config"]["piece_count"], line["config"]["piece_size"]
 
 per = collections.defaultdict(dict)
+kind = {}
 for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "gf_bs_kernel" not in r["Kernel_Name"]:
+        key = (int(r["Dispatch_Id"]), int(r["Grid_Size"]))
+        kind[key] = ("bs" if "gf_bs_kernel" in r["Kernel_Name"] else
+                     "copy" if "copy_bitslice" in r["Kernel_Name"] else "other")
+        if kind[key] != "bs":
             continue
-        key = (r["Dispatch_Id"], int(r["Grid_Size"]))
         per[key][r["Counter_Name"]] = float(r["Counter_Value"])
         if r.get("Start_Timestamp") and r.get("End_Timestamp"):
             per[key]["us"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+# GetPieces and the encode's bit-sliced launch may share a grid (tools/rt_roles.py)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from rt_roles import get_ids  # noqa: E402
+getset = get_ids(sorted(kind), lambda x: x[1] if kind[x] == "bs" else None, lambda x: kind[x] == "copy",
+                 lambda x: x)
 
 out = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT of "
                  "bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline (tools/gpu_r6_val.sh)",
        "simds": SIMDS, "cycles_per_wave64_valu": 2, "nominal_clock_hz": NOMINAL_HZ}
-for leg, macs in (("encode_launch", G * (k + 2) * k * L), ("get_pieces_call", G * k * k * L)):
+enc_rows = k + 2 - legs["encode_launch"].get("split_tail_rows", 0)  # the bit-sliced launch's rows
+for leg, macs in (("encode_launch", G * enc_rows * k * L), ("get_pieces_call", G * k * k * L)):
     plan = legs[leg]["plan"]
     grid = plan["workgroups"] * 64 * plan["waves"] * plan["generations"]
-    vs = [v for (disp, g), v in per.items() if g == grid and "SQ_INSTS_VALU" in v]
+    want_get = leg == "get_pieces_call"
+    vs = [v for key, v in per.items() if key[1] == grid and "SQ_INSTS_VALU" in v and (key in getset) == want_get]
     if not vs:
         continue
     med = {c: statistics.median(v[c] for v in vs if c in v)

@@ -20,6 +20,7 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import bench  # noqa: E402
 
 
@@ -87,12 +88,27 @@ def main():
     nws = legs.get("serial_warmup_steps", 0)
     pip = line["config"].get("pipelined", False)
     pis = legs.get("pipelined_in_step", {})
-    enc_sel = of_plan(rows, legs["encode_launch"]["plan"])
-    get_sel = of_plan(rows, legs["get_pieces_call"]["plan"])
+    # (with the split tail the encode's bit-sliced launch and GetPieces are one
+    # kernel instance on one grid: tools/rt_roles.py tells them apart by order)
+    from rt_roles import get_ids
+    gget = of_plan(rows, legs["get_pieces_call"]["plan"])
+    gset = {id(r) for r in gget}
+    gets = get_ids(rows, lambda r: r[2] if id(r) in gset else None, lambda r: "copy_bitslice" in r[1], id)
+    enc_sel = [r for r in of_plan(rows, legs["encode_launch"]["plan"]) if id(r) not in gets]
+    get_sel = [r for r in gget if id(r) in gets]
     elim = [r for r in rows if "gf_elim_mc" in r[1] and r[3] == G]
     twin = [r for r in rows if "copy_bitslice" in r[1]]
     ser_enc = wenc + steps + nws if pip else wenc
     ser = n_warm + steps + nws if pip else n_warm
+    # the encode call = its bit-sliced launch + the split tail's gf_gemm launch
+    # (the first gf_gemm_kernel to start after it): durations summed
+    tail = legs["encode_launch"].get("split_tail_rows", 0)
+    if tail:
+        gemms = [r for r in rows if "gf_gemm_kernel" in r[1]]
+        def with_tail(r):
+            nxt = next((g for g in gemms if g[0] >= r[0] + r[4] * 1e3), None)
+            return (r[0], r[1], r[2], r[3], r[4] + (nxt[4] if nxt else 0.0))
+        enc_sel = [with_tail(r) for r in enc_sel]
     leg("roundtrip_encode", enc_sel, legs["encode_launch"]["avg_us"], macs=G * n * k * L, first=ser_enc)
     leg("roundtrip_get_pieces", get_sel, legs["get_pieces_call"]["avg_us"], macs=G * k * k * L, first=ser)
     leg("roundtrip_elimination", elim, None, macs=G * k ** 3, first=ser)

@@ -1,0 +1,23 @@
+"""Which gf_bs_kernel launches of the round trip are GetPieces and which are
+encodes (shared by prof_roundtrip.py, pmc_roundtrip.py, pmc_valu.py).
+
+Since round 6 the round trip's encode hands its two tail rows to gf_gemm and
+runs 256 rows on the same kernel instance and grid as GetPieces, so the grid
+no longer tells them apart.  Order does: GetPieces of a step starts (or is
+dispatched) after that step's twin copy (copy_bitslice_*), and it is the
+first launch of its grid to do so; the encodes are the rest (a pipelined
+step's next encode starts beside the elimination, before the copy)."""
+
+
+def get_ids(seq, grid_of, is_copy, key):
+    """seq: launches in start (or dispatch) order; grid_of(x): the launch's
+    grid or None if it is not a gf_bs_kernel launch; is_copy(x): a twin copy;
+    key(x): an id.  Returns {(grid, ...)}: the ids of the GetPieces launches."""
+    gets, armed = set(), False
+    for x in seq:
+        if is_copy(x):
+            armed = True
+        elif armed and grid_of(x) is not None:
+            gets.add(key(x))
+            armed = False
+    return gets
