@@ -548,7 +548,6 @@ def roundtrip_kernels(rt, k, L):
     enc_macs, get_macs, elim_macs = G * n * k * L, G * k * k * L, G * k ** 3
     return {
         "encode_launch": {"kernel": "gf_bs_kernel (grouped, B = k + 2 per generation)", "avg_us": round(te * 1e6, 2),
-                          "split_tail_rows": n % 8 if n >= 64 and n % 8 in (1, 2) else 0,
                           "us_per_generation": round(te / G * 1e6, 2),
                           "gf_macs_per_s": float(f"{enc_macs / te:.4g}"),
                           "issue_frac": round(enc_macs / te / VALU_FLOOR_MACS_PER_S, 4),

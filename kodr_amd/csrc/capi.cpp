@@ -428,12 +428,7 @@ static size_t group_bs_min() {
   static const size_t v = kodr_amd::tune_env("KODR_GROUP_BS_MIN") ? (size_t)atol(kodr_amd::tune_env("KODR_GROUP_BS_MIN")) : kGroupBsMinRows;
   return v;
 }
-// grouped bit-sliced launches hand a one- or two-row tail to gf_gemm
-// (KODR_SPLIT_TAIL=0 keeps it in the bit-sliced launch: A/B measurements)
-static bool split_tail_enabled() {
-  static const bool v = kodr_amd::tune_env("KODR_SPLIT_TAIL") ? atoi(kodr_amd::tune_env("KODR_SPLIT_TAIL")) != 0 : true;
-  return v;
-}
+
 
 namespace {
 
@@ -469,36 +464,20 @@ int group_encode(rlnc_encoder* const* encs, size_t n_enc, const uint8_t* dA, siz
     for (size_t i = 0; i < n_enc; i++)
       if (!encs[i]->compact)
         TRY(build_twin(ctx, encs[i]->pieces.p, encs[i]->pieces_bs, encs[i]->bs_valid, k, e0->pitch, L));
-    // A batch of 8m + 1 or 8m + 2 pieces (the round trip's k + 2) leaves the
-    // bit-sliced launch a last 8-row group with one or two real rows, which
-    // costs a whole group's tables, jumps and a round of resident waves:
-    // 16 x 258 pieces took 104.7 us per generation against 93.3 for 256
-    // (profiles/r06/bounds/).  Those rows go to the grouped v_perm launch over
-    // the plain rows instead (one more streaming read of each generation,
-    // ~6 us), the rest to the bit-sliced launch.  Same bytes.
-    size_t tail = count % 8;
-    bool plain = (e0->pitch % 16) == 0 && k * e0->pitch < kMaxDescBytes && (ldy % 16) == 0;
-    for (size_t i = 0; i < n_enc && plain; i++) plain = !encs[i]->compact;
-    if (!(count >= 64 && (tail == 1 || tail == 2) && plain && split_tail_enabled())) tail = 0;
-    const size_t main_rows = count - tail;
+    // (a batch of 8m + 1 or 8m + 2 pieces -- the round trip's k + 2 -- pays a
+    // whole last 8-row group for its one or two tail rows: 16 x 258 pieces
+    // 103-108 us per generation against 93-98 for 256.  Handing the tail to a
+    // launch of its own -- the grouped v_perm kernel over the plain rows, or a
+    // second bit-sliced launch that splits K over a workgroup's waves -- and
+    // every plan's KW were measured no faster: the tail's launch must stream
+    // the whole generation from HBM again (profiles/r06/split_tail/, r06/kw/).)
     const uint8_t* xs[kodr_amd::kGemmGroupMax];
     for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
       const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
       for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces_bs.p;
       const kodr_amd::GemmGroupArgs grp{(int)n, xs, a_stride, y_stride};
-      HIPC(kodr_amd::gf_gemm_bs(dA + g0 * a_stride, lda, main_rows, k, xs[0], e0->pitch, dY + g0 * y_stride, ldy,
-                                L, ctx->device, ctx->stream, false, &grp));
-    }
-    if (tail) {
-      const kodr_amd::LaunchPlan keep = kodr_amd::last_launch_plan();  // the plan callers pin: the main launch
-      for (size_t g0 = 0; g0 < n_enc; g0 += kodr_amd::kGemmGroupMax) {
-        const size_t n = std::min<size_t>(kodr_amd::kGemmGroupMax, n_enc - g0);
-        for (size_t i = 0; i < n; i++) xs[i] = encs[g0 + i]->pieces.p;
-        const kodr_amd::GemmGroupArgs grp{(int)n, xs, a_stride, y_stride};
-        HIPC(kodr_amd::gf_gemm(dA + g0 * a_stride + main_rows * lda, lda, tail, k, xs[0], e0->pitch,
-                               dY + g0 * y_stride + main_rows * ldy, ldy, L, ctx->stream, nullptr, false, &grp));
-      }
-      kodr_amd::last_launch_plan() = keep;
+      HIPC(kodr_amd::gf_gemm_bs(dA + g0 * a_stride, lda, count, k, xs[0], e0->pitch, dY + g0 * y_stride, ldy, L,
+                                ctx->device, ctx->stream, false, &grp));
     }
     return RLNC_OK;
   }

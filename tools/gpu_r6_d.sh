@@ -13,7 +13,7 @@ ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "stop: rc $rc at $2
 timeout -k 10 600 python -u -m pytest -v --timeout 200 --timeout-method thread -m gpu \
   tests/test_gpu_headline.py > $O/pytest_headline.log 2>&1; ok $? pytest
 grep -E "FAIL|ERROR" $O/pytest_headline.log | head; tail -1 $O/pytest_headline.log
-for s in 1 0 1 0; do
+for s in 2 0 1 2 0 1; do
   KODR_RLNC_LIB=kodr_amd/ab_modes/libkodr_rlnc.so KODR_SPLIT_TAIL=$s timeout -k 10 200 python -u tools/group_bs_time.py 258 256 \
     > $O/split_$s.log 2>&1; ok $? split_$s
   echo "split $s: $(tail -1 $O/split_$s.log | cut -c1-300)"
