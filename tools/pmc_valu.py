@@ -54,8 +54,7 @@ getset = get_ids(sorted(kind), lambda x: x[1] if kind[x] == "bs" else None, lamb
 out = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT of "
                  "bench.py --steps 20 --warmup 5 --no-extras --no-cpu-baseline (tools/gpu_r6_val.sh)",
        "simds": SIMDS, "cycles_per_wave64_valu": 2, "nominal_clock_hz": NOMINAL_HZ}
-enc_rows = k + 2 - legs["encode_launch"].get("split_tail_rows", 0)  # the bit-sliced launch's rows
-for leg, macs in (("encode_launch", G * enc_rows * k * L), ("get_pieces_call", G * k * k * L)):
+for leg, macs in (("encode_launch", G * (k + 2) * k * L), ("get_pieces_call", G * k * k * L)):
     plan = legs[leg]["plan"]
     grid = plan["workgroups"] * 64 * plan["waves"] * plan["generations"]
     want_get = leg == "get_pieces_call"

@@ -100,15 +100,6 @@ def main():
     twin = [r for r in rows if "copy_bitslice" in r[1]]
     ser_enc = wenc + steps + nws if pip else wenc
     ser = n_warm + steps + nws if pip else n_warm
-    # the encode call = its bit-sliced launch + the split tail's gf_gemm launch
-    # (the first gf_gemm_kernel to start after it): durations summed
-    tail = legs["encode_launch"].get("split_tail_rows", 0)
-    if tail:
-        gemms = [r for r in rows if "gf_gemm_kernel" in r[1]]
-        def with_tail(r):
-            nxt = next((g for g in gemms if g[0] >= r[0] + r[4] * 1e3), None)
-            return (r[0], r[1], r[2], r[3], r[4] + (nxt[4] if nxt else 0.0))
-        enc_sel = [with_tail(r) for r in enc_sel]
     leg("roundtrip_encode", enc_sel, legs["encode_launch"]["avg_us"], macs=G * n * k * L, first=ser_enc)
     leg("roundtrip_get_pieces", get_sel, legs["get_pieces_call"]["avg_us"], macs=G * k * k * L, first=ser)
     leg("roundtrip_elimination", elim, None, macs=G * k ** 3, first=ser)

@@ -1,9 +1,10 @@
 """Which gf_bs_kernel launches of the round trip are GetPieces and which are
 encodes (shared by prof_roundtrip.py, pmc_roundtrip.py, pmc_valu.py).
 
-Since round 6 the round trip's encode hands its two tail rows to gf_gemm and
-runs 256 rows on the same kernel instance and grid as GetPieces, so the grid
-no longer tells them apart.  Order does: GetPieces of a step starts (or is
+When the round trip's encode and GetPieces launch the same kernel instance on
+the same grid (a plan choice: the encode of k + 2 rows takes KW = 4 today,
+GetPieces of k rows the direct plan), the grid cannot tell them apart.  Order
+does: GetPieces of a step starts (or is
 dispatched) after that step's twin copy (copy_bitslice_*), and it is the
 first launch of its grid to do so; the encodes are the rest (a pipelined
 step's next encode starts beside the elimination, before the copy)."""
