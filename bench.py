@@ -394,19 +394,19 @@ class RoundTripStep:
         if self.pipelined:
             self.dctx.wait(e[1])              # the decoders' stream reads the rows this encode wrote
         ahead = self.pipelined and (self.limit is None or i + 1 < self.limit)
-        if self.pipelined and self.overlap in ("elim", "elim_only"):
-            # the elimination needs all of its workgroups resident at once:
-            # launched into a GPU still running the previous step's GetPieces
-            # (or this step's encode) it starts behind them, and the next
-            # encode queued by the hook takes the CUs first -- measured, its
-            # 16 x 8 workgroups then took 1.45 ms instead of 0.16.  So the
-            # call starts on an idle GPU (one host wait per step), and the
-            # hook's encode fills the CUs the elimination leaves.
+        if self.pipelined and self.overlap == "elim_sync":
+            # the elimination needs all of its workgroups resident at once: an
+            # encode dispatched ahead of them takes the CUs first (measured,
+            # 16 x 8 workgroups then took 1.45 ms instead of 0.16).  The
+            # library calls the hook only once the work ahead of the launch on
+            # the decoders' stream (the previous GetPieces) is done; this
+            # variant also starts the call on an idle GPU (one host wait per
+            # step: the gap between GetPieces and the next elimination)
             self.dctx.synchronize()
             self.ctx.synchronize()
         ta0 = time.perf_counter()
         cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
-        if ahead and self.overlap in ("elim", "elim_only"):
+        if ahead and self.overlap in ("elim", "elim_sync", "elim_only"):
             # step i + 1's encode queued from inside the AddPiece call, right
             # after the elimination's launch: it runs beside the elimination
             # (on the CUs its workgroups leave free) and the twin copy
@@ -425,11 +425,11 @@ class RoundTripStep:
         ta1 = time.perf_counter()
         self.dctx.record(e[2])
         if ahead:
-            if self.overlap not in ("elim", "elim_only"):
+            if self.overlap not in ("elim", "elim_sync", "elim_only"):
                 en = self._events(i + 1, timed)
                 self._encode(i + 1, en)        # beside this step's twin copy (and GetPieces)
             self.ahead = (i + 1, en)
-            if self.overlap in ("copy", "elim", "elim_only"):
+            if self.overlap in ("copy", "elim", "elim_sync", "elim_only"):
                 self.dctx.wait(en[1])          # GetPieces after it: two bit-sliced launches side by side lose
         errors.check(L_.rlnc_decoders_get_pieces_device(darr, G, self.dO, L))
         self.dctx.record(e[3])
@@ -586,7 +586,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the secondary measurements")
-    ap.add_argument("--overlap", choices=("elim", "elim_only", "copy", "get"), default="elim",
+    ap.add_argument("--overlap", choices=("elim", "elim_sync", "elim_only", "copy", "get"), default="elim",
                     help="pipelined round trip: what step i + 1's encode runs beside (RoundTripStep)")
     ap.add_argument("--serial-roundtrip", action="store_true",
                     help="encoders and decoders on one context (stream): no encode of step i + 1 beside step i's "

@@ -325,13 +325,16 @@ int rlnc_decoder_add_pieces_gpu(rlnc_decoder* dec, const uint8_t* d_rows, size_t
 int rlnc_decoders_add_pieces_gpu(rlnc_decoder* const* decs, size_t G, const uint8_t* const* d_rows,
                                  const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                  int* status);
-/* The same, calling after_launch(user) once from inside the call right after
- * the first elimination launch is on its way (or, when no batch goes to the
- * GPU, before returning), while the call still waits for the result: a
- * caller queues its own independent work on another context's stream there
- * (e.g. the next batch's encode), so that it runs beside the elimination on
- * the CUs the elimination's workgroups leave free -- queued before, it could
- * hold the CUs those workgroups need to be resident together.  The hook may
+/* The same, calling after_launch(user) once from inside the call after the
+ * first elimination launch is queued and the work queued ahead of it on the
+ * context's stream has completed (the launch is being dispatched; or, when
+ * no batch goes to the GPU, before returning), while the call still waits for
+ * the result: a caller queues its own independent work on another context's
+ * stream there (e.g. the next batch's encode), so that it runs beside the
+ * elimination on the CUs the elimination's workgroups leave free -- queued
+ * earlier, it could hold the CUs those workgroups need to be resident
+ * together.  The caller therefore need not wait for its earlier work on this
+ * context (e.g. the previous batch's GetPieces) before the call.  The hook may
  * return a hipEvent_t (or NULL): the rest of the call's work on this
  * context's stream (the received rows' copies) is then ordered behind it.
  * The hook must not call into this context. */

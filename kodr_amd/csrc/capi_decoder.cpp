@@ -830,15 +830,26 @@ int rlnc_decoders_add_pieces_gpu_hook(rlnc_decoder* const* ds, size_t G, const u
                                       const size_t* counts, size_t pitch, size_t piece_len, size_t* consumed,
                                       int* status, rlnc_hook_fn after_launch, void* user) {
   if (!ds || !rows || !counts || !consumed || !status || !G) return RLNC_ERR_INVALID_ARGUMENT;
-  // the caller's hook, once: right after the first elimination launch, else on the way out
+  // the caller's hook, once: after the first elimination launch, once the
+  // work queued ahead of it on the context stream has completed (`ready`), so
+  // that the launch's workgroups are dispatched before anything the hook
+  // queues on other streams can take their CUs; else on the way out
   bool hooked = after_launch == nullptr;
   hipEvent_t hook_ev = nullptr;  // what the hook asked this call's later work to wait for
-  auto run_hook = [&] {
-    if (hooked) return;
+  auto run_hook = [&](hipEvent_t ready) -> int {
+    if (hooked) return RLNC_OK;
     hooked = true;
+    hipError_t q = hipSuccess;
+    for (unsigned spins = 0; ready && (q = hipEventQuery(ready)) == hipErrorNotReady;)
+      if (++spins < 4096)
+        _mm_pause();
+      else
+        std::this_thread::yield();
     hook_ev = static_cast<hipEvent_t>(after_launch(user));
+    HIPC(q == hipErrorNotReady ? hipSuccess : q);
+    return RLNC_OK;
   };
-  auto hook_guard = on_scope_exit([&] { run_hook(); });
+  auto hook_guard = on_scope_exit([&] { (void)run_hook(nullptr); });
   rlnc_ctx* ctx = ds[0] ? ds[0]->ctx : nullptr;
   if (!ctx) return RLNC_ERR_NO_DEVICE;
   const size_t k = ds[0]->core.piece_count();
@@ -1041,7 +1052,7 @@ int rlnc_decoders_add_pieces_gpu_hook(rlnc_decoder* const* ds, size_t G, const u
     // (the first launch starts right behind rows_ready; a later one behind the launch before it)
     if (direct && c0 > 0) HIPC(hipEventRecord(ctx->elim_ready, ctx->stream));
     HIPC(kodr_amd::gf_elim(a, (int)nc, ctx->stream));
-    run_hook();
+    TRY(run_hook(c0 == 0 ? ctx->rows_ready : direct ? ctx->elim_ready : nullptr));
     if (hook_ev) {
       HIPC(hipStreamWaitEvent(ctx->stream, hook_ev, 0));  // the copies (context stream) after the caller's work
       hook_ev = nullptr;

@@ -135,7 +135,7 @@ def test_bench_roundtrip_step_exact(gpu_ctx):
         hs.close()
 
 
-@pytest.mark.parametrize("overlap", ["elim", "elim_only", "copy", "get"])
+@pytest.mark.parametrize("overlap", ["elim", "elim_sync", "elim_only", "copy", "get"])
 def test_bench_roundtrip_pipelined_exact(gpu_ctx, overlap):
     # The bench's pipelined round trip (the decoders on a context of their
     # own; step i + 1's encode queued beside step i's elimination -- from the
