@@ -1019,14 +1019,20 @@ __device__ __forceinline__ uint32_t mc3_block_update_c(const uint4* tab, uint32_
   return mc3_dot8x(tab, acc, fw + 2, &rp[8][col0 + d], 64);
 }
 
-// The circular-form inversion ((t, d) layout as mc3_gj_circ), branch-free:
-// the candidates are a ballot of f != 0 under an SGPR mask of the unpicked
-// rows' lanes (t, 0); the row's own tables (of f) are read right after f,
-// beside the pivot path (ballot -> s_ff1 -> v_readlane of dp -> uniform read
-// of inv(dp)'s tables, and ds_bpermute of the pivot row); every row then
-// computes both the pivot's and a non-pivot row's new value and selects.
-__device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, uint32_t P, int lane, uint32_t* s_val,
-                                          int* s_row) {
+// The circular-form inversion ((t, d) layout as mc3_gj_circ), branch-free
+// in the common case.  The pivot of column c is the lowest unpicked row whose
+// entry is non-zero; the step guesses the lowest unpicked row (its lane is
+// known from the SGPR candidate mask before the step) and reads its entry dp
+// with one v_readlane of P, then the uniform read of inv(dp)'s tables and the
+// ds_bpermute of the pivot row go out at once; only when dp is zero (1 in
+// 256) does it take the ballot of f != 0 under the mask (the same rule, so
+// the same pivots).  The row's own tables (of f) are read right after f,
+// beside the pivot path; every row computes both the pivot's and a non-pivot
+// row's new value and selects.  (Before round 6 the ballot -> s_ff1 ->
+// v_readlane of dp ran on every step: 5,258 against 4,927 cycles per panel,
+// tools/probe/chain_probe.hip, profiles/r06/chain/.)
+__device__ __forceinline__ bool mc3_gj(const uint4* tab, const uint4* itab, uint32_t P, int lane, uint32_t* s_val,
+                                       int* s_row) {
   const int t = lane >> 2, d = lane & 3;
   uint64_t cand = 0x1111111111111111ull;
   uint64_t pinv = 0;  // nibble tp = the slot (column) row tp pivoted: SALU only
@@ -1037,19 +1043,27 @@ __device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, u
     const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
     const uint4 tf = tab[2 * f];
     const uint32_t tf2 = tab[2 * f + 1].x;
-    const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
-    fail |= m == 0;
-    const int pl = (int)__builtin_ctzll(m | (1ull << 60));  // a failed column picks lane 60 (result unused)
+    int pl = (int)__builtin_ctzll(cand);
+    uint32_t dp = (__builtin_amdgcn_readlane(P, pl + cd) >> cb) & 0xffu;
+    uint4 ti = itab[2 * dp];
+    uint32_t ti2 = itab[2 * dp + 1].x;
+    uint32_t Pp = bperm(P, pl + d);
+    if (__builtin_expect(dp == 0u, 0)) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
+      fail |= m == 0;
+      pl = (int)__builtin_ctzll(m | (1ull << 60));  // a failed column picks lane 60 (result unused)
+      dp = __builtin_amdgcn_readlane(f, pl);
+      ti = itab[2 * dp];
+      ti2 = itab[2 * dp + 1].x;
+      Pp = bperm(P, pl + d);
+    }
     const int tp = pl >> 2;
     cand &= ~(1ull << pl);
     pinv |= (uint64_t)c << (4 * tp);
-    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
-    const uint4 ti = itab[2 * dp];
-    const uint32_t ti2 = itab[2 * dp + 1].x;
-    const uint32_t Pp = bperm(P, pl + d);
     const uint32_t inv = (ti.x >> 8) & 0xffu;
     const uint32_t Q = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp)) ^ (d == cd ? inv << cb : 0u);
-    const uint32_t upd = P ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
+    uint32_t upd = P ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
+    asm volatile("" : "+v"(upd));  // (on every lane: not sunk into an exec-masked branch)
     P = t == tp ? Q ^ (d == cd ? 1u << cb : 0u) : upd;
   }
   // S row c = the slots of row pi(c) with output byte j from slot pi^-1(j) =
@@ -1267,7 +1281,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
             MC2_STAMP(4 * p + 2);
             uint32_t sval = 0;
             int srow = 0;
-            const bool inv_ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
+            const bool inv_ok = mc3_gj(lds.tab, lds.itab, blk, lane, &sval, &srow);
             if (inv_ok) {
               lds.sp[slot][srow][d] = sval;
               mc_put(base + 16 * 64 + srow * 4 + d, tag, sval);
@@ -1397,7 +1411,7 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
 //  * the chain workgroup (blockIdx.x = NP): wave 1 stages MB_p and R_{p-1}'s
 //    panel-p columns (both as of p - 2) into LDS as they appear; wave 0 updates
 //    the block with S_{p-1} (two 16-term products, mc4_block_update), inverts
-//    it (mc3_gj_v5) and publishes S_p.
+//    it (mc3_gj) and publishes S_p.
 // The row data the chain needs for panel p leaves the row workgroups one
 // panel earlier (after apply(p - 2)), so the chain waits on them only when a
 // row workgroup's hand-off and apply take longer than one chain step.
@@ -1669,7 +1683,7 @@ __global__ __launch_bounds__(kMc4Threads) void gf_elim_mc4_kernel(ElimArgs args)
           MC4_STAMP(16 + p);
           uint32_t sval = 0;
           int srow = 0;
-          if (!mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow)) {
+          if (!mc3_gj(lds.tab, lds.itab, blk, lane, &sval, &srow)) {
             mc_set_fail(&lds.fail, mc_singular_why(blk, lane, p, k));
             break;
           }

@@ -409,6 +409,198 @@ __device__ __forceinline__ uint32_t mc3_block_update_b(const uint4* tab, uint32_
 
 
 
+// ---- the library's inversion before round 6 (ballot on every step) ----
+// The circular-form inversion ((t, d) layout as mc3_gj_circ), branch-free:
+// the candidates are a ballot of f != 0 under an SGPR mask of the unpicked
+// rows' lanes (t, 0); the row's own tables (of f) are read right after f,
+// beside the pivot path (ballot -> s_ff1 -> v_readlane of dp -> uniform read
+// of inv(dp)'s tables, and ds_bpermute of the pivot row); every row then
+// computes both the pivot's and a non-pivot row's new value and selects.
+__device__ __forceinline__ bool mc3_gj_v5(const uint4* tab, const uint4* itab, uint32_t P, int lane, uint32_t* s_val,
+                                          int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint64_t cand = 0x1111111111111111ull;
+  uint64_t pinv = 0;  // nibble tp = the slot (column) row tp pivoted: SALU only
+  bool fail = false;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
+    fail |= m == 0;
+    const int pl = (int)__builtin_ctzll(m | (1ull << 60));  // a failed column picks lane 60 (result unused)
+    const int tp = pl >> 2;
+    cand &= ~(1ull << pl);
+    pinv |= (uint64_t)c << (4 * tp);
+    const uint32_t dp = __builtin_amdgcn_readlane(f, pl);
+    const uint4 ti = itab[2 * dp];
+    const uint32_t ti2 = itab[2 * dp + 1].x;
+    const uint32_t Pp = bperm(P, pl + d);
+    const uint32_t inv = (ti.x >> 8) & 0xffu;
+    const uint32_t Q = gmul4(ti, ti2, sel0(Pp), sel1(Pp), sel2(Pp)) ^ (d == cd ? inv << cb : 0u);
+    const uint32_t upd = P ^ gmul4(tf, tf2, sel0(Q), sel1(Q), sel2(Q));
+    P = t == tp ? Q ^ (d == cd ? 1u << cb : 0u) : upd;
+  }
+  // S row c = the slots of row pi(c) with output byte j from slot pi^-1(j) =
+  // nibble j of pinv; row t pivoted column nibble t
+  uint32_t selA = 0, selB = 0, mskA = 0;
+  const uint32_t pq = (uint32_t)(pinv >> (16 * d));  // nibbles 4d .. 4d + 3: this lane's output bytes
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t sl = (pq >> (4 * b)) & 15u;
+    selA |= (sl & 7u) << (8 * b);
+    selB |= (sl & 7u) << (8 * b);
+    mskA |= sl < 8 ? 0xffu << (8 * b) : 0u;
+  }
+  const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
+  *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
+  *s_row = (int)((pinv >> (4 * t)) & 15u);
+  return !fail;
+}
+
+// ---- division-free, guessed pivot (round 6: slower, more VALU per step) ----
+// The same inversion (same pivots, same S), division-free, with the pivot
+// row guessed before its column is known.  mc3_gj_v5's step waits on a
+// chain of ballot -> s_ff1 -> v_readlane -> inverse tables -> Q -> Q's
+// selectors -> the row update; here:
+//  * the pivot is the lowest unpicked row when its entry a in column c is
+//    non-zero (255 in 256; otherwise the ballot picks, as in v5, so the pivots
+//    are v5's), its lane known from the SGPR candidate mask before the step:
+//    a = one v_readlane of the previous step's P;
+//  * no row is normalized: a non-pivot row becomes a x row ^ f x pivot row,
+//    the pivot row stays, so the update needs a's tables (one uniform LDS
+//    read) and the row's own tables of f (gathered beside it), and its
+//    selectors are ready before a is;
+//  * slot c (T's column pi(c) from now on) takes f x s on a non-pivot row and
+//    s on the pivot row, s = the product of the pivots so far (the implicit
+//    T[t][t] of every unpicked row, which every step scaled by its pivot);
+//  * a row's scale dsc = its own pivot times every later one; at the end one
+//    gather of inv(dsc)'s tables normalizes it: the slots equal v5's.
+__device__ __forceinline__ bool mc3_gj_v6(const uint4* tab, const uint4* itab, uint32_t P, int lane, uint32_t* s_val,
+                                          int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint64_t cand = 0x1111111111111111ull;
+  uint64_t pinv = 0;
+  bool fail = false;
+  uint32_t s = 1u, dsc = 1u;  // bytes
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t s0 = sel0(P), s1 = sel1(P), s2 = sel2(P);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    int pl = (int)__builtin_ctzll(cand);
+    uint32_t a = (__builtin_amdgcn_readlane(P, pl + cd) >> cb) & 0xffu;
+    if (a == 0u) {  // the lowest unpicked row has a zero: v5's rule
+      const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
+      fail |= m == 0;
+      pl = (int)__builtin_ctzll(m | (1ull << 60));  // a failed column picks lane 60 (result unused)
+      a = __builtin_amdgcn_readlane(f, pl);
+    }
+    const int tp = pl >> 2;
+    cand &= ~(1ull << pl);
+    pinv |= (uint64_t)c << (4 * tp);
+    const uint4 ta = tab[2 * a];
+    const uint32_t ta2 = tab[2 * a + 1].x;
+    const uint32_t Pp = bperm(P, pl + d);
+    const uint32_t X = d == cd ? Pp ^ (s << cb) : Pp;  // slot c: a ^ s, so that a x f ^ f x (a ^ s) = f x s
+    uint32_t upd = gmul4(ta, ta2, s0, s1, s2) ^ gmul4(tf, tf2, sel0(X), sel1(X), sel2(X));
+    uint32_t dup = gmul4(ta, ta2, sel0(dsc), sel1(dsc), sel2(dsc));
+    // (computed on every lane: left to itself the compiler sinks them into
+    // exec-masked branches around the selects, which serialize the step)
+    asm volatile("" : "+v"(upd), "+v"(dup));
+    const bool piv = t == tp;
+    P = piv ? (d == cd ? P ^ ((a ^ s) << cb) : P) : upd;
+    dsc = piv ? a : dup;
+    s = gmul4(ta, ta2, sel0(s), sel1(s), sel2(s));
+  }
+  {
+    const uint4 ti = itab[2 * dsc];
+    const uint32_t ti2 = itab[2 * dsc + 1].x;
+    P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
+  }
+  uint32_t selA = 0, selB = 0, mskA = 0;
+  const uint32_t pq = (uint32_t)(pinv >> (16 * d));
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t sl = (pq >> (4 * b)) & 15u;
+    selA |= (sl & 7u) << (8 * b);
+    selB |= (sl & 7u) << (8 * b);
+    mskA |= sl < 8 ? 0xffu << (8 * b) : 0u;
+  }
+  const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
+  *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
+  *s_row = (int)((pinv >> (4 * t)) & 15u);
+  return !fail;
+}
+
+// mc3_gj_v6 with the guessed pivot's loads (a's tables, the pivot row) issued
+// before the zero check (the rare fallback reloads them); RB: the pivot row
+// by four v_readlane and a select instead of ds_bpermute
+template <bool RB>
+__device__ __forceinline__ bool mc3_gj_v7(const uint4* tab, const uint4* itab, uint32_t P, int lane, uint32_t* s_val,
+                                          int* s_row) {
+  const int t = lane >> 2, d = lane & 3;
+  uint64_t cand = 0x1111111111111111ull;
+  uint64_t pinv = 0;
+  bool fail = false;
+  uint32_t s = 1u, dsc = 1u;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int cd = c >> 2, cb = 8 * (c & 3);
+    const uint32_t s0 = sel0(P), s1 = sel1(P), s2 = sel2(P);
+    const uint32_t f = (quad_bcast(P, cd) >> cb) & 0xffu;
+    const uint4 tf = tab[2 * f];
+    const uint32_t tf2 = tab[2 * f + 1].x;
+    int pl = (int)__builtin_ctzll(cand);
+    uint32_t a = (__builtin_amdgcn_readlane(P, pl + cd) >> cb) & 0xffu;
+    uint4 ta = tab[2 * a];
+    uint32_t ta2 = tab[2 * a + 1].x;
+    uint32_t Pp = RB ? row_bcast(P, pl >> 2, d) : bperm(P, pl + d);
+    if (__builtin_expect(a == 0u, 0)) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(f != 0u) & cand;
+      fail |= m == 0;
+      pl = (int)__builtin_ctzll(m | (1ull << 60));
+      a = __builtin_amdgcn_readlane(f, pl);
+      ta = tab[2 * a];
+      ta2 = tab[2 * a + 1].x;
+      Pp = RB ? row_bcast(P, pl >> 2, d) : bperm(P, pl + d);
+    }
+    const int tp = pl >> 2;
+    cand &= ~(1ull << pl);
+    pinv |= (uint64_t)c << (4 * tp);
+    const uint32_t X = d == cd ? Pp ^ (s << cb) : Pp;
+    uint32_t upd = gmul4(ta, ta2, s0, s1, s2) ^ gmul4(tf, tf2, sel0(X), sel1(X), sel2(X));
+    uint32_t dup = gmul4(ta, ta2, sel0(dsc), sel1(dsc), sel2(dsc));
+    asm volatile("" : "+v"(upd), "+v"(dup));
+    const bool piv = t == tp;
+    P = piv ? (d == cd ? P ^ ((a ^ s) << cb) : P) : upd;
+    dsc = piv ? a : dup;
+    s = gmul4(ta, ta2, sel0(s), sel1(s), sel2(s));
+  }
+  {
+    const uint4 ti = itab[2 * dsc];
+    const uint32_t ti2 = itab[2 * dsc + 1].x;
+    P = gmul4(ti, ti2, sel0(P), sel1(P), sel2(P));
+  }
+  uint32_t selA = 0, selB = 0, mskA = 0;
+  const uint32_t pq = (uint32_t)(pinv >> (16 * d));
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t sl = (pq >> (4 * b)) & 15u;
+    selA |= (sl & 7u) << (8 * b);
+    selB |= (sl & 7u) << (8 * b);
+    mskA |= sl < 8 ? 0xffu << (8 * b) : 0u;
+  }
+  const uint32_t w0 = quad_bcast(P, 0), w1 = quad_bcast(P, 1), w2 = quad_bcast(P, 2), w3 = quad_bcast(P, 3);
+  *s_val = (__builtin_amdgcn_perm(w1, w0, selA) & mskA) | (__builtin_amdgcn_perm(w3, w2, selB) & ~mskA);
+  *s_row = (int)((pinv >> (4 * t)) & 15u);
+  return !fail;
+}
+
 struct ProbeIn {  // one iteration's data (dwords)
   uint32_t mb[16][8];  // block rows: panel p - 1 columns (0-3), panel p columns (4-7)
   uint32_t sp[16][4];  // S_{p-1}
@@ -524,6 +716,10 @@ __global__ __launch_bounds__(1024) void chain_probe(const uint32_t* tables, cons
     else if (GJV == 3)
       ok = mc3_gj_circ(lds.tab, lds.itab, blk, lane, &sval, &srow);
     if (GJV == 5) ok = mc3_gj_v5(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    if (GJV == 6) ok = mc3_gj_v6(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    if (GJV == 7) ok = mc3_gj_v7<false>(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    if (GJV == 8) ok = mc3_gj_v7<true>(lds.tab, lds.itab, blk, lane, &sval, &srow);
+    if (GJV == 9) ok = mc3_gj(lds.tab, lds.itab, blk, lane, &sval, &srow);
     uint32_t Pr[4], Sr[4];
     if (GJV == 4) {  // (t, d) layout -> one row per lane, then the row-form inversion
 #pragma unroll
@@ -682,6 +878,10 @@ int main(int argc, char** argv) {
     run<2, 3>("pre-R update / circ gj", dtab, din, hin, iters, mode, dstats, dS);
     run<3, 5>("batched update / gj v5", dtab, din, hin, iters, mode, dstats, dS);
     run<4, 5>("batched-c update / gj v5", dtab, din, hin, iters, mode, dstats, dS);
+    run<4, 6>("batched-c update / gj v6", dtab, din, hin, iters, mode, dstats, dS);
+    run<4, 7>("batched-c update / gj v7", dtab, din, hin, iters, mode, dstats, dS);
+    run<4, 8>("batched-c update / gj v7 rb", dtab, din, hin, iters, mode, dstats, dS);
+    run<4, 9>("batched-c update / gj (lib)", dtab, din, hin, iters, mode, dstats, dS);
   }
   return 0;
 }
