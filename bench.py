@@ -704,10 +704,18 @@ def main():
         for leg in ("encode_launch", "get_pieces_call"):
             if pv and leg in pv:
                 q, t_leg = pv[leg], legs[leg]["avg_us"] * 1e-6
+                busy = round(q["valu_insts_per_launch"] * 2 / (1024 * 2.4e9 * t_leg), 4)
+                sp = q.get("serial_phase") or {}
                 legs[leg]["valu"] = {
                     "insts_per_launch": q["valu_insts_per_launch"],
-                    "busy_at_nominal_clock": round(q["valu_insts_per_launch"] * 2 / (1024 * 2.4e9 * t_leg), 4),
-                    "busy_at_measured_clock_pmc": q.get("valu_busy_at_measured_clock"),
+                    "busy_at_nominal_clock": busy,
+                    # the PMC pass's own launches of the same (serial) phase,
+                    # with their rocprof durations: the like-for-like check
+                    "busy_at_nominal_clock_pmc": sp.get("valu_busy_at_nominal_clock"),
+                    "line_over_pmc": (round(busy / sp["valu_busy_at_nominal_clock"], 4)
+                                      if sp.get("valu_busy_at_nominal_clock") else None),
+                    "busy_at_measured_clock_pmc": sp.get("valu_busy_at_measured_clock",
+                                                         q.get("valu_busy_at_measured_clock")),
                     "clock_ghz_pmc": q.get("clock_ghz"),
                     "source": pmc_valu_file(G, k, L)}
 

@@ -53,5 +53,5 @@ print(json.dumps({
     "write_size_kb_per_launch": round(statistics.mean(write), 1),
     "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
     "compulsory_bytes_per_launch": compulsory, "traffic_over_compulsory": round((rd + wr) / compulsory, 4),
-    "source": "tools/gpu_r5_val.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE of bench.py --steps 20 "
+    "source": "tools/gpu_r6_val.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE of bench.py --steps 20 "
               "--warmup 5 --no-extras --no-cpu-baseline"}, indent=1))

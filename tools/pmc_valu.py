@@ -3,7 +3,8 @@
 gf_bs_kernel legs (the encode launch and the grouped GetPieces) from one
 rocprofv3 --pmc pass of the driver's bench command (SQ_INSTS_VALU
 SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT; no tracing domains), and
-the hardware VALU-busy fraction each implies:
+the hardware VALU-busy fraction each implies (over every launch, and over
+the serial phase's launches -- the ones the line's legs are timed on):
 
   SIMD-cycles of a launch  = 1,024 SIMDs x GRBM_GUI_ACTIVE / 8
                              (GRBM_GUI_ACTIVE sums the 8 XCDs' busy cycles,
@@ -32,6 +33,7 @@ d, bj = sys.argv[1], sys.argv[2]
 line = json.loads([x for x in open(bj) if x.startswith("{")][-1])
 legs = line["roofline"]["legs"]
 G, k, L = line["config"]["generations_per_step"], line["config"]["piece_count"], line["config"]["piece_size"]
+rt = line.get("roundtrip", {})
 
 per = collections.defaultdict(dict)
 kind = {}
@@ -58,12 +60,18 @@ for leg, macs in (("encode_launch", G * (k + 2) * k * L), ("get_pieces_call", G 
     plan = legs[leg]["plan"]
     grid = plan["workgroups"] * 64 * plan["waves"] * plan["generations"]
     want_get = leg == "get_pieces_call"
-    vs = [v for key, v in per.items() if key[1] == grid and "SQ_INSTS_VALU" in v and (key in getset) == want_get]
+    ordered = [(key, v) for key, v in sorted(per.items()) if key[1] == grid and "SQ_INSTS_VALU" in v and
+               (key in getset) == want_get]
+    vs = [v for _, v in ordered]
     if not vs:
         continue
     med = {c: statistics.median(v[c] for v in vs if c in v)
            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "GRBM_GUI_ACTIVE", "GRBM_COUNT", "us")
            if any(c in v for v in vs)}
+    # the serial phase the line's legs are timed in: every launch after the
+    # pipelined phase (its warmup encodes / steps and its timed steps)
+    n_pipe = (rt.get("warmup_encodes_run", 0) if not want_get else rt.get("warmup_steps_run", 0)) + line["steps"]
+    ser = [v for v in vs[n_pipe:] if "us" in v]
     e = {"plan": plan, "counter_grid_threads": grid, "launches": len(vs),
          "valu_insts_per_launch": int(med["SQ_INSTS_VALU"]), "salu_insts_per_launch": int(med.get("SQ_INSTS_SALU", 0)),
          "waves_per_launch": int(med.get("SQ_WAVES", 0)), "gf_macs_per_launch": macs,
@@ -76,5 +84,12 @@ for leg, macs in (("encode_launch", G * (k + 2) * k * L), ("get_pieces_call", G 
             e["pmc_launch_us"] = round(med["us"], 2)
             e["clock_ghz"] = round(med["GRBM_GUI_ACTIVE"] / 8 / (med["us"] * 1e3), 3)
             e["valu_busy_at_nominal_clock"] = round(med["SQ_INSTS_VALU"] * 2 / (SIMDS * NOMINAL_HZ * med["us"] * 1e-6), 4)
+    if ser:
+        us = statistics.median(v["us"] for v in ser)
+        e["serial_phase"] = {
+            "launches": len(ser), "pmc_launch_us": round(us, 2),
+            "valu_busy_at_nominal_clock": round(med["SQ_INSTS_VALU"] * 2 / (SIMDS * NOMINAL_HZ * us * 1e-6), 4),
+            "valu_busy_at_measured_clock": round(statistics.median(
+                v["SQ_INSTS_VALU"] * 2 / (SIMDS * v["GRBM_GUI_ACTIVE"] / 8) for v in ser if "GRBM_GUI_ACTIVE" in v), 4)}
     out[leg] = e
 print(json.dumps(out, indent=1))
