@@ -41,13 +41,17 @@ def test_elimination_beside_a_long_kernel_returns_early():
 
 
 
-def test_work_queued_ahead_does_not_start_the_give_up_clock():
+@pytest.mark.parametrize("hook", [False, True])
+def test_work_queued_ahead_does_not_start_the_give_up_clock(hook):
     """More than kElimGiveUp (5 ms) of work queued ahead of the launch on the
     context's own stream (the occupier, one workgroup for 20 ms, standing in
     for a large encode or the previous step's GetPieces) must not count
     against the launch: the give-up clock starts when the launch becomes
     eligible (capi_decoder.cpp elim_direct_wait, `ready`).  Every decoder
-    stays on the GPU route and equals the oracle."""
+    stays on the GPU route and equals the oracle.  hook: through
+    rlnc_decoders_add_pieces_gpu_hook, whose hook must run only once that
+    work is done (the launch is next on the device), not right after the
+    launch is queued."""
     if not os.path.exists(os.path.join(HERE, "cpp", "libkodr_occupy.so")):
         pytest.skip("test occupier not built (__graft_entry__.build)")
     import ctypes
@@ -98,8 +102,24 @@ def test_work_queued_ahead_does_not_start_the_give_up_clock():
         ctx.synchronize()
         assert occ.kodr_test_occupy(ctypes.c_void_p(ctx.stream), 1, 20.0, 1024) == 0
         t0 = time.perf_counter()
-        cons, sts = child.add(lib, hs, ds, k, pitch, L)
+        t_hook = []
+        if hook:
+            arr = (ctypes.c_void_p * G)(*[h.value for h in hs])
+            rws = (ctypes.c_void_p * G)(*ds)
+            counts = (ctypes.c_size_t * G)(*([k + 2] * G))
+            cons, sts = (ctypes.c_size_t * G)(), (ctypes.c_int * G)()
+
+            def _hook(_u):
+                t_hook.append(time.perf_counter())
+                return None
+            fn = _lib.HOOK_FN(_hook)
+            errors.check(lib.rlnc_decoders_add_pieces_gpu_hook(arr, G, rws, counts, pitch, L, cons, sts, fn, None))
+        else:
+            cons, sts = child.add(lib, hs, ds, k, pitch, L)
         dt = time.perf_counter() - t0
+        if hook:
+            assert len(t_hook) == 1
+            assert t_hook[0] - t0 >= 0.015, t_hook[0] - t0  # called once the occupier was done
         routes = [elim_stats(h) for h in hs]
         print(f"call {dt * 1e3:.2f} ms; routes {routes}")
         assert dt >= 0.015, dt  # it did wait for the queued work
