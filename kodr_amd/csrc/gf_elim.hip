@@ -1083,7 +1083,12 @@ __device__ __forceinline__ bool mc3_gj(const uint4* tab, const uint4* itab, uint
   return !fail;
 }
 
-__global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
+#ifdef KODR_MC2_WAVES_PER_EU  // (tuning builds only: mc2's register cap, tools/gpu_r6_i.sh)
+#define KODR_MC2_ATTR __attribute__((amdgpu_waves_per_eu(KODR_MC2_WAVES_PER_EU)))
+#else
+#define KODR_MC2_ATTR
+#endif
+__global__ __launch_bounds__(1024) KODR_MC2_ATTR void gf_elim_mc2_kernel(ElimArgs args) {
   __shared__ ElimMc2Lds lds;
   const int q = blockIdx.x, g = blockIdx.y, P = gridDim.x, NP = 2 * gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1190,7 +1195,10 @@ __global__ __launch_bounds__(1024) void gf_elim_mc2_kernel(ElimArgs args) {
         // share its CUs; capped at 96 (waves_per_eu 5, a few bytes spilled) with
         // the copies at 2 or 4 loads per lane, the round trip measured slower
         // (238-241 against 230-235, 235-236 against 228-230 us per generation,
-        // profiles/r04/var_ab/)
+        // profiles/r04/var_ab/); in the pipelined round trip (round 6, encode
+        // waves beside it) 96 VGPRs measured the same as 128 (3.336-3.355 ms
+        // per step both), 80 and 64 slower (3.39-3.48: spills),
+        // profiles/r06/mc2_vgpr/
 #pragma unroll 1
         for (int cb = 0; cb < 16; cb += kMc2ApplyCols) {
           uint32_t gw[4];  // the bytes of columns cb .. of each row's G (wave-uniform)
