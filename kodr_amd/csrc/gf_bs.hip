@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   // rows of its task, so there is no cross-wave fold; its accumulators leave
   // the asm in registers and are transposed and stored straight from there
   // (no 16 KiB LDS sum buffer, no barrier: 16 workgroups per CU fit)
-  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || MODE == 30 || MODE == 31 || MODE == 32 || MODE == 33 || MODE == 34 || MODE == 35 || MODE == 36 || MODE == 37) &&
+  constexpr bool DIRECT = KW == 1 && GRP && (MODE == 0 || (MODE >= 30 && MODE <= 38)) &&
                          (RP == 2 || RP == 3);
   // A direct launch whose grid is resident at once (<= 16 workgroups per CU
   // on 256 CUs: blocks L, L + 256, ... land on CU L mod 256) puts the row
@@ -506,6 +506,8 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
   }
   // XCD-aware order: the nrg row groups of one column chunk go to blocks
   // b, b+8, ... (one XCD) and re-read that chunk from its L2.  Speed only.
+  // (row groups past 32 in bands of 32, each band in this order over its own
+  // blocks, measured the same at B = 258: profiles/r06/tail/)
   const int b = blockIdx.x;
   const int rg = cm_rg >= 0 ? cm_rg : (b >> 3) % nrg;
   const int cx = cm_cx >= 0 ? cm_cx : (b / (8 * nrg)) * 8 + (b & 7);
@@ -521,6 +523,8 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
     return;
   }
   const int m0 = rg * kBsRows, kb = w * rpw;
+  if constexpr (MODE == 38)  // tuning: a last row group with fewer than 8 rows does nothing (wrong products)
+    if (m0 + kBsRows > M) return;
   // this wave's input rows: [kb, kb + nr), nr a multiple of the 8-row
   // program chunk (rows >= K read zero and have coefficient 0)
   const int kpad = (K + kBsChunk - 1) / kBsChunk * kBsChunk;
@@ -914,7 +918,7 @@ hipError_t bs_launch(const uint8_t* A, int lda, int M, int K, const uint8_t* X, 
     g.y_stride = group->y_stride;
     // gridDim.x is a multiple of 8, so the XCD order of each generation's
     // blocks is the single-generation one; the two-row ring (plain loop only)
-    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || (MODE >= 30 && MODE <= 37) ? 2 : KODR_BS_P;
+    constexpr int rp = MODE == 33 ? (KW == 1 ? 3 : 2) : MODE == 0 || (MODE >= 30 && MODE <= 38) ? 2 : KODR_BS_P;
     hipLaunchKernelGGL((gf_bs_kernel<KW, MODE, true, rp>), dim3(nb, group->n), dim3(64 * KW), lds_bytes, st, A,
                        lda, M, K, X, ldx, Y, ldy, ncols, rpw, ncx, nrg, bd->tgt, bd->thi, accum, g, BsSideK{});
     last_launch_plan() = LaunchPlan{2, kBsRows, KW, 1, rp, rpw, group->n, nb};
@@ -1144,6 +1148,7 @@ hipError_t gf_gemm_bs(const uint8_t* dA, size_t lda, size_t M, size_t K, const u
          : mode == 32 ? KODR_BS_CALL(KW_, 32) : mode == 33 ? KODR_BS_CALL(KW_, 33)           \
          : mode == 34 ? KODR_BS_CALL(KW_, 34) : mode == 35 ? KODR_BS_CALL(KW_, 35)           \
          : mode == 36 ? KODR_BS_CALL(KW_, 36) : mode == 37 ? KODR_BS_CALL(KW_, 37)           \
+         : mode == 38 ? KODR_BS_CALL(KW_, 38)                                                    \
                                                : KODR_BS_CALL(KW_, 0);
 #else
 #define KODR_BS_CASE(KW_) \

@@ -245,12 +245,16 @@ def group_run(ctx, gens, count, V, out_pitch=None, expect=0, prepare=False):
 
 @pytest.mark.parametrize("G,k,L,count,prepare", [(3, 64, 4096, 66, True), (2, 64, 4096, 65, True),
                                                   (2, 128, 8192, 130, False), (34, 32, 2048, 66, True),
-                                                  (2, 64, 4096, 67, True), (2, 64, 4096 + 16, 72, True)])
+                                                  (2, 64, 4096, 67, True), (2, 64, 4096 + 16, 72, True),
+                                                  (2, 64, 4096, 258, True), (3, 32, 2048 + 16, 300, True),
+                                                  (2, 32, 4096, 512, False), (2, 16, 2048, 520, True)])
 def test_grouped_encode_ragged_row_groups(gpu_ctx, G, k, L, count, prepare):
     # grouped bit-sliced batches of 8m + 1 / 8m + 2 pieces (the round trip's
     # k + 2: a last 8-row group with one or two real rows, zero and unit
     # vectors among them), 8m + 3 and 8m (67, 72), prepared and lazily built
-    # twins, 34 generations over two launches; every piece against the oracle
+    # twins, 34 generations over two launches; past 32 row groups the blocks
+    # go in bands of 32 (gf_bs.hip): 33, 38, 64 and 65 groups (258, 300, 512,
+    # 520 pieces); every piece against the oracle
     rng = np.random.default_rng(G * 7 + k + count)
     gens = [rng.integers(0, 256, (k, L), dtype=np.uint8) for _ in range(G)]
     V = rng.integers(0, 256, (G, count, k), dtype=np.uint8)
