@@ -774,10 +774,10 @@ bool DecoderCore::load_rref(const uint8_t* state, size_t pitch, size_t c) {
 bool DecoderCore::load_inverse(const uint8_t* tinv, size_t pitch) {
   const size_t k = k_;
   if (received_ != 0 || k < 2) return false;
-  pinv_.resize(k * k);
   if (pitch == k) {
-    memcpy(pinv_.data(), tinv, k * k);
+    pinv_.assign(tinv, tinv + k * k);  // (one pass: no zero fill before the copy)
   } else {
+    pinv_.resize(k * k);
     for (size_t i = 0; i < k; i++) memcpy(pinv_.data() + i * k, tinv + i * pitch, k);
   }
   pinv_on_ = true;
