@@ -150,6 +150,16 @@ __global__ __launch_bounds__(256) void copy_bitslice_kernel(const uint8_t* __res
 // work per byte counts: no division per item (the row and half-block advance
 // by the grid stride's quotient and remainder), half the butterfly per lane.
 constexpr int kCopyUnroll = 4;
+// The copy streams its rows and the twin past the caches (nontemporal loads
+// and stores: nothing of either is read again before it has left L2), so
+// beside the pipelined encode it leaves the encode's column chunks in L2:
+// the AddPiece leg alone 362-370 against 371-384 us, the pipelined step
+// 3.336-3.350 against 3.342-3.356 ms (tools/gpu_r6_m.sh, profiles/r06/copy_nt/).
+// KODR_COPY_NT=0 builds the cached variant (A/B).
+#ifndef KODR_COPY_NT
+#define KODR_COPY_NT 1
+#endif
+typedef uint32_t cp_u32x4 __attribute__((ext_vector_type(4)));
 
 // planes of the 32-byte block whose dwords d[0..3] are in the lower lane of a
 // pair and d[4..7] in the upper one: h = this lane's four, p = the partner's;
@@ -183,10 +193,15 @@ __device__ __forceinline__ void copy_bs_pair(const CopyGroup& g, int y, uint32_t
                          (uint32_t)__builtin_amdgcn_mov_dpp((int)a.z, 0xb1, 0xf, 0xf, false),
                          (uint32_t)__builtin_amdgcn_mov_dpp((int)a.w, 0xb1, 0xf, 0xf, false)};
   const size_t off = (size_t)r * dpitch + (size_t)hi * 16;
-  if (g.dst[y]) *reinterpret_cast<uint4*>(g.dst[y] + off) = a;  // (null: twin only)
   uint32_t h[4] = {a.x, a.y, a.z, a.w};
   bitslice32_half(h, p, (hi & 1) == 0);
+#if KODR_COPY_NT
+  if (g.dst[y]) __builtin_nontemporal_store(cp_u32x4{a.x, a.y, a.z, a.w}, reinterpret_cast<cp_u32x4*>(g.dst[y] + off));
+  __builtin_nontemporal_store(cp_u32x4{h[0], h[1], h[2], h[3]}, reinterpret_cast<cp_u32x4*>(g.dbs[y] + off));
+#else
+  if (g.dst[y]) *reinterpret_cast<uint4*>(g.dst[y] + off) = a;  // (null: twin only)
   *reinterpret_cast<uint4*>(g.dbs[y] + off) = make_uint4(h[0], h[1], h[2], h[3]);
+#endif
 }
 
 __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g, size_t spitch, size_t dpitch,
@@ -222,7 +237,14 @@ __global__ __launch_bounds__(256) void copy_bitslice_grouped_kernel(CopyGroup g,
       ru[u] = rr;
       hu[u] = hh;
       a[u] = make_uint4(0u, 0u, 0u, 0u);
+#if KODR_COPY_NT
+      if (rr < rows) {
+        const cp_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const cp_u32x4*>(g.src[y] + (size_t)rr * spitch + (size_t)hh * 16));
+        a[u] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+#else
       if (rr < rows) a[u] = *reinterpret_cast<const uint4*>(g.src[y] + (size_t)rr * spitch + (size_t)hh * 16);
+#endif
       step(rr, hh);
     }
 #pragma unroll
