@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round 6: the twin copy with streaming (nontemporal) loads and stores (now
-# the default; the cached variant is -DKODR_COPY_NT=0)
-# (-DKODR_COPY_NT=1, kodr_amd/ab_nt), so that it does not evict the encode's
-# column chunks from L2 beside the pipelined encode, against the shipped
-# build: the round-trip parity test on the A/B build, then the driver's bench
-# command (--no-extras), three interleaved reps; a kernel trace of each.
+# Round 6: the twin copy with streaming (nontemporal) loads and stores, so
+# that it does not evict the encode's column chunks from L2 beside the
+# pipelined encode.  As run: kodr_amd/ab_nt (built with -DKODR_COPY_NT=1)
+# against the shipped build of the time (cached copy); the streaming copy is
+# now the default and -DKODR_COPY_NT=0 builds the cached one.  The round-trip
+# parity test on the A/B build, then the driver's bench command (--no-extras),
+# three interleaved reps; a kernel trace of each.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
