@@ -161,6 +161,23 @@ constexpr int kCopyUnroll = 4;
 #endif
 typedef uint32_t cp_u32x4 __attribute__((ext_vector_type(4)));
 
+// one 32-byte block of a product's output rows.  KODR_BS_NT_STORE=1 streams
+// them past the caches: measured no faster (3.312-3.317 against 3.305-3.317 ms
+// per round-trip step), and the twin copy that reads the encode's rows next
+// then takes them from HBM (tools/gpu_r6_n.sh, profiles/r06/store_nt/)
+#ifndef KODR_BS_NT_STORE
+#define KODR_BS_NT_STORE 0
+#endif
+__device__ __forceinline__ void bs_store32(uint8_t* dst, const uint4& v0, const uint4& v1) {
+#if KODR_BS_NT_STORE
+  __builtin_nontemporal_store(cp_u32x4{v0.x, v0.y, v0.z, v0.w}, reinterpret_cast<cp_u32x4*>(dst));
+  __builtin_nontemporal_store(cp_u32x4{v1.x, v1.y, v1.z, v1.w}, reinterpret_cast<cp_u32x4*>(dst) + 1);
+#else
+  reinterpret_cast<uint4*>(dst)[0] = v0;
+  reinterpret_cast<uint4*>(dst)[1] = v1;
+#endif
+}
+
 // planes of the 32-byte block whose dwords d[0..3] are in the lower lane of a
 // pair and d[4..7] in the upper one: h = this lane's four, p = the partner's;
 // on return h = planes 0..3 (lower lane) or 4..7 (upper), as bitslice32 leaves
@@ -517,8 +534,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
           v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
           v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
         }
-        reinterpret_cast<uint4*>(dst)[0] = v0;
-        reinterpret_cast<uint4*>(dst)[1] = v1;
+        bs_store32(dst, v0, v1);
       } else {
         for (int i = 0; cc + i < ncols; i++)
           dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
@@ -763,8 +779,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
           v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
           v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
         }
-        reinterpret_cast<uint4*>(dst)[0] = v0;
-        reinterpret_cast<uint4*>(dst)[1] = v1;
+        bs_store32(dst, v0, v1);
       } else {
         for (int i = 0; cc + i < ncols; i++)
           dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
@@ -839,8 +854,7 @@ __global__ __launch_bounds__(64 * KW) __attribute__((amdgpu_waves_per_eu(512 / K
         v0 = make_uint4(v0.x ^ o0.x, v0.y ^ o0.y, v0.z ^ o0.z, v0.w ^ o0.w);
         v1 = make_uint4(v1.x ^ o1.x, v1.y ^ o1.y, v1.z ^ o1.z, v1.w ^ o1.w);
       }
-      reinterpret_cast<uint4*>(dst)[0] = v0;
-      reinterpret_cast<uint4*>(dst)[1] = v1;
+      bs_store32(dst, v0, v1);
     } else {
       for (int i = 0; cc + i < ncols; i++)
         dst[i] = (uint8_t)(d[i >> 2] >> (8 * (i & 3))) ^ (accum ? dst[i] : (uint8_t)0);
