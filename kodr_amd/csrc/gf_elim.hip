@@ -1083,6 +1083,14 @@ __device__ __forceinline__ bool mc3_gj(const uint4* tab, const uint4* itab, uint
   return !fail;
 }
 
+// the chain waves' sleep between hand-off polls: 8 and 32 measured the same
+// beside the pipelined encode (3.334-3.358 against 3.337-3.352 ms per step)
+// and alone (mc2 16 decoders 188.7 / 192.5 against 188.4 us), so the polls'
+// agent-scope traffic is not what slows the encode beside it
+// (tools/gpu_r6_p.sh, profiles/r06/poll_sleep/)
+#ifndef KODR_MC2_POLL_SLEEP
+#define KODR_MC2_POLL_SLEEP 2
+#endif
 #ifdef KODR_MC2_WAVES_PER_EU  // (tuning builds only: mc2's register cap, tools/gpu_r6_i.sh)
 #define KODR_MC2_ATTR __attribute__((amdgpu_waves_per_eu(KODR_MC2_WAVES_PER_EU)))
 #else
@@ -1329,7 +1337,7 @@ __global__ __launch_bounds__(1024) KODR_MC2_ATTR void gf_elim_mc2_kernel(ElimArg
               why = 2;
               break;
             }
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(KODR_MC2_POLL_SLEEP);
           }
           if (why) {
             mc_set_fail(&lds.fail, why);
